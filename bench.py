@@ -1,0 +1,159 @@
+"""Slide-encoder throughput benchmark (BASELINE.json metric) on 1..8 MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--tiles 70000]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+A step = one gigapath_slide_enc12l768d forward (bf16, inference) over one synthetic slide of
+--tiles tiles (default 70,000 = BASELINE config C3), inputs and weights resident in HBM.
+Multi-GPU: one process per GPU, each rank encodes its own slide (replicas, no data-path
+collective): value = tiles processed by all ranks / max-over-ranks wall time ("weak").
+Rank 0 prints ONE JSON line including the attention kernel's roofline (HIP events around
+every gp_dilated_attn_fwd launch in the timed region) and a CPU baseline (the fp32 oracle on
+a bounded sample of the same workload, timed on this host).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "prov-gigapath-replication_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "slide-encoder tiles/sec at 1/2/4/8 GPUs (12L768d LongNet); attn MFMA util %"
+ARCH = "gigapath_slide_enc12l768d"
+PEAK_BF16_TFLOPS = 2500.0     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-level table)
+PEAK_HBM_GBS = 8000.0
+
+
+def make_slide(n_tiles, seed=1, in_chans=1536, tile=256):
+    """Synthetic slide of SURVEY §8(d): N(0,1) tile embeddings, distinct raster-sorted grid cells."""
+    rx = np.random.Generator(np.random.PCG64(seed))
+    x = rx.standard_normal((1, n_tiles, in_chans), dtype=np.float32)
+    rc = np.random.Generator(np.random.PCG64(seed + 1))
+    side = max(int(math.ceil(math.sqrt(n_tiles / 0.7))), int(math.ceil(math.sqrt(n_tiles))))
+    cells = np.sort(rc.choice(side * side, size=n_tiles, replace=False))
+    coords = np.stack([cells // side, cells % side], -1).astype(np.float32)[None] * tile
+    return x, coords
+
+
+def cpu_baseline(n_tiles, threads):
+    """fp32 CPU oracle on a bounded sample: patch embed + pos add + ONE of the 12 encoder layers
+    of the same slide, extrapolated to the full 12-layer forward."""
+    import oracle
+    torch.set_num_threads(threads)
+    cfg = oracle.arch_config(ARCH)
+    W = {k: torch.from_numpy(v) for k, v in oracle.make_weights(cfg, seed=0).items()
+         if k.startswith(("patch_embed", "cls_token", "encoder.layers.0."))}
+    x, coords = make_slide(n_tiles)
+    with torch.no_grad():
+        t0 = time.perf_counter()
+        h = torch.nn.functional.linear(torch.from_numpy(x), W["patch_embed.proj.weight"], W["patch_embed.proj.bias"])
+        pos = oracle.coords_to_pos(coords)
+        h = h + torch.from_numpy(oracle.pos_embed_rows(pos, oracle.sincos_axis_table(768, 1000), 1000))
+        h = torch.cat([W["cls_token"].view(1, 1, 768), h], 1)
+        t1 = time.perf_counter()
+        oracle.encoder_layer(h, W, "encoder.layers.0", cfg["segment_length"], cfg["dilated_ratio"], 16)
+        t2 = time.perf_counter()
+    full = (t1 - t0) + cfg["depth"] * (t2 - t1)
+    return {"value": round(n_tiles / full, 2), "unit": "tiles/s", "cores": threads, "kind": "port",
+            "sample": "oracle fp32 torch-CPU: embed + 1 of 12 layers of the %d-tile slide (%.1f s), x12 layers "
+                      "extrapolated (%.1f s per forward)" % (n_tiles, t2 - t0, full)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--tiles", type=int, default=70000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    from gigapath import runtime, slide_encoder
+    model = slide_encoder.create_model("", ARCH, 1536).to(dev).eval()
+    model.validate_positions = True
+    x, coords = make_slide(args.tiles, seed=1 + rank)
+    xt = torch.from_numpy(x).to(dev)
+    ct = torch.from_numpy(coords).to(dev)
+
+    def step():
+        return model(xt, ct, all_layer_embed=True)
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        runtime.TIMER.reset()
+        runtime.TIMER.enabled = True
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            out = step()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+        runtime.TIMER.enabled = False
+    elapsed = t1 - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    assert all(torch.isfinite(o).all() for o in out)
+
+    kt = runtime.TIMER.totals_ms()
+    segs = model.encoder.layers[0].self_attn.args.segment_length
+    ratios = model.encoder.layers[0].self_attn.args.dilated_ratio
+    L = args.tiles + 1
+    att_flops_launch = runtime.attention_valid_flops(L, segs, ratios, 16, 48)
+    n_att, ms_att = kt.get("attn", (0, 0.0))
+    avg_att_s = ms_att / max(n_att, 1) / 1e3
+    achieved = att_flops_launch / avg_att_s / 1e12 if avg_att_s > 0 else 0.0
+    gemm_tf = runtime.gemm_flops(1, args.tiles, 768, 3072, 1536, 12) / 1e12
+    total_tf = gemm_tf + 12 * att_flops_launch / 1e12
+    value = world * args.tiles * args.steps / elapsed
+    ms_step = elapsed / args.steps * 1e3
+    result = {
+        "metric": METRIC, "value": round(value, 2), "unit": "tiles/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic (PCG64 N(0,1) 1536-d tile embeddings, distinct grid coords; random-init weights)",
+        "config": {"workload": "C3: %s forward, one %d-tile slide per GPU, all_layer_embed=True"
+                               % (ARCH, args.tiles),
+                   "tiles_per_slide": args.tiles, "slides_per_gpu": 1, "parallelism": "replica x%d" % world},
+        "roofline": {"bound": "mfma", "kernel": "gp_dilated_attn_fwd", "achieved": round(achieved, 2),
+                     "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
+                     "traffic": None, "flops_per_launch": att_flops_launch, "avg_launch_ms": round(avg_att_s * 1e3, 4),
+                     "launches": n_att},
+        "attn_mfma_util_pct": round(100 * achieved / PEAK_BF16_TFLOPS, 2),
+        "model_tflops": round(total_tf * args.steps * world / elapsed, 2),
+        "kernel_ms_per_step": {k: round(v[1] / args.steps, 3) for k, v in sorted(kt.items())},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        result["cpu_baseline"] = cpu_baseline(args.tiles, threads)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,128 @@
+/*
+ * gigapath_hip.h — C ABI of the MI355X (gfx950) slide-encoder hot path.
+ *
+ * One shared library, libgigapath_hip.so, built with hipcc --offload-arch=gfx950.
+ * Conventions (all entry points):
+ *   - extern "C", plain pointers and sizes, no framework types.
+ *   - Every tensor pointer is a DEVICE pointer to caller-allocated, contiguous memory;
+ *     the library never allocates.  "bf16" buffers are uint16_t bit patterns.
+ *   - Work is enqueued on `stream` (a hipStream_t passed as void*; NULL = default stream)
+ *     and is stream-ordered; nothing synchronises the host.
+ *   - Return value: 0 = ok, GP_EARG (-1) = bad argument, otherwise a hipError_t.
+ *     gp_last_error_string() describes the last failure of the calling thread.
+ *   - No global mutable state; calls on distinct streams may run concurrently.
+ *
+ * Each entry cites the reference interface it replaces (paths relative to the reference
+ * repository root, qimingfan10/Prov-gigapath-replication).
+ */
+#ifndef GIGAPATH_HIP_H
+#define GIGAPATH_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GP_ABI_VERSION 1
+#define GP_EARG (-1)
+#define GP_MAX_BRANCHES 8
+
+/* ABI version of the loaded library (== GP_ABI_VERSION). */
+int gp_abi_version(void);
+
+/* Human-readable description of the calling thread's last error ("" if none). */
+const char* gp_last_error_string(void);
+
+/* Coordinates -> flat pos-embed index, bit-exact with
+ * LongNetViT.coords_to_pos (gigapath/slide_encoder.py:166-179):
+ *   pos = (int64)(floor(x / tile) * grid + floor(y / tile)) + 1, computed in the coords dtype.
+ * coords: [n_tiles, 2] float32 (coords_is_f64 = 0) or float64 (= 1).  pos: [n_tiles] int64.
+ * err_count (device int32, may be NULL) is incremented once per index outside the
+ * [-(grid*grid+1), grid*grid] range torch indexing of pos_embed accepts (slide_encoder.py:200). */
+int gp_coords_to_pos(const void* coords, int coords_is_f64, int64_t n_tiles, int grid,
+                     double tile_size, int64_t* pos, int32_t* err_count, void* stream);
+
+/* Patch-embed epilogue + 2-D sin-cos position add + CLS concat (slide_encoder.py:195-205,
+ * pos_embed.py:30-77) fused with the first pre-LN (encoder.py:126).
+ *   x_out[b, 0, :]   = cls                                  (pos_embed row 0 is zero)
+ *   x_out[b, 1+t, :] = xp[b, t, :] + [tab[(p-1) % G] | tab[(p-1) / G]],  p = pos[b, t]
+ *   ln_out           = LayerNorm(x_out; ln_w, ln_b, eps)    (skipped if ln_w == NULL)
+ * xp: [B, N, E] bf16 (patch projection incl. bias); tab: [G, E/2] fp32 one-axis sin-cos
+ * table (fp64-built); cls: [E] fp32; x_out: [B, N+1, E] fp32; ln_out: [B, N+1, E] bf16.
+ * E must be 64 * {12, 16, 24}. */
+int gp_posembed_cls_ln(const uint16_t* xp, const int64_t* pos, const float* tab, const float* cls,
+                       int64_t B, int64_t N, int E, int G, const float* ln_w, const float* ln_b,
+                       float eps, float* x_out, uint16_t* ln_out, void* stream);
+
+/* Dilated sparsify of one branch (DilatedAttention.gathering / dense_to_sparse,
+ * torchscale/component/dilated_attention.py:16-31, 76-98), bit-exact:
+ *   dst[((b*nseg + n)*H + h)*m + i, :] = src[b*L + n*s + i*r + h/(Hp/r), col_off + h*D + :]
+ *   or zeros where the reference pads (i*r + j >= s, or the token >= L).
+ * s = min(sl, L), nseg = ceil(L/s), m = ceil(s/r), Hp = H rounded up to a multiple of r.
+ * src: [B*L, row_stride] bf16; dst: [B*nseg*H*m, D] bf16.  D % 8 == 0. */
+int gp_dilated_gather(const uint16_t* src, int64_t row_stride, int64_t col_off, int64_t B, int64_t L,
+                      int H, int D, int sl, int r, uint16_t* dst, void* stream);
+
+/* All dilation branches of one DilatedAttention layer in ONE launch: the dilated gather is
+ * folded into the attention addressing, and zero-padded keys are added analytically
+ * (replaces gathering x3 + flash_attn_func per branch: dilated_attention.py:199-208,
+ * multihead_attention.py:97-107, flash_attention.py:13-16).
+ * q/k/v: [B*L, row_stride] bf16 (head h at columns h*D .. h*D+D-1 of each pointer; a fused
+ *   QKV buffer passes q = base, k = base + E, v = base + 2E, row_stride = 3E).
+ * Branch b (sl = seg_len[b], r = ratios[b]) writes
+ *   o_out[b]:   [B*nseg_b, m_b, H, D] bf16   (flash_attn's "out" layout per segment)
+ *   lse_out[b]: [B*nseg_b, H, m_b]    fp32   (natural-log LSE, flash_attn's softmax_lse)
+ * Rows whose values the merge can never read (beyond the last segment's tokens) are left
+ * unwritten.  softmax_scale <= 0 selects D^-0.5.  D in {48, 64, 96}. */
+int gp_dilated_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, int64_t row_stride,
+                        int64_t B, int64_t L, int H, int D, const int32_t* seg_len,
+                        const int32_t* ratios, int nbranch, uint16_t* const* o_out,
+                        float* const* lse_out, float softmax_scale, void* stream);
+
+/* Drop-in for the operator seam flash_attn_func(q, k, v, 0.0, None, scale, False)
+ * (torchscale/component/flash_attention.py:13-16): non-causal, no mask, dropout 0.
+ * q/k/v/o: [nbatch, seqlen, H, D] bf16 contiguous; lse: [nbatch, H, seqlen] fp32. */
+int gp_seg_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, int64_t nbatch,
+                    int64_t seqlen, int H, int D, float softmax_scale, uint16_t* o, float* lse,
+                    void* stream);
+
+/* Branch merge (DilatedAttention.scattering / sparse_to_dense, dilated_attention.py:33-53,
+ * 100-131) fused with inner_attn_ln (:212-213):
+ *   per (token p, head h): lse_b = covered ? lse_b[..] : -1e8, lse_b == 0 -> -1e8,
+ *   w_b = softmax_b(lse_b) in fp32, out = sum_b w_b * o_b, then LayerNorm over H*D
+ *   (skipped if ln_w == NULL).  Inputs are gp_dilated_attn_fwd's outputs.
+ * out: [B*L, H*D] bf16. */
+int gp_branch_merge_ln(const uint16_t* const* o_in, const float* const* lse_in,
+                       const int32_t* seg_len, const int32_t* ratios, int nbranch, int64_t B,
+                       int64_t L, int H, int D, const float* ln_w, const float* ln_b, float eps,
+                       uint16_t* out, void* stream);
+
+/* Residual add fused with the next pre-LN (encoder.py:141,147 / :159,126):
+ *   x += y + bias (fp32 residual stream, in place);  ln_out = LayerNorm(x) (skipped if ln_w == NULL).
+ * x: [rows, cols] fp32; y: [rows, cols] bf16 (GEMM output without bias); bias: [cols] fp32 or NULL;
+ * ln_out: [rows, cols] bf16.  cols = 64 * {12, 16, 24}. */
+int gp_residual_layernorm(float* x, const uint16_t* y, const float* bias, const float* ln_w,
+                          const float* ln_b, float eps, uint16_t* ln_out, int64_t rows, int cols,
+                          void* stream);
+
+/* FFN middle (feedforward_network.py:131-137): out = LayerNorm(gelu_erf(h)) in fp32.
+ * h, out: [rows, cols] bf16 (in place allowed); cols = 64 * {48, 64, 96}. */
+int gp_gelu_layernorm(const uint16_t* h, const float* ln_w, const float* ln_b, float eps,
+                      uint16_t* out, int64_t rows, int cols, void* stream);
+
+/* Plain fp32 LayerNorm over rows with a row stride (readout: encoder.py:387-388,
+ * slide_encoder.py:213-221).  out: [rows, cols] fp32 contiguous.  cols = 64 * {12, 16, 24}. */
+int gp_layernorm_f32(const float* x, int64_t row_stride, const float* ln_w, const float* ln_b,
+                     float eps, float* out, int64_t rows, int cols, void* stream);
+
+/* Global average pool (slide_encoder.py:215): out[b, :] = mean_{t >= start} x[b, t, :].
+ * x: [B, L, E] fp32; out: [B, E] fp32. */
+int gp_mean_tokens(const float* x, int64_t B, int64_t L, int E, int64_t start, float* out,
+                   void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GIGAPATH_HIP_H */

@@ -1,0 +1,483 @@
+// Dilated attention for gfx950: sparsify (gather), per-segment flash attention with MFMA,
+// and the LSE-weighted branch merge.  Replaces DilatedAttention.gathering / flash_attn_func /
+// scattering (torchscale/component/dilated_attention.py:16-131, flash_attention.py:13-16).
+//
+// Attention kernel design (one launch covers every branch of a layer):
+//   * work item = (branch, batch*segment, head, 128-row q-block); items ordered heaviest
+//     branch first (LPT) and regrouped so that 8 consecutive q-blocks of one (segment, head)
+//     run on one XCD and share its L2 for K/V;
+//   * 4 waves x 32 query rows; K/V tiles of 64 keys are register-staged into LDS, double
+//     buffered (one barrier per tile).  The dilated gather is folded into the addressing:
+//     sparse row i of (segment n, head h) is token n*s + i*r + h/(Hp/r);
+//   * S^T = K.Q^T with v_mfma_f32_16x16x32_bf16 (D padded to 32*KS with zero Q lanes), so
+//     each lane owns one query's scores: softmax needs only 2 cross-lane max steps per tile;
+//   * O^T += V^T.P^T with the same MFMA: P is taken straight from the S accumulators (no lane
+//     movement), V^T fragments come from ds_read_b64_tr_b16 on the row-major V tile;
+//   * the reference's zero-padded keys (dilated_attention.py:85-91, unmasked in flash-attn)
+//     are added analytically at the end: n_pad * exp(0 - max) in the denominator.
+#include <math.h>
+
+#include "gp_api.h"
+#include "gp_common.h"
+
+namespace {
+
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+struct AttnBranch {
+  GpBranch g;
+  int32_t nqb;          // q-blocks per (batch-segment, head)
+  int64_t item_begin;   // first work item of this branch
+  uint16_t* o;          // [B*nseg, m, H, D]
+  float* lse;           // [B*nseg, H, m]
+};
+
+struct AttnArgs {
+  const uint16_t* q;
+  const uint16_t* k;
+  const uint16_t* v;
+  int64_t row_stride;
+  int64_t L;
+  int32_t H;
+  int32_t nbranch;
+  float c_log2;         // softmax_scale * log2(e)
+  int64_t total_items;
+  AttnBranch br[GP_MAX_BRANCHES];   // work order (heaviest first)
+};
+
+constexpr int kWaves = 4;
+constexpr int kQT = 2;                       // 16-row q-tiles per wave
+constexpr int kQB = kWaves * kQT * 16;       // 128 query rows per workgroup
+constexpr int kKB = 64;                      // keys per K/V tile
+
+// Blocks b, b+8, b+16, ... share an XCD (round-robin dispatch).  Within each chunk of 64
+// blocks give the 8 blocks of one XCD 8 consecutive work items (same segment and head).
+GP_DEV int64_t xcd_group(int64_t bid, int64_t nb) {
+  const int64_t full = nb & ~int64_t(63);
+  if (bid >= full) return bid;
+  const int64_t base = bid & ~int64_t(63);
+  const int64_t in = bid & 63;
+  return base + (in & 7) * 8 + (in >> 3);
+}
+
+template <int D>
+__global__ __launch_bounds__(256, 2) void dilated_attn_kernel(const AttnArgs a) {
+  constexpr int KS = (D + 31) / 32;          // 32-deep k-steps of Q.K (zero-padded d)
+  constexpr int DT = D / 16;                 // 16-wide d tiles of P.V
+  constexpr int ROWB = D * 2;                // LDS bytes per K/V row
+  constexpr int TILEB = kKB * ROWB;
+  constexpr int CH = D / 8;                  // 16-byte chunks per row
+  constexpr int LPT = 2 * kKB * CH / 256;    // K+V chunks per thread per tile
+  static_assert((2 * kKB * CH) % 256 == 0, "tile must split evenly over 256 threads");
+  // [K0 | V0 | K1 | V1] + slack: the zero-weight d>=D lanes of the last K row read into V.
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILEB + 64];
+
+  const int64_t item = xcd_group(blockIdx.x, gridDim.x);
+  int bi = 0;
+#pragma unroll
+  for (int t = 1; t < GP_MAX_BRANCHES; ++t)
+    if (t < a.nbranch && item >= a.br[t].item_begin) bi = t;
+  const GpBranch g = a.br[bi].g;
+  int64_t local = item - a.br[bi].item_begin;
+  const int nqb = a.br[bi].nqb;
+  const int qb = (int)(local % nqb);
+  local /= nqb;
+  const int hh = (int)(local % a.H);
+  const int64_t bn = local / a.H;
+  const int64_t bidx = bn / g.nseg;
+  const int n = (int)(bn % g.nseg);
+  const int j = hh / g.hpg;
+  const int c = gp_valid_rows(g, a.L, n, j);
+  // Non-last segments: every sparse row can reach the output (incl. the r-pad row when
+  // s % r != 0, whose dense slot lands inside [0, L)).  Last segment: only valid rows can.
+  const int rows_needed = (n < g.nseg - 1) ? g.m : c;
+  const int q0 = qb * kQB;
+  if (q0 >= rows_needed) return;
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int l16 = lane & 15, g4 = lane >> 4;
+  const int64_t tok0 = bidx * a.L + (int64_t)n * g.s + j;     // token of sparse row 0
+  const int64_t rstride = (int64_t)g.r * a.row_stride;        // elements between sparse rows
+  const uint16_t* qbase = a.q + tok0 * a.row_stride + hh * D;
+  const uint16_t* kbase = a.k + tok0 * a.row_stride + hh * D;
+  const uint16_t* vbase = a.v + tok0 * a.row_stride + hh * D;
+
+  // ---- Q fragments (B operand of S^T = K.Q^T): lane holds Q[row l16][d = 32ks + 8g4 .. +7]
+  bf16x8 qf[kQT][KS];
+#pragma unroll
+  for (int qt = 0; qt < kQT; ++qt) {
+    const int i = q0 + w * 32 + qt * 16 + l16;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int d0 = ks * 32 + g4 * 8;
+      bf16x8 z = {};
+      if (i < c && d0 < D) z = *reinterpret_cast<const bf16x8*>(qbase + (int64_t)i * rstride + d0);
+      qf[qt][ks] = z;
+    }
+  }
+
+  // ---- K/V tile staging (global -> registers -> LDS), chunk u of this thread
+  uint4 stage[LPT];
+  auto load_tile = [&](int kv0) {
+#pragma unroll
+    for (int u = 0; u < LPT; ++u) {
+      const int idx = threadIdx.x + 256 * u;
+      const int tsel = idx / (kKB * CH);
+      const int rem = idx % (kKB * CH);
+      const int row = rem / CH, ch = rem % CH;
+      const int key = kv0 + row;
+      uint4 z = make_uint4(0, 0, 0, 0);
+      if (key < c) z = *reinterpret_cast<const uint4*>((tsel ? vbase : kbase) + (int64_t)key * rstride + ch * 8);
+      stage[u] = z;
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < LPT; ++u) {
+      const int idx = threadIdx.x + 256 * u;
+      const int tsel = idx / (kKB * CH);
+      const int rem = idx % (kKB * CH);
+      const int row = rem / CH, ch = rem % CH;
+      *reinterpret_cast<uint4*>(smem + (2 * buf + tsel) * TILEB + row * ROWB + ch * 16) = stage[u];
+    }
+  };
+
+  float m_run[kQT], l_run[kQT];
+  f32x4 oacc[kQT][DT];
+#pragma unroll
+  for (int qt = 0; qt < kQT; ++qt) {
+    m_run[qt] = -INFINITY;
+    l_run[qt] = 0.f;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) oacc[qt][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  const int ntiles = (c + kKB - 1) / kKB;
+  if (ntiles > 0) {
+    load_tile(0);
+    store_tile(0);
+  }
+  __syncthreads();
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int kv0 = t * kKB;
+    if (t + 1 < ntiles) load_tile(kv0 + kKB);
+    const char* Kb = smem + (2 * (t & 1)) * TILEB;
+    const char* Vb = Kb + TILEB;
+
+    // S^T[key][q] for 4 key sub-tiles of 16: lane holds keys 16kt + 4g4 + reg of query l16
+    f32x4 sacc[kQT][4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      bf16x8 kf[KS];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+        kf[ks] = *reinterpret_cast<const bf16x8*>(Kb + (kt * 16 + l16) * ROWB + ks * 64 + g4 * 16);
+#pragma unroll
+      for (int qt = 0; qt < kQT; ++qt) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[ks], qf[qt][ks], acc, 0, 0, 0);
+        sacc[qt][kt] = acc;
+      }
+    }
+    if (kv0 + kKB > c) {   // last partial tile: keys >= c are zero pads, handled analytically
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (kv0 + kt * 16 + g4 * 4 + r >= c)
+#pragma unroll
+            for (int qt = 0; qt < kQT; ++qt) sacc[qt][kt][r] = -INFINITY;
+    }
+
+    // online softmax (log2 domain), one query per lane; 4 lanes (g4) share a query
+    bf16x8 pf[kQT][2];
+#pragma unroll
+    for (int qt = 0; qt < kQT; ++qt) {
+      float mx = sacc[qt][0][0];
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, sacc[qt][kt][r]);
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mnew = fmaxf(m_run[qt], mx * a.c_log2);
+      const float alpha = exp2f(m_run[qt] - mnew);
+      m_run[qt] = mnew;
+      float ps = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = exp2f(fmaf(sacc[qt][kt][r], a.c_log2, -mnew));
+          sacc[qt][kt][r] = p;
+          ps += p;
+        }
+      l_run[qt] = l_run[qt] * alpha + ps;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) oacc[qt][dt] *= alpha;
+      // B operand of O^T += V^T.P^T: element e<4 = key 32u+4g4+e, e>=4 = key 32u+16+4g4+e-4
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          pf[qt][u][e] = (__bf16)sacc[qt][2 * u][e];
+          pf[qt][u][4 + e] = (__bf16)sacc[qt][2 * u + 1][e];
+        }
+    }
+
+    // O^T[d][q] += V^T[d][key] . P^T[key][q]; V^T fragment by transposed LDS reads
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const char* base = Vb + (32 * u + 4 * g4 + (l16 >> 2)) * ROWB + (16 * dt + 4 * (l16 & 3)) * 2;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + 16 * ROWB));
+        const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+        for (int qt = 0; qt < kQT; ++qt)
+          oacc[qt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qt][u], oacc[qt][dt], 0, 0, 0);
+      }
+    }
+
+    if (t + 1 < ntiles) store_tile((t + 1) & 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: analytic zero-pad keys, normalise, store O rows and LSE
+  const int npad = g.m - c;
+  AttnBranch br = a.br[bi];
+#pragma unroll
+  for (int qt = 0; qt < kQT; ++qt) {
+    float l = l_run[qt];
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    float mr = m_run[qt];
+    float so = 1.f;
+    if (npad > 0) {
+      const float mf = fmaxf(mr, 0.f);
+      so = exp2f(mr - mf);
+      l = l * so + (float)npad * exp2f(-mf);
+      mr = mf;
+    }
+    const float inv = so / l;
+    const int i = q0 + w * 32 + qt * 16 + l16;
+    if (i < rows_needed) {
+      uint16_t* orow = br.o + ((bn * g.m + i) * a.H + hh) * (int64_t)D;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        float vv[4] = {oacc[qt][dt][0] * inv, oacc[qt][dt][1] * inv, oacc[qt][dt][2] * inv, oacc[qt][dt][3] * inv};
+        store_bf16<4>(orow + 16 * dt + 4 * g4, vv);
+      }
+      if (g4 == 0) br.lse[(bn * a.H + hh) * (int64_t)g.m + i] = (mr + log2f(l)) * 0.69314718055994530942f;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+struct MergeBranch {
+  GpBranch g;
+  const uint16_t* o;
+  const float* lse;
+};
+
+struct MergeArgs {
+  int64_t B, L;
+  int32_t H, D, E, nbranch;
+  MergeBranch br[GP_MAX_BRANCHES];
+  const float* ln_w;
+  const float* ln_b;
+  float eps;
+  uint16_t* out;
+};
+
+template <int EPL>
+__global__ __launch_bounds__(256) void branch_merge_kernel(const MergeArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= a.B * a.L) return;
+  const int64_t bidx = row / a.L, p = row % a.L;
+  const int col0 = lane * EPL;
+  const int hh = col0 / a.D, dcol = col0 % a.D;
+
+  float lse[GP_MAX_BRANCHES];
+  int64_t off[GP_MAX_BRANCHES];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int b = 0; b < GP_MAX_BRANCHES; ++b) {
+    lse[b] = -1e8f;
+    off[b] = -1;
+    if (b < a.nbranch) {
+      const GpBranch g = a.br[b].g;
+      const int64_t n = p / g.g, t = p % g.g;
+      const int64_t i = t / g.r;
+      const int jj = (int)(t % g.r);
+      if (hh / g.hpg == jj) {   // sparse_to_dense: covered heads of this dense slot
+        const int64_t sn = bidx * g.nseg + n;
+        float v = a.br[b].lse[(sn * a.H + hh) * (int64_t)g.m + i];
+        lse[b] = (v == 0.f) ? -1e8f : v;      // dilated_attention.py:46
+        off[b] = ((sn * g.m + i) * a.H + hh) * (int64_t)a.D + dcol;
+      }
+      mx = fmaxf(mx, lse[b]);
+    }
+  }
+  float wsum = 0.f;
+#pragma unroll
+  for (int b = 0; b < GP_MAX_BRANCHES; ++b) {
+    if (b < a.nbranch) {
+      lse[b] = expf(lse[b] - mx);
+      wsum += lse[b];
+    }
+  }
+  float acc[EPL];
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) acc[e] = 0.f;
+#pragma unroll
+  for (int b = 0; b < GP_MAX_BRANCHES; ++b) {
+    if (b < a.nbranch && off[b] >= 0) {
+      const float wb = lse[b] / wsum;
+      float ov[EPL];
+      load_bf16<EPL>(a.br[b].o + off[b], ov);
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) acc[e] += ov[e] * wb;
+    }
+  }
+  if (a.ln_w != nullptr) wave_layernorm<EPL>(acc, a.E, a.ln_w, a.ln_b, a.eps, col0);
+  store_bf16<EPL>(a.out + row * a.E + col0, acc);
+}
+
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void dilated_gather_kernel(const uint16_t* __restrict__ src, int64_t row_stride,
+                                                             int64_t col_off, int64_t L, int H, int D, GpBranch g,
+                                                             int64_t total_rows, uint16_t* __restrict__ dst) {
+  const int CH = D / 8;
+  const int64_t id = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t row = id / CH;
+  if (row >= total_rows) return;
+  const int ch = (int)(id % CH);
+  const int i = (int)(row % g.m);
+  const int64_t t = row / g.m;
+  const int hh = (int)(t % H);
+  const int64_t bn = t / H;
+  const int64_t bidx = bn / g.nseg;
+  const int n = (int)(bn % g.nseg);
+  const int j = hh / g.hpg;
+  uint4 v = make_uint4(0, 0, 0, 0);
+  if (i < gp_valid_rows(g, L, n, j)) {
+    const int64_t tok = bidx * L + (int64_t)n * g.s + j + (int64_t)i * g.r;
+    v = *reinterpret_cast<const uint4*>(src + tok * row_stride + col_off + hh * D + ch * 8);
+  }
+  *reinterpret_cast<uint4*>(dst + row * D + ch * 8) = v;
+}
+
+}  // namespace
+
+// =========================================================================================
+extern "C" int gp_dilated_gather(const uint16_t* src, int64_t row_stride, int64_t col_off, int64_t B, int64_t L,
+                                 int H, int D, int sl, int r, uint16_t* dst, void* stream) {
+  GP_REQUIRE(B > 0 && L > 0 && H > 0 && D > 0 && sl > 0 && r > 0, "gp_dilated_gather: bad sizes");
+  GP_REQUIRE(D % 8 == 0 && row_stride % 8 == 0 && col_off % 8 == 0 && row_stride >= col_off + (int64_t)H * D,
+             "gp_dilated_gather: D, row_stride and col_off must be multiples of 8 elements");
+  GP_REQUIRE(src && dst && gp_aligned(src, 16) && gp_aligned(dst, 16), "gp_dilated_gather: pointers must be 16-byte aligned");
+  const GpBranch g = gp_make_branch(L, sl, r, H);
+  const int64_t rows = B * g.nseg * (int64_t)H * g.m;
+  const int64_t chunks = rows * (D / 8);
+  dilated_gather_kernel<<<(unsigned)((chunks + 255) / 256), 256, 0, gp_stream(stream)>>>(src, row_stride, col_off, L,
+                                                                                         H, D, g, rows, dst);
+  return gp_check_launch("gp_dilated_gather");
+}
+
+extern "C" int gp_dilated_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, int64_t row_stride,
+                                   int64_t B, int64_t L, int H, int D, const int32_t* seg_len, const int32_t* ratios,
+                                   int nbranch, uint16_t* const* o_out, float* const* lse_out, float softmax_scale,
+                                   void* stream) {
+  GP_REQUIRE(D == 48 || D == 64 || D == 96, "gp_dilated_attn_fwd: head dim %d unsupported (48, 64, 96)", D);
+  GP_REQUIRE(nbranch >= 1 && nbranch <= GP_MAX_BRANCHES, "gp_dilated_attn_fwd: nbranch must be 1..%d", GP_MAX_BRANCHES);
+  GP_REQUIRE(B > 0 && L > 0 && H > 0 && row_stride >= (int64_t)H * D && row_stride % 8 == 0,
+             "gp_dilated_attn_fwd: bad sizes");
+  GP_REQUIRE(q && k && v && seg_len && ratios && o_out && lse_out, "gp_dilated_attn_fwd: null pointer");
+  GP_REQUIRE(gp_aligned(q, 16) && gp_aligned(k, 16) && gp_aligned(v, 16), "gp_dilated_attn_fwd: q/k/v must be 16-byte aligned");
+  AttnArgs a;
+  a.q = q; a.k = k; a.v = v;
+  a.row_stride = row_stride;
+  a.L = L;
+  a.H = H;
+  a.nbranch = nbranch;
+  const float scale = softmax_scale > 0.f ? softmax_scale : 1.0f / sqrtf((float)D);
+  a.c_log2 = scale * 1.44269504088896340736f;
+  // order branches by keys per work item (descending) so the longest items start first
+  int order[GP_MAX_BRANCHES];
+  GpBranch geo[GP_MAX_BRANCHES];
+  for (int b = 0; b < nbranch; ++b) {
+    GP_REQUIRE(seg_len[b] > 0 && ratios[b] > 0, "gp_dilated_attn_fwd: branch %d has sl=%d r=%d", b, seg_len[b], ratios[b]);
+    GP_REQUIRE(o_out[b] && lse_out[b] && gp_aligned(o_out[b], 8), "gp_dilated_attn_fwd: branch %d output null/misaligned", b);
+    geo[b] = gp_make_branch(L, seg_len[b], ratios[b], H);
+    order[b] = b;
+  }
+  for (int x = 1; x < nbranch; ++x)
+    for (int y = x; y > 0 && geo[order[y]].m > geo[order[y - 1]].m; --y) {
+      int tmp = order[y]; order[y] = order[y - 1]; order[y - 1] = tmp;
+    }
+  int64_t items = 0;
+  for (int x = 0; x < nbranch; ++x) {
+    const int b = order[x];
+    AttnBranch& e = a.br[x];
+    e.g = geo[b];
+    e.nqb = (geo[b].m + kQB - 1) / kQB;
+    e.item_begin = items;
+    e.o = o_out[b];
+    e.lse = lse_out[b];
+    items += B * (int64_t)geo[b].nseg * H * e.nqb;
+  }
+  for (int x = nbranch; x < GP_MAX_BRANCHES; ++x) a.br[x] = a.br[nbranch - 1];
+  a.total_items = items;
+  GP_REQUIRE(items < (int64_t)0x7fffffff, "gp_dilated_attn_fwd: too many work items");
+  hipStream_t s = gp_stream(stream);
+  switch (D) {
+    case 48: dilated_attn_kernel<48><<<(unsigned)items, 256, 0, s>>>(a); break;
+    case 64: dilated_attn_kernel<64><<<(unsigned)items, 256, 0, s>>>(a); break;
+    case 96: dilated_attn_kernel<96><<<(unsigned)items, 256, 0, s>>>(a); break;
+  }
+  return gp_check_launch("gp_dilated_attn_fwd");
+}
+
+extern "C" int gp_seg_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, int64_t nbatch,
+                               int64_t seqlen, int H, int D, float softmax_scale, uint16_t* o, float* lse,
+                               void* stream) {
+  GP_REQUIRE(seqlen > 0 && seqlen < (int64_t)0x7fffffff, "gp_seg_attn_fwd: bad seqlen");
+  const int32_t sl = (int32_t)seqlen, r = 1;
+  return gp_dilated_attn_fwd(q, k, v, (int64_t)H * D, nbatch, seqlen, H, D, &sl, &r, 1, &o, &lse, softmax_scale,
+                             stream);
+}
+
+extern "C" int gp_branch_merge_ln(const uint16_t* const* o_in, const float* const* lse_in, const int32_t* seg_len,
+                                  const int32_t* ratios, int nbranch, int64_t B, int64_t L, int H, int D,
+                                  const float* ln_w, const float* ln_b, float eps, uint16_t* out, void* stream) {
+  const int E = H * D;
+  GP_REQUIRE(nbranch >= 1 && nbranch <= GP_MAX_BRANCHES, "gp_branch_merge_ln: nbranch must be 1..%d", GP_MAX_BRANCHES);
+  GP_REQUIRE(E % 64 == 0 && (E / 64 == 12 || E / 64 == 16 || E / 64 == 24) && D % (E / 64) == 0,
+             "gp_branch_merge_ln: H*D=%d unsupported", E);
+  GP_REQUIRE(B > 0 && L > 0, "gp_branch_merge_ln: bad sizes");
+  GP_REQUIRE(o_in && lse_in && seg_len && ratios && out, "gp_branch_merge_ln: null pointer");
+  GP_REQUIRE(ln_w == nullptr || ln_b != nullptr, "gp_branch_merge_ln: ln_w without ln_b");
+  MergeArgs a;
+  a.B = B; a.L = L; a.H = H; a.D = D; a.E = E; a.nbranch = nbranch;
+  for (int b = 0; b < nbranch; ++b) {
+    GP_REQUIRE(seg_len[b] > 0 && ratios[b] > 0 && o_in[b] && lse_in[b], "gp_branch_merge_ln: bad branch %d", b);
+    a.br[b].g = gp_make_branch(L, seg_len[b], ratios[b], H);
+    a.br[b].o = o_in[b];
+    a.br[b].lse = lse_in[b];
+  }
+  for (int b = nbranch; b < GP_MAX_BRANCHES; ++b) a.br[b] = a.br[nbranch - 1];
+  a.ln_w = ln_w; a.ln_b = ln_b; a.eps = eps; a.out = out;
+  const unsigned nb = (unsigned)((B * L + 3) / 4);
+  hipStream_t s = gp_stream(stream);
+  switch (E / 64) {
+    case 12: branch_merge_kernel<12><<<nb, 256, 0, s>>>(a); break;
+    case 16: branch_merge_kernel<16><<<nb, 256, 0, s>>>(a); break;
+    case 24: branch_merge_kernel<24><<<nb, 256, 0, s>>>(a); break;
+  }
+  return gp_check_launch("gp_branch_merge_ln");
+}

@@ -1,0 +1,123 @@
+// Shared device helpers for the gfx950 slide-encoder kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define GP_DEV __device__ __forceinline__
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// bf16 <-> fp32 on raw bit patterns.  f2bf is round-to-nearest-even (keeps NaN a NaN).
+GP_DEV float bf2f(uint16_t b) { return __uint_as_float(((uint32_t)b) << 16); }
+GP_DEV uint16_t f2bf(float f) {
+  __bf16 h = (__bf16)f;
+  return __builtin_bit_cast(uint16_t, h);
+}
+
+GP_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+GP_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Load / store N consecutive bf16 (N % 4 == 0, 8-byte aligned) as fp32.
+template <int N>
+GP_DEV void load_bf16(const uint16_t* p, float* out) {
+  static_assert(N % 4 == 0, "");
+  const uint2* q = reinterpret_cast<const uint2*>(p);
+#pragma unroll
+  for (int i = 0; i < N / 4; ++i) {
+    uint2 u = q[i];
+    out[4 * i + 0] = __uint_as_float(u.x << 16);
+    out[4 * i + 1] = __uint_as_float(u.x & 0xffff0000u);
+    out[4 * i + 2] = __uint_as_float(u.y << 16);
+    out[4 * i + 3] = __uint_as_float(u.y & 0xffff0000u);
+  }
+}
+template <int N>
+GP_DEV void store_bf16(uint16_t* p, const float* v) {
+  static_assert(N % 4 == 0, "");
+  uint2* q = reinterpret_cast<uint2*>(p);
+#pragma unroll
+  for (int i = 0; i < N / 4; ++i) {
+    uint2 u;
+    u.x = (uint32_t)f2bf(v[4 * i + 0]) | ((uint32_t)f2bf(v[4 * i + 1]) << 16);
+    u.y = (uint32_t)f2bf(v[4 * i + 2]) | ((uint32_t)f2bf(v[4 * i + 3]) << 16);
+    q[i] = u;
+  }
+}
+template <int N>
+GP_DEV void load_f32(const float* p, float* out) {
+  static_assert(N % 4 == 0, "");
+  const float4* q = reinterpret_cast<const float4*>(p);
+#pragma unroll
+  for (int i = 0; i < N / 4; ++i) {
+    float4 u = q[i];
+    out[4 * i + 0] = u.x; out[4 * i + 1] = u.y; out[4 * i + 2] = u.z; out[4 * i + 3] = u.w;
+  }
+}
+template <int N>
+GP_DEV void store_f32(float* p, const float* v) {
+  static_assert(N % 4 == 0, "");
+  float4* q = reinterpret_cast<float4*>(p);
+#pragma unroll
+  for (int i = 0; i < N / 4; ++i) q[i] = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+}
+
+// LayerNorm of one row held as EPL values per lane across a 64-lane wave (torch semantics:
+// biased variance, y = (x - mean) / sqrt(var + eps) * w + b), fp32 throughout.
+template <int EPL>
+GP_DEV void wave_layernorm(float* v, int cols, const float* w, const float* b, float eps, int col0) {
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) s += v[i];
+  const float mean = wave_sum(s) / (float)cols;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) {
+    const float d = v[i] - mean;
+    q += d * d;
+  }
+  const float rstd = rsqrtf(wave_sum(q) / (float)cols + eps);
+  float wv[EPL], bv[EPL];
+  load_f32<EPL>(w + col0, wv);
+  load_f32<EPL>(b + col0, bv);
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) v[i] = (v[i] - mean) * rstd * wv[i] + bv[i];
+}
+
+// Per-branch geometry of the dilated schedule (dilated_attention.py:16-31, 76-98).
+struct GpBranch {
+  int32_t s;      // min(sl, L)
+  int32_t r;      // dilation ratio
+  int32_t m;      // ceil(s / r) sparse rows per segment
+  int32_t nseg;   // ceil(L / s) segments per batch
+  int32_t g;      // m * r: dense length per segment after sparse_to_dense
+  int32_t hpg;    // heads per dilation group: (H rounded up to r) / r
+};
+
+inline GpBranch gp_make_branch(int64_t L, int sl, int r, int H) {
+  GpBranch b;
+  b.s = (int32_t)(sl < L ? sl : L);
+  b.r = r;
+  b.m = (b.s + r - 1) / r;
+  b.nseg = (int32_t)((L + b.s - 1) / b.s);
+  b.g = b.m * r;
+  const int hp = H + ((H % r) ? (r - H % r) : 0);
+  b.hpg = hp / r;
+  return b;
+}
+
+// Number of valid (non-pad) sparse rows of segment n for head group j.
+GP_DEV int gp_valid_rows(const GpBranch& br, int64_t L, int n, int j) {
+  const int64_t rem = L - (int64_t)n * br.s;
+  const int64_t lim = (rem < br.s ? rem : br.s) - j;
+  return lim > 0 ? (int)((lim + br.r - 1) / br.r) : 0;
+}

@@ -1,0 +1,188 @@
+"""ctypes binding of libgigapath_hip.so (the C ABI declared in include/gigapath_hip.h).
+
+Tensors are passed as raw device pointers; every call is enqueued on torch's *current*
+HIP stream.  There is no fallback: if the library is missing or a call fails, this module
+raises.  torch is imported first so that its bundled HIP runtime (same soname,
+libamdhip64.so.7) is the one the library binds to.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Sequence
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("GIGAPATH_HIP_LIB", os.path.join(_HERE, "_lib", "libgigapath_hip.so"))
+ABI_VERSION = 1
+MAX_BRANCHES = 8
+
+c_i32, c_i64, c_f32, c_f64, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_double, ctypes.c_void_p
+
+# name -> argtypes (mirrors include/gigapath_hip.h)
+SIGNATURES = {
+    "gp_abi_version": [],
+    "gp_last_error_string": [],
+    "gp_coords_to_pos": [c_vp, c_i32, c_i64, c_i32, c_f64, c_vp, c_vp, c_vp],
+    "gp_posembed_cls_ln": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp],
+    "gp_dilated_gather": [c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp],
+    "gp_dilated_attn_fwd": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp,
+                            c_f32, c_vp],
+    "gp_seg_attn_fwd": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i32, c_f32, c_vp, c_vp, c_vp],
+    "gp_branch_merge_ln": [c_vp, c_vp, c_vp, c_vp, c_i32, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_f32, c_vp, c_vp],
+    "gp_residual_layernorm": [c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_vp, c_i64, c_i32, c_vp],
+    "gp_gelu_layernorm": [c_vp, c_vp, c_vp, c_f32, c_vp, c_i64, c_i32, c_vp],
+    "gp_layernorm_f32": [c_vp, c_i64, c_vp, c_vp, c_f32, c_vp, c_i64, c_i32, c_vp],
+    "gp_mean_tokens": [c_vp, c_i64, c_i64, c_i32, c_i64, c_vp, c_vp],
+}
+
+_lib = None
+
+
+class HipLibraryError(RuntimeError):
+    pass
+
+
+def load_library(path: Optional[str] = None) -> ctypes.CDLL:
+    """Load (once) and type the C ABI.  Raises HipLibraryError if it is absent."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise HipLibraryError(
+            "libgigapath_hip.so not found at %s: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "or `make -C prov-gigapath-replication_amd/csrc`" % p)
+    lib = ctypes.CDLL(p)
+    for name, args in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = ctypes.c_char_p if name == "gp_last_error_string" else ctypes.c_int
+    if lib.gp_abi_version() != ABI_VERSION:
+        raise HipLibraryError("ABI mismatch: library %d, binding %d" % (lib.gp_abi_version(), ABI_VERSION))
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def _check(rc: int, name: str):
+    if rc != 0:
+        msg = _lib.gp_last_error_string().decode(errors="replace")
+        raise RuntimeError("%s failed (rc=%d): %s" % (name, rc, msg))
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def _dev(t: torch.Tensor, dtype=None, name="tensor"):
+    if not t.is_cuda:
+        raise RuntimeError("gigapath HIP path: %s must be a ROCm device tensor (got %s)" % (name, t.device))
+    if dtype is not None and t.dtype != dtype:
+        raise TypeError("gigapath HIP path: %s must be %s (got %s)" % (name, dtype, t.dtype))
+    if not t.is_contiguous():
+        raise ValueError("gigapath HIP path: %s must be contiguous" % name)
+    return t
+
+
+def _i32_array(vals: Sequence[int]):
+    return (ctypes.c_int32 * len(vals))(*[int(v) for v in vals])
+
+
+def _ptr_array(ts: Sequence[torch.Tensor]):
+    return (ctypes.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
+
+
+# ------------------------------------------------------------------------------------------
+# typed wrappers
+# ------------------------------------------------------------------------------------------
+def coords_to_pos(coords: torch.Tensor, grid: int, tile_size: float, pos_out: torch.Tensor,
+                  err_count: Optional[torch.Tensor]):
+    lib = load_library()
+    _dev(coords, name="coords")
+    if coords.dtype not in (torch.float32, torch.float64):
+        raise TypeError("coords must be float32 or float64")
+    _dev(pos_out, torch.int64, "pos")
+    n = coords.numel() // 2
+    _check(lib.gp_coords_to_pos(_ptr(coords), int(coords.dtype == torch.float64), n, grid, float(tile_size),
+                                _ptr(pos_out), _ptr(err_count), _stream()), "gp_coords_to_pos")
+
+
+def posembed_cls_ln(xp, pos, tab, cls, B, N, E, G, ln_w, ln_b, eps, x_out, ln_out):
+    lib = load_library()
+    _dev(xp, torch.bfloat16, "xp"); _dev(pos, torch.int64, "pos"); _dev(tab, torch.float32, "tab")
+    _dev(cls, torch.float32, "cls"); _dev(x_out, torch.float32, "x_out")
+    _check(lib.gp_posembed_cls_ln(_ptr(xp), _ptr(pos), _ptr(tab), _ptr(cls), B, N, E, G, _ptr(ln_w), _ptr(ln_b),
+                                  eps, _ptr(x_out), _ptr(ln_out), _stream()), "gp_posembed_cls_ln")
+
+
+def dilated_gather(src, row_stride, col_off, B, L, H, D, sl, r, dst):
+    lib = load_library()
+    _dev(src, torch.bfloat16, "src"); _dev(dst, torch.bfloat16, "dst")
+    _check(lib.gp_dilated_gather(_ptr(src), row_stride, col_off, B, L, H, D, sl, r, _ptr(dst), _stream()),
+           "gp_dilated_gather")
+
+
+def dilated_attn_fwd(q, k, v, row_stride, B, L, H, D, segs, ratios, outs, lses, softmax_scale=0.0):
+    lib = load_library()
+    for t in (q, k, v):
+        if not t.is_cuda or t.dtype != torch.bfloat16:
+            raise TypeError("q/k/v must be bf16 device tensors")
+    oa, la = _ptr_array(outs), _ptr_array(lses)
+    _check(lib.gp_dilated_attn_fwd(_ptr(q), _ptr(k), _ptr(v), row_stride, B, L, H, D, _i32_array(segs),
+                                   _i32_array(ratios), len(segs), oa, la, float(softmax_scale), _stream()),
+           "gp_dilated_attn_fwd")
+
+
+def seg_attn_fwd(q, k, v, o, lse, softmax_scale=0.0):
+    lib = load_library()
+    nb, sl, H, D = q.shape
+    for nm, t in (("q", q), ("k", k), ("v", v), ("o", o)):
+        _dev(t, torch.bfloat16, nm)
+    _dev(lse, torch.float32, "lse")
+    _check(lib.gp_seg_attn_fwd(_ptr(q), _ptr(k), _ptr(v), nb, sl, H, D, float(softmax_scale), _ptr(o), _ptr(lse),
+                               _stream()), "gp_seg_attn_fwd")
+
+
+def branch_merge_ln(outs, lses, segs, ratios, B, L, H, D, ln_w, ln_b, eps, out):
+    lib = load_library()
+    _dev(out, torch.bfloat16, "out")
+    _check(lib.gp_branch_merge_ln(_ptr_array(outs), _ptr_array(lses), _i32_array(segs), _i32_array(ratios),
+                                  len(segs), B, L, H, D, _ptr(ln_w), _ptr(ln_b), eps, _ptr(out), _stream()),
+           "gp_branch_merge_ln")
+
+
+def residual_layernorm(x, y, bias, ln_w, ln_b, eps, ln_out, rows, cols):
+    lib = load_library()
+    _dev(x, torch.float32, "x"); _dev(y, torch.bfloat16, "y")
+    _check(lib.gp_residual_layernorm(_ptr(x), _ptr(y), _ptr(bias), _ptr(ln_w), _ptr(ln_b), eps, _ptr(ln_out),
+                                     rows, cols, _stream()), "gp_residual_layernorm")
+
+
+def gelu_layernorm(h, ln_w, ln_b, eps, out, rows, cols):
+    lib = load_library()
+    _dev(h, torch.bfloat16, "h"); _dev(out, torch.bfloat16, "out")
+    _check(lib.gp_gelu_layernorm(_ptr(h), _ptr(ln_w), _ptr(ln_b), eps, _ptr(out), rows, cols, _stream()),
+           "gp_gelu_layernorm")
+
+
+def layernorm_f32(x, row_stride, ln_w, ln_b, eps, out, rows, cols):
+    lib = load_library()
+    if not x.is_cuda or x.dtype != torch.float32:
+        raise TypeError("x must be an fp32 device tensor")
+    _dev(out, torch.float32, "out")
+    _check(lib.gp_layernorm_f32(_ptr(x), row_stride, _ptr(ln_w), _ptr(ln_b), eps, _ptr(out), rows, cols,
+                                _stream()), "gp_layernorm_f32")
+
+
+def mean_tokens(x, B, L, E, start, out):
+    lib = load_library()
+    _dev(x, torch.float32, "x"); _dev(out, torch.float32, "out")
+    _check(lib.gp_mean_tokens(_ptr(x), B, L, E, start, _ptr(out), _stream()), "gp_mean_tokens")

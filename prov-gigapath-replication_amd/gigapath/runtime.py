@@ -1,0 +1,272 @@
+"""MI355X execution engine of the LongNet slide-encoder forward.
+
+Per layer the engine issues 9 launches on torch's current HIP stream (M = B*L tokens):
+
+    qkv  = a . Wqkv^T + bqkv             hipBLASLt (bias epilogue)         [M, 3E] bf16
+    attn = gp_dilated_attn_fwd(qkv)        ONE launch, all dilation branches  sparse o / lse
+    a    = LN_inner(merge(attn))           gp_branch_merge_ln                 [M, E] bf16
+    y    = a . Wo^T                        hipBLASLt                          [M, E] bf16
+    x   += y + bo ; a = LN2(x)             gp_residual_layernorm (fp32 residual stream)
+    f    = a . W1^T + b1                   hipBLASLt (bias epilogue)          [M, F] bf16
+    f    = LN_ffn(gelu(f))                 gp_gelu_layernorm
+    y    = f . W2^T                        hipBLASLt
+    x   += y + b2 ; a = LN1(next layer)    gp_residual_layernorm
+
+which is EncoderLayer.forward (torchscale/architecture/encoder.py:116-162) with
+DilatedAttention.forward (component/dilated_attention.py:133-217) and the FFN
+(component/feedforward_network.py:131-142) in eval mode.  The residual stream stays fp32;
+GEMM operands are bf16 with fp32 accumulation.  Weights are packed once per parameter
+version (fused QKV weight, bf16 GEMM operands, fp32 norms/biases) and workspaces are reused
+across calls of the same shape.  No CPU fallback exists: every non-GEMM op is a HIP kernel.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import _hip
+
+
+# ------------------------------------------------------------------------------------------
+# optional live timing of the hot kernels (bench.py: roofline "achieved" numbers)
+# ------------------------------------------------------------------------------------------
+class KernelTimer:
+    """Records HIP events (on the launch stream) around selected kernels when enabled."""
+
+    def __init__(self):
+        self.enabled = False
+        self.events: Dict[str, List[Tuple[torch.cuda.Event, torch.cuda.Event]]] = {}
+
+    def reset(self):
+        self.events = {}
+
+    def span(self, name: str):
+        timer = self
+
+        class _Span:
+            def __enter__(self_inner):
+                if timer.enabled:
+                    self_inner.e0 = torch.cuda.Event(enable_timing=True)
+                    self_inner.e1 = torch.cuda.Event(enable_timing=True)
+                    self_inner.e0.record()
+                return self_inner
+
+            def __exit__(self_inner, *exc):
+                if timer.enabled:
+                    self_inner.e1.record()
+                    timer.events.setdefault(name, []).append((self_inner.e0, self_inner.e1))
+                return False
+
+        return _Span()
+
+    def totals_ms(self) -> Dict[str, Tuple[int, float]]:
+        """name -> (launch count, summed milliseconds).  Synchronises."""
+        torch.cuda.synchronize()
+        return {k: (len(v), sum(a.elapsed_time(b) for a, b in v)) for k, v in self.events.items()}
+
+
+TIMER = KernelTimer()
+
+
+# ------------------------------------------------------------------------------------------
+# geometry (dilated_attention.py:16-31, 76-98)
+# ------------------------------------------------------------------------------------------
+def branch_geometry(L: int, sl: int, r: int) -> Tuple[int, int, int]:
+    """(s, nseg, m) of one branch at sequence length L."""
+    s = min(sl, L)
+    return s, -(-L // s), -(-s // r)
+
+
+def attention_valid_flops(L: int, segs: Sequence[int], ratios: Sequence[int], H: int, D: int, B: int = 1) -> float:
+    """Algorithmic FLOPs of one layer's dilated attention: 4*D*c^2 per (segment, head), c = real
+    (non-pad) tokens the head sees in that segment.  Zero pads count 0."""
+    tot = 0
+    for sl, r in zip(segs, ratios):
+        s, nseg, m = branch_geometry(L, sl, r)
+        hp = H + ((r - H % r) % r)
+        hpg = hp // r
+        for n in range(nseg):
+            rem = min(L - n * s, s)
+            for h in range(H):
+                j = h // hpg
+                lim = rem - j
+                c = -(-lim // r) if lim > 0 else 0
+                tot += 4 * D * c * c
+    return float(tot * B)
+
+
+# ------------------------------------------------------------------------------------------
+# packed weights
+# ------------------------------------------------------------------------------------------
+def _bf16(t: torch.Tensor, dev) -> torch.Tensor:
+    return t.detach().to(device=dev, dtype=torch.bfloat16).contiguous()
+
+
+def _f32(t: torch.Tensor, dev) -> torch.Tensor:
+    return t.detach().to(device=dev, dtype=torch.float32).contiguous()
+
+
+@dataclass
+class PackedAttention:
+    E: int
+    H: int
+    D: int
+    segs: List[int]
+    ratios: List[int]
+    w_qkv: torch.Tensor      # [3E, E] bf16 (q | k | v rows)
+    b_qkv: torch.Tensor      # [3E] bf16
+    w_o: torch.Tensor        # [E, E] bf16
+    b_o: torch.Tensor        # [E] fp32 (added in the residual kernel)
+    b_o_bf16: torch.Tensor   # [E] bf16 (standalone module forward)
+    ln_w: torch.Tensor
+    ln_b: torch.Tensor
+    ln_eps: float
+
+    @staticmethod
+    def from_module(m, dev) -> "PackedAttention":
+        E, H = m.embed_dim, m.num_heads
+        return PackedAttention(
+            E=E, H=H, D=E // H, segs=list(m.args.segment_length), ratios=list(m.args.dilated_ratio),
+            w_qkv=_bf16(torch.cat([m.q_proj.weight, m.k_proj.weight, m.v_proj.weight], 0), dev),
+            b_qkv=_bf16(torch.cat([m.q_proj.bias, m.k_proj.bias, m.v_proj.bias], 0), dev),
+            w_o=_bf16(m.out_proj.weight, dev), b_o=_f32(m.out_proj.bias, dev), b_o_bf16=_bf16(m.out_proj.bias, dev),
+            ln_w=_f32(m.inner_attn_ln.weight, dev), ln_b=_f32(m.inner_attn_ln.bias, dev),
+            ln_eps=float(m.inner_attn_ln.eps))
+
+
+@dataclass
+class PackedLayer:
+    attn: PackedAttention
+    ln1_w: torch.Tensor
+    ln1_b: torch.Tensor
+    ln1_eps: float
+    ln2_w: torch.Tensor
+    ln2_b: torch.Tensor
+    ln2_eps: float
+    w1: torch.Tensor         # [F, E] bf16
+    b1: torch.Tensor         # [F] bf16
+    fln_w: torch.Tensor      # [F] fp32
+    fln_b: torch.Tensor
+    fln_eps: float
+    w2: torch.Tensor         # [E, F] bf16
+    b2: torch.Tensor         # [E] fp32
+
+    @staticmethod
+    def from_module(layer, dev) -> "PackedLayer":
+        ffn = layer.ffn
+        return PackedLayer(
+            attn=PackedAttention.from_module(layer.self_attn, dev),
+            ln1_w=_f32(layer.self_attn_layer_norm.weight, dev), ln1_b=_f32(layer.self_attn_layer_norm.bias, dev),
+            ln1_eps=float(layer.self_attn_layer_norm.eps),
+            ln2_w=_f32(layer.final_layer_norm.weight, dev), ln2_b=_f32(layer.final_layer_norm.bias, dev),
+            ln2_eps=float(layer.final_layer_norm.eps),
+            w1=_bf16(ffn.fc1.weight, dev), b1=_bf16(ffn.fc1.bias, dev),
+            fln_w=_f32(ffn.ffn_layernorm.weight, dev), fln_b=_f32(ffn.ffn_layernorm.bias, dev),
+            fln_eps=float(ffn.ffn_layernorm.eps),
+            w2=_bf16(ffn.fc2.weight, dev), b2=_f32(ffn.fc2.bias, dev))
+
+
+def param_signature(module: torch.nn.Module) -> tuple:
+    return tuple((p.data_ptr(), p._version, p.dtype) for p in module.parameters())
+
+
+# ------------------------------------------------------------------------------------------
+# the dilated attention core (gather + attention + merge + inner LN), shared by the engine
+# and by the standalone DilatedAttention module
+# ------------------------------------------------------------------------------------------
+class AttentionScratch:
+    def __init__(self, dev, B: int, L: int, H: int, D: int, segs, ratios):
+        self.key = (B, L, H, D, tuple(segs), tuple(ratios))
+        self.outs, self.lses = [], []
+        for sl, r in zip(segs, ratios):
+            s, nseg, m = branch_geometry(L, sl, r)
+            self.outs.append(torch.empty(B * nseg * m * H * D, dtype=torch.bfloat16, device=dev))
+            self.lses.append(torch.empty(B * nseg * H * m, dtype=torch.float32, device=dev))
+
+
+def dilated_attention_core(pa: PackedAttention, qkv: torch.Tensor, B: int, L: int, scratch: AttentionScratch,
+                           out: torch.Tensor, inner_ln: bool = True):
+    """qkv: [B*L, 3E] bf16 (q | k | v); out: [B*L, E] bf16 = inner_attn_ln(merge(branches))."""
+    E, H, D = pa.E, pa.H, pa.D
+    with TIMER.span("attn"):
+        _hip.dilated_attn_fwd(qkv, qkv[:, E:], qkv[:, 2 * E:], 3 * E, B, L, H, D, pa.segs, pa.ratios,
+                              scratch.outs, scratch.lses)
+    with TIMER.span("merge"):
+        _hip.branch_merge_ln(scratch.outs, scratch.lses, pa.segs, pa.ratios, B, L, H, D,
+                             pa.ln_w if inner_ln else None, pa.ln_b if inner_ln else None, pa.ln_eps, out)
+
+
+# ------------------------------------------------------------------------------------------
+# encoder engine
+# ------------------------------------------------------------------------------------------
+class Workspace:
+    def __init__(self, dev, B: int, L: int, E: int, F: int, H: int, segs, ratios):
+        M = B * L
+        self.key = (str(dev), B, L, E, F, H, tuple(segs), tuple(ratios))
+        self.x = torch.empty(M, E, dtype=torch.float32, device=dev)
+        self.a = torch.empty(M, E, dtype=torch.bfloat16, device=dev)
+        self.qkv = torch.empty(M, 3 * E, dtype=torch.bfloat16, device=dev)
+        self.y = torch.empty(M, E, dtype=torch.bfloat16, device=dev)
+        self.f = torch.empty(M, F, dtype=torch.bfloat16, device=dev)
+        self.attn = AttentionScratch(dev, B, L, H, E // H, segs, ratios)
+
+
+class EncoderEngine:
+    """Runs the 12-layer (or 24-) LongNet stack on one device for inputs already embedded."""
+
+    def __init__(self):
+        self._sig = None
+        self.layers: List[PackedLayer] = []
+        self.ws: Optional[Workspace] = None
+
+    def pack(self, encoder, dev):
+        sig = (str(dev), param_signature(encoder))
+        if sig != self._sig:
+            self.layers = [PackedLayer.from_module(l, dev) for l in encoder.layers]
+            self._sig = sig
+        return self.layers
+
+    def workspace(self, dev, B, L, E, F, H, segs, ratios) -> Workspace:
+        key = (str(dev), B, L, E, F, H, tuple(segs), tuple(ratios))
+        if self.ws is None or self.ws.key != key:
+            self.ws = None
+            self.ws = Workspace(dev, B, L, E, F, H, segs, ratios)
+        return self.ws
+
+    def run_layers(self, ws: Workspace, B: int, L: int, layer_hook=None):
+        """ws.x holds the fp32 embedding and ws.a = LN1_0(ws.x) (bf16).  Runs every layer in
+        place; layer_hook(i) is called after layer i-1 finishes (i = 1..depth)."""
+        M = B * L
+        E = ws.x.shape[1]
+        F = ws.f.shape[1]
+        nl = len(self.layers)
+        for li, pl in enumerate(self.layers):
+            pa = pl.attn
+            with TIMER.span("gemm_qkv"):
+                torch.addmm(pa.b_qkv, ws.a, pa.w_qkv.t(), out=ws.qkv)
+            dilated_attention_core(pa, ws.qkv, B, L, ws.attn, ws.a)
+            with TIMER.span("gemm_out"):
+                torch.mm(ws.a, pa.w_o.t(), out=ws.y)
+            with TIMER.span("resid_ln"):
+                _hip.residual_layernorm(ws.x, ws.y, pa.b_o, pl.ln2_w, pl.ln2_b, pl.ln2_eps, ws.a, M, E)
+            with TIMER.span("gemm_fc1"):
+                torch.addmm(pl.b1, ws.a, pl.w1.t(), out=ws.f)
+            with TIMER.span("gelu_ln"):
+                _hip.gelu_layernorm(ws.f, pl.fln_w, pl.fln_b, pl.fln_eps, ws.f, M, F)
+            with TIMER.span("gemm_fc2"):
+                torch.mm(ws.f, pl.w2.t(), out=ws.y)
+            nxt = self.layers[li + 1] if li + 1 < nl else None
+            with TIMER.span("resid_ln"):
+                _hip.residual_layernorm(ws.x, ws.y, pl.b2, nxt.ln1_w if nxt else None, nxt.ln1_b if nxt else None,
+                                        nxt.ln1_eps if nxt else 1e-5, ws.a, M, E)
+            if layer_hook is not None:
+                layer_hook(li + 1)
+
+
+def gemm_flops(B: int, N: int, E: int, F: int, C: int, depth: int) -> float:
+    L = N + 1
+    return float(2 * B * L * (4 * E * E + 2 * E * F) * depth + 2 * B * N * C * E)

@@ -1,0 +1,253 @@
+"""Prov-GigaPath slide encoder — MI355X drop-in for ``gigapath.slide_encoder``.
+
+Same public surface as the reference (gigapath/slide_encoder.py:32-270): ``PatchEmbed``,
+``LongNetViT`` (constructor kwargs, ``forward(x, coords, all_layer_embed=False) -> list``,
+``coords_to_pos``, ``get_optimal_segment_length``), ``create_model(pretrained, model_arch,
+in_chans, local_dir, **kwargs)`` and the three registered architectures, with the same
+247-key state dict.  The forward is inference-only and runs on a ROCm device:
+
+    patch GEMM (hipBLASLt) -> gp_coords_to_pos -> gp_posembed_cls_ln (pos add + CLS + LN1)
+    -> 12 x LongNet layer (runtime.EncoderEngine) -> LN readouts (gp_layernorm_f32 /
+    gp_mean_tokens)
+
+The 3.07 GB fp32 ``pos_embed`` buffer of the reference is replaced by its exact [G, E/2]
+factor (see pos_embed.py); ``model.pos_embed`` is still available, built lazily on the CPU.
+"""
+from __future__ import annotations
+
+import os
+from functools import partial
+from typing import Dict, List
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import _hip, runtime
+from .pos_embed import axis_table, get_2d_sincos_pos_embed
+from .torchscale.model.LongNet import make_longnet_from_name
+
+_REGISTRY: Dict[str, callable] = {}
+
+
+def register_model(fn):
+    _REGISTRY[fn.__name__] = fn
+    return fn
+
+
+def list_models() -> List[str]:
+    return sorted(_REGISTRY)
+
+
+class PatchEmbed(nn.Module):
+    """Slide patch embedding: Linear(in_chans -> embed_dim) (+ optional norm)."""
+
+    def __init__(self, in_chans=1536, embed_dim=768, norm_layer=None, bias=True):
+        super().__init__()
+        self.proj = nn.Linear(in_chans, embed_dim, bias=bias)
+        self.norm = norm_layer(embed_dim) if norm_layer else nn.Identity()
+
+    def forward(self, x):
+        if not isinstance(self.norm, nn.Identity):
+            raise NotImplementedError("PatchEmbed norm is not used by the registered slide encoders")
+        dev = x.device
+        if dev.type != "cuda":
+            raise RuntimeError("PatchEmbed (MI355X path) needs ROCm device tensors")
+        B, L, C = x.shape
+        y = torch.addmm(self.proj.bias.to(dev, torch.bfloat16), x.reshape(B * L, C).to(torch.bfloat16),
+                        self.proj.weight.to(dev, torch.bfloat16).t())
+        return y.view(B, L, -1).to(x.dtype)
+
+
+class LongNetViT(nn.Module):
+    """LongNet slide encoder backbone (reference gigapath/slide_encoder.py:54-223)."""
+
+    def __init__(self, in_chans=1536, embed_dim=256, depth=12, slide_ngrids=1000, tile_size=256,
+                 max_wsi_size=262144, norm_layer=nn.LayerNorm, global_pool=False, dropout=0.25,
+                 drop_path_rate=0.1, **kwargs):
+        super().__init__()
+        self.patch_embed = PatchEmbed(in_chans, embed_dim)
+        self.tile_size = tile_size
+        self.slide_ngrids = slide_ngrids
+        self.embed_dim = embed_dim
+        self.cls_token = nn.Parameter(torch.zeros(1, 1, embed_dim))
+        self.encoder_name = "LongNet_{}_layers_{}_dim".format(depth, embed_dim)
+        if kwargs.get("mlp_ratio", 4.0) != 4.0:
+            self.encoder_name += "_mlp{}".format(kwargs.get("mlp_ratio"))
+        segment_length = self.get_optimal_segment_length(max_wsi_size, tile_size)
+        self.encoder = make_longnet_from_name(self.encoder_name, drop_path_rate=drop_path_rate, dropout=dropout,
+                                              segment_length=segment_length)
+        self.norm = norm_layer(embed_dim)
+        self.global_pool = global_pool
+        self.validate_positions = True      # raise IndexError on out-of-range coords like the reference
+        print("Global Pooling:", self.global_pool)
+        self._top_sig = None
+        self._top = None
+        self._pos_full = None
+        self.initialize_vit_weights()
+
+    # ---------------------------------------------------------------- init / helpers
+    def initialize_vit_weights(self):
+        w = self.patch_embed.proj.weight.data
+        torch.nn.init.xavier_uniform_(w.view([w.shape[0], -1]))
+        torch.nn.init.normal_(self.cls_token, std=0.02)
+        self.apply(self._init_weights)
+
+    def _init_weights(self, m):
+        if isinstance(m, nn.Linear):
+            torch.nn.init.xavier_uniform_(m.weight)
+            if m.bias is not None:
+                nn.init.constant_(m.bias, 0)
+        elif isinstance(m, nn.LayerNorm):
+            nn.init.constant_(m.bias, 0)
+            nn.init.constant_(m.weight, 1.0)
+
+    def get_optimal_segment_length(self, max_wsi_size: int = 262144, tile_size: int = 256) -> str:
+        """Five segment lengths 2**linspace(10, log2((max_wsi/tile)^2), 5) (reference :137-154),
+        rendered with plain ints (the reference's str(list(np.int64)) breaks under numpy>=2)."""
+        max_seq_len = (max_wsi_size // tile_size) ** 2
+        seg = np.power(2, np.linspace(np.log2(1024), int(np.log2(max_seq_len)), 5)).astype(int)
+        return str([int(v) for v in seg])
+
+    @property
+    def pos_embed(self) -> torch.Tensor:
+        """The reference's [1, G*G+1, E] fp32 table (3.07 GB at G=1000), built lazily on the CPU.
+        The forward never uses it."""
+        if self._pos_full is None:
+            self._pos_full = torch.from_numpy(
+                get_2d_sincos_pos_embed(self.embed_dim, self.slide_ngrids, cls_token=True)).float().unsqueeze(0)
+        return self._pos_full
+
+    def coords_to_pos(self, coords, tile_size: int = 256):
+        """[B, N, 2] pixel coordinates -> [B, N] int64 flat pos-embed rows (reference :166-179)."""
+        if coords.device.type != "cuda":
+            raise RuntimeError("coords_to_pos (MI355X path) needs ROCm device tensors")
+        c = coords if coords.dtype in (torch.float32, torch.float64) else coords.float()
+        c = c.contiguous()
+        pos = torch.empty(c.shape[:-1], dtype=torch.int64, device=c.device)
+        _hip.coords_to_pos(c, self.slide_ngrids, tile_size, pos, None)
+        return pos
+
+    def _packed_top(self, dev):
+        mods = (self.patch_embed, self.norm, self.encoder.layer_norm, self.encoder.layers[0].self_attn_layer_norm)
+        sig = (str(dev), self.cls_token.data_ptr(), self.cls_token._version,
+               tuple(runtime.param_signature(m) for m in mods))
+        if sig != self._top_sig:
+            f32, bf = runtime._f32, runtime._bf16
+            ln1 = self.encoder.layers[0].self_attn_layer_norm
+            self._top = dict(
+                wp=bf(self.patch_embed.proj.weight, dev), bp=bf(self.patch_embed.proj.bias, dev),
+                cls=f32(self.cls_token.reshape(-1), dev),
+                tab=torch.from_numpy(axis_table(self.embed_dim, self.slide_ngrids)).to(dev),
+                ln1_w=f32(ln1.weight, dev), ln1_b=f32(ln1.bias, dev), ln1_eps=float(ln1.eps),
+                enc_w=f32(self.encoder.layer_norm.weight, dev), enc_b=f32(self.encoder.layer_norm.bias, dev),
+                enc_eps=float(self.encoder.layer_norm.eps),
+                norm_w=f32(self.norm.weight, dev), norm_b=f32(self.norm.bias, dev), norm_eps=float(self.norm.eps))
+            self._top_sig = sig
+        return self._top
+
+    # ---------------------------------------------------------------- forward
+    def forward(self, x, coords, all_layer_embed=False):
+        """x [B, N, in_chans], coords [B, N, 2] (pixels) -> list of [B, E] slide embeddings:
+        1 (final, after encoder.layer_norm) or, with all_layer_embed, 1 + depth (embedding and
+        every layer output, before encoder.layer_norm), each through self.norm; CLS row, or the
+        mean over tiles when global_pool (reference :181-223, encoder.py:360-388)."""
+        self.encoder.check_eval()
+        dev = self.cls_token.device
+        if dev.type != "cuda" or x.device != dev or coords.device != dev:
+            raise RuntimeError("LongNetViT (MI355X path): model, x and coords must be on the same ROCm device "
+                               "(model %s, x %s, coords %s)" % (dev, x.device, coords.device))
+        B, N, C = x.shape
+        if coords.shape != (B, N, 2):
+            raise ValueError("coords must be [B, N, 2], got %s" % (tuple(coords.shape),))
+        E, L, M = self.embed_dim, N + 1, B * (N + 1)
+        top = self._packed_top(dev)
+        eng = self.encoder.engine
+        layers = eng.pack(self.encoder, dev)
+        pa = layers[0].attn
+        ws = eng.workspace(dev, B, L, E, self.encoder.args.encoder_ffn_embed_dim, pa.H, pa.segs, pa.ratios)
+        if not hasattr(ws, "pos") or ws.pos.numel() != B * N:
+            ws.pos = torch.empty(B * N, dtype=torch.int64, device=dev)
+            ws.err = torch.zeros(1, dtype=torch.int32, device=dev)
+
+        # patch embedding (hipBLASLt, bias epilogue) into the spare bf16 buffer
+        xp = ws.y[:B * N]
+        with runtime.TIMER.span("gemm_patch"):
+            torch.addmm(top["bp"], x.reshape(B * N, C).to(torch.bfloat16), top["wp"].t(), out=xp)
+        c = coords if coords.dtype in (torch.float32, torch.float64) else coords.float()
+        ws.err.zero_()
+        _hip.coords_to_pos(c.contiguous(), self.slide_ngrids, self.tile_size, ws.pos, ws.err)
+        if self.validate_positions and int(ws.err.item()) > 0:
+            raise IndexError("coords map outside pos_embed (%d rows): %d tiles" %
+                             (self.slide_ngrids ** 2 + 1, int(ws.err.item())))
+        with runtime.TIMER.span("posembed"):
+            _hip.posembed_cls_ln(xp, ws.pos, top["tab"], top["cls"], B, N, E, self.slide_ngrids, top["ln1_w"],
+                                 top["ln1_b"], top["ln1_eps"], ws.x, ws.a)
+
+        n_out = (1 + len(layers)) if all_layer_embed else 1
+        res = torch.empty(n_out, B, E, dtype=torch.float32, device=dev)
+        pool = torch.empty(B, E, dtype=torch.float32, device=dev) if self.global_pool else None
+
+        def readout(slot: int):
+            if self.global_pool:
+                _hip.mean_tokens(ws.x, B, L, E, 1, pool)
+                _hip.layernorm_f32(pool, E, top["norm_w"], top["norm_b"], top["norm_eps"], res[slot], B, E)
+            else:
+                _hip.layernorm_f32(ws.x, L * E, top["norm_w"], top["norm_b"], top["norm_eps"], res[slot], B, E)
+
+        if all_layer_embed:
+            readout(0)
+        eng.run_layers(ws, B, L, readout if all_layer_embed else None)
+        if not all_layer_embed:
+            if self.global_pool:
+                _hip.layernorm_f32(ws.x, E, top["enc_w"], top["enc_b"], top["enc_eps"], ws.x, M, E)
+                readout(0)
+            else:
+                cls_rows = torch.empty(B, E, dtype=torch.float32, device=dev)
+                _hip.layernorm_f32(ws.x, L * E, top["enc_w"], top["enc_b"], top["enc_eps"], cls_rows, B, E)
+                _hip.layernorm_f32(cls_rows, E, top["norm_w"], top["norm_b"], top["norm_eps"], res[0], B, E)
+        out_dtype = self.norm.weight.dtype
+        return [res[i].to(out_dtype) for i in range(n_out)]
+
+
+def create_model(pretrained: str, model_arch: str, in_chans: int,
+                 local_dir: str = os.path.join(os.path.expanduser("~"), ".cache/"), **kwargs):
+    """Build a registered slide encoder and (optionally) load ``{"model": state_dict}`` weights
+    with strict=False semantics (reference :226-252)."""
+    if model_arch not in _REGISTRY:
+        raise RuntimeError("Unknown model (%s)" % model_arch)
+    model = _REGISTRY[model_arch](in_chans=in_chans, **kwargs)
+    if pretrained.startswith("hf_hub:"):
+        import huggingface_hub
+        hub_name = pretrained.split(":")[1]
+        huggingface_hub.hf_hub_download(hub_name, filename="slide_encoder.pth", local_dir=local_dir,
+                                        force_download=True)
+        local_path = os.path.join(local_dir, "slide_encoder.pth")
+    else:
+        local_path = pretrained
+    if os.path.exists(local_path):
+        state_dict = torch.load(local_path, map_location="cpu", weights_only=True)["model"]
+        missing_keys, unexpected_keys = model.load_state_dict(state_dict, strict=False)
+        for k in missing_keys:
+            print("Missing ", k)
+        for k in unexpected_keys:
+            print("Unexpected ", k)
+        print("\033[92m Successfully Loaded Pretrained GigaPath model from {} \033[00m".format(pretrained))
+    else:
+        print("\033[93m Pretrained weights not found at {}. Randomly initialized the model! \033[00m".format(local_path))
+    return model
+
+
+@register_model
+def gigapath_slide_enc12l768d(**kwargs):
+    return LongNetViT(embed_dim=768, depth=12, mlp_ratio=4, norm_layer=partial(nn.LayerNorm, eps=1e-6), **kwargs)
+
+
+@register_model
+def gigapath_slide_enc24l1024d(**kwargs):
+    return LongNetViT(embed_dim=1024, depth=24, mlp_ratio=4, norm_layer=partial(nn.LayerNorm, eps=1e-6), **kwargs)
+
+
+@register_model
+def gigapath_slide_enc12l1536d(**kwargs):
+    return LongNetViT(embed_dim=1536, depth=12, mlp_ratio=4, norm_layer=partial(nn.LayerNorm, eps=1e-6), **kwargs)

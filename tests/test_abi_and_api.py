@@ -1,0 +1,152 @@
+"""CPU-side checks of the product: the C-ABI library loads and exports every symbol the header
+declares, and the Python drop-in mirrors the reference API (no GPU needed, no compute calls)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, PKG_ROOT, ROOT, load_golden
+
+HEADER = os.path.join(ROOT, "include", "gigapath_hip.h")
+
+
+def _lib_path():
+    from gigapath import _hip
+    if not os.path.exists(_hip.LIB_PATH):
+        subprocess.run(["make", "-C", os.path.join(PKG_ROOT, "csrc"), "-j8"], check=True,
+                       stdout=subprocess.DEVNULL)
+    return _hip.LIB_PATH
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(gp_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_expected_entry_points():
+    fns = header_functions()
+    for f in ("gp_coords_to_pos", "gp_posembed_cls_ln", "gp_dilated_gather", "gp_dilated_attn_fwd",
+              "gp_seg_attn_fwd", "gp_branch_merge_ln", "gp_residual_layernorm", "gp_gelu_layernorm",
+              "gp_layernorm_f32", "gp_mean_tokens", "gp_abi_version", "gp_last_error_string"):
+        assert f in fns
+
+
+def test_library_exports_every_header_symbol():
+    path = _lib_path()
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (gp_[a-z0-9_]+)", out))
+    missing = [f for f in header_functions() if f not in exported]
+    assert not missing, missing
+
+
+def test_library_loads_and_binding_covers_header():
+    _lib_path()
+    from gigapath import _hip
+    lib = _hip.load_library()
+    assert lib.gp_abi_version() == _hip.ABI_VERSION
+    assert set(_hip.SIGNATURES) == set(header_functions())
+    assert lib.gp_last_error_string() == b""
+
+
+def test_library_is_gfx950_code():
+    blob = open(_lib_path(), "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob          # embedded code-object target id
+
+
+def test_argument_errors_are_reported_without_gpu():
+    """Bad arguments are rejected on the host before any launch (GP_EARG + message)."""
+    _lib_path()
+    from gigapath import _hip
+    lib = _hip.load_library()
+    rc = lib.gp_dilated_attn_fwd(None, None, None, 0, 1, 10, 16, 40, None, None, 1, None, None, 0.0, None)
+    assert rc == -1
+    assert b"head dim 40" in lib.gp_last_error_string()
+    rc = lib.gp_residual_layernorm(None, None, None, None, None, 1e-5, None, 4, 100, None)
+    assert rc == -1 and b"cols=100" in lib.gp_last_error_string()
+
+
+# ------------------------------------------------------------------ Python drop-in surface
+@pytest.fixture(scope="module")
+def model():
+    from gigapath import slide_encoder
+    return slide_encoder.create_model("", "gigapath_slide_enc12l768d", 1536)
+
+
+def test_state_dict_matches_reference(model, golden_meta):
+    sd = model.state_dict()
+    assert [[k, list(v.shape)] for k, v in sd.items()] == golden_meta["state_dict"]
+    assert sum(p.numel() for p in model.parameters()) == 86330880
+
+
+def test_registered_architectures():
+    from gigapath import slide_encoder
+    assert slide_encoder.list_models() == ["gigapath_slide_enc12l1536d", "gigapath_slide_enc12l768d",
+                                           "gigapath_slide_enc24l1024d"]
+    with pytest.raises(RuntimeError):
+        slide_encoder.create_model("", "no_such_model", 1536)
+
+
+def test_segment_schedule_and_config(model, golden_meta):
+    args = model.encoder.layers[0].self_attn.args
+    assert args.segment_length == [1024, 5792, 32768, 185363, 1048576]
+    assert args.dilated_ratio == [1, 2, 4, 8, 16]
+    for mw, segs in golden_meta["schedules"].items():
+        assert eval(model.get_optimal_segment_length(int(mw), 256)) == segs
+
+
+def test_loads_seeded_weights_strict(model):
+    import oracle
+    W = oracle.make_weights(oracle.arch_config("gigapath_slide_enc12l768d"), seed=0)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()}, strict=True)
+
+
+def test_create_model_loads_checkpoint(tmp_path, capsys):
+    import oracle
+    from gigapath import slide_encoder
+    W = oracle.make_weights(oracle.arch_config("gigapath_slide_enc12l768d"), seed=0)
+    sd = {k: torch.from_numpy(v) for k, v in W.items()}
+    sd.pop("norm.bias")
+    sd["extra.key"] = torch.zeros(1)
+    p = tmp_path / "slide_encoder.pth"
+    torch.save({"model": sd}, p)
+    m = slide_encoder.create_model(str(p), "gigapath_slide_enc12l768d", 1536)
+    out = capsys.readouterr().out
+    assert "Missing  norm.bias" in out and "Unexpected  extra.key" in out
+    assert torch.equal(m.cls_token, sd["cls_token"])
+
+
+def test_pos_table_product_bit_exact():
+    from gigapath.pos_embed import axis_table
+    import oracle
+    g = load_golden("pos_embed_rows.npz")
+    ours = oracle.pos_embed_rows(g["rows"], axis_table(768, 1000), 1000)
+    assert np.array_equal(ours.view(np.uint32), g["values"].view(np.uint32))
+
+
+def test_product_fails_loudly_on_cpu(model):
+    model.eval()
+    x = torch.zeros(1, 4, 1536)
+    c = torch.zeros(1, 4, 2)
+    with pytest.raises(RuntimeError, match="ROCm"):
+        model(x, c)
+
+
+def test_training_mode_is_rejected(model):
+    model.train()
+    with pytest.raises(RuntimeError, match="eval"):
+        model(torch.zeros(1, 4, 1536), torch.zeros(1, 4, 2))
+    model.eval()
+
+
+def test_flops_model_matches_survey():
+    from gigapath import runtime
+    segs, ratios = [1024, 5792, 32768, 185363, 1048576], [1, 2, 4, 8, 16]
+    att = 12 * runtime.attention_valid_flops(70001, segs, ratios, 16, 48)
+    gemm = runtime.gemm_flops(1, 70000, 768, 3072, 1536, 12)
+    assert abs(att / 1e12 - 14.868) < 0.01
+    assert abs((att + gemm) / 1e12 - 26.924) < 0.01

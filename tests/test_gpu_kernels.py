@@ -1,0 +1,291 @@
+"""Kernel-level parity of the HIP path against the CPU oracle (run with -m gpu on an MI355X).
+
+Index bookkeeping (coords->pos, pos-embed add, dilated gather, merge coverage) is checked
+bit-exactly; attention / merge / norms against fp32 restatements on the SAME bf16 inputs.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle as orc
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _hip():
+    from gigapath import _hip
+    _hip.load_library()
+    return _hip
+
+
+def bf16_round(a):
+    return torch.from_numpy(np.asarray(a, dtype=np.float32)).bfloat16().float()
+
+
+# ------------------------------------------------------------------ coords -> pos
+def test_coords_to_pos_bit_exact_golden():
+    h = _hip()
+    g = load_golden("coords_to_pos.npz")
+    c = torch.from_numpy(g["coords"]).to(DEV)
+    pos = torch.empty(c.shape[:-1], dtype=torch.int64, device=DEV)
+    err = torch.zeros(1, dtype=torch.int32, device=DEV)
+    h.coords_to_pos(c, 1000, 256, pos, err)
+    assert np.array_equal(pos.cpu().numpy(), g["pos"])
+    # negative (wrapped) index -0.5/256 -> floor -1 -> p = -1000+1... stays in torch's legal range
+    assert int(err.item()) == int(((g["pos"] > 1000000) | (g["pos"] < -1000001)).sum())
+
+
+def test_coords_to_pos_f64_and_range_errors():
+    h = _hip()
+    rng = np.random.default_rng(3)
+    c = rng.random((1000, 2)) * 256000
+    c[0] = [256000.0 * 1000, 0]          # out of range -> counted
+    ct = torch.from_numpy(c).to(DEV)
+    pos = torch.empty(1000, dtype=torch.int64, device=DEV)
+    err = torch.zeros(1, dtype=torch.int32, device=DEV)
+    h.coords_to_pos(ct, 1000, 256, pos, err)
+    exp = (np.floor(c[:, 0] / 256.0) * 1000 + np.floor(c[:, 1] / 256.0)).astype(np.int64) + 1
+    assert np.array_equal(pos.cpu().numpy(), exp)
+    assert int(err.item()) == 1
+
+
+# ------------------------------------------------------------------ pos-embed + CLS + LN
+@pytest.mark.parametrize("B,N", [(1, 1000), (2, 37)])
+def test_posembed_cls_bit_exact(B, N):
+    h = _hip()
+    E, G = 768, 1000
+    rng = np.random.default_rng(B * 100 + N)
+    xp = torch.from_numpy(rng.standard_normal((B * N, E)).astype(np.float32)).bfloat16()
+    pos = rng.integers(-1000001, 1000001, size=B * N).astype(np.int64)
+    pos[:3] = [0, 1, 1000000]
+    tab = orc.sincos_axis_table(E, G)
+    cls = rng.standard_normal(E).astype(np.float32)
+    lw = (1 + 0.1 * rng.standard_normal(E)).astype(np.float32)
+    lb = (0.1 * rng.standard_normal(E)).astype(np.float32)
+    x_out = torch.empty(B * (N + 1), E, dtype=torch.float32, device=DEV)
+    ln_out = torch.empty(B * (N + 1), E, dtype=torch.bfloat16, device=DEV)
+    h.posembed_cls_ln(xp.to(DEV), torch.from_numpy(pos).to(DEV), torch.from_numpy(tab).to(DEV),
+                      torch.from_numpy(cls).to(DEV), B, N, E, G, torch.from_numpy(lw).to(DEV),
+                      torch.from_numpy(lb).to(DEV), 1e-5, x_out, ln_out)
+    ref = np.empty((B, N + 1, E), np.float32)
+    ref[:, 0] = cls
+    ref[:, 1:] = (xp.float().numpy() + orc.pos_embed_rows(pos, tab, G)).reshape(B, N, E)
+    got = x_out.cpu().numpy().reshape(B, N + 1, E)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    ln_ref = torch.nn.functional.layer_norm(torch.from_numpy(ref), (E,), torch.from_numpy(lw),
+                                            torch.from_numpy(lb), 1e-5)
+    d = (ln_out.float().cpu().view(B, N + 1, E) - ln_ref).abs().max().item()
+    assert d <= 2 ** -7 * ln_ref.abs().max().item()
+
+
+# ------------------------------------------------------------------ dilated gather (bit-exact)
+GATHER_CASES = [
+    (1, 1025, 1024, 1), (1, 1025, 5792, 2), (2, 4098, 1024, 1), (1, 4098, 32768, 4),
+    (1, 200, 90, 4), (2, 200, 120, 8), (1, 200, 1000, 16), (1, 50, 20, 3), (1, 50, 45, 5),
+    (1, 7, 1048576, 16), (1, 30001, 23170, 4),
+]
+
+
+@pytest.mark.parametrize("B,L,sl,r", GATHER_CASES)
+def test_dilated_gather_bit_exact(B, L, sl, r):
+    h = _hip()
+    H, D = 16, 48
+    E = H * D
+    rng = np.random.default_rng(L + sl + r)
+    src = torch.from_numpy(rng.standard_normal((B * L, 3 * E)).astype(np.float32)).bfloat16()
+    geo = orc.branch_geometry(L, sl, r, H)
+    dst = torch.empty(B * geo["nseg"] * H * geo["m"], D, dtype=torch.bfloat16, device=DEV)
+    h.dilated_gather(src.to(DEV), 3 * E, E, B, L, H, D, sl, r, dst)   # the K slice of a fused QKV row
+    k = src[:, E:2 * E].view(B, L, H, D)
+    ref = orc.dilated_gather(k, sl, r)                     # [B, nseg, H, m, D]
+    got = dst.cpu().view(B, geo["nseg"], H, geo["m"], D)
+    assert torch.equal(got.view(torch.int16), ref.contiguous().view(torch.int16))
+
+
+# ------------------------------------------------------------------ attention (all branches)
+def _rand_qkv(B, L, E, seed, scale=1.0):
+    rng = np.random.default_rng(seed)
+    return torch.from_numpy((scale * rng.standard_normal((B * L, 3 * E))).astype(np.float32)).bfloat16()
+
+
+def _run_attn(h, qkv, B, L, H, D, segs, ratios):
+    E = H * D
+    outs, lses = [], []
+    for sl, r in zip(segs, ratios):
+        geo = orc.branch_geometry(L, sl, r, H)
+        outs.append(torch.full((B * geo["nseg"] * geo["m"] * H * D,), float("nan"), dtype=torch.bfloat16, device=DEV))
+        lses.append(torch.full((B * geo["nseg"] * H * geo["m"],), float("nan"), dtype=torch.float32, device=DEV))
+    q = qkv.to(DEV)
+    h.dilated_attn_fwd(q, q[:, E:], q[:, 2 * E:], 3 * E, B, L, H, D, segs, ratios, outs, lses)
+    torch.cuda.synchronize()
+    return outs, lses
+
+
+def _rows_needed(L, sl, r, H):
+    """[nseg, H] number of sparse rows whose values the merge can read."""
+    geo = orc.branch_geometry(L, sl, r, H)
+    tok = orc.gather_index(L, sl, r, H)
+    c = (tok >= 0).sum(-1)
+    need = np.where(np.arange(geo["nseg"])[:, None] < geo["nseg"] - 1, geo["m"], c)
+    return need
+
+
+ATTN_CASES = [
+    ("default_1025", 1, 1025, [1024, 5792, 32768, 185363, 1048576], [1, 2, 4, 8, 16]),
+    ("custom_misaligned", 2, 200, [32, 60, 90, 120, 1000], [1, 2, 4, 8, 16]),
+    ("wsi250k_small", 1, 700, [64, 130, 250, 333, 1000], [1, 2, 4, 8, 16]),
+    ("head_pad", 1, 50, [16, 20, 45], [1, 3, 5]),
+    ("tiny", 1, 5, [1024, 5792], [1, 16]),
+]
+
+
+@pytest.mark.parametrize("name,B,L,segs,ratios", ATTN_CASES)
+def test_dilated_attention_vs_oracle(name, B, L, segs, ratios):
+    h = _hip()
+    H, D = 16, 48
+    E = H * D
+    qkv = _rand_qkv(B, L, E, seed=L)
+    outs, lses = _run_attn(h, qkv, B, L, H, D, segs, ratios)
+    q, k, v = (qkv[:, i * E:(i + 1) * E].float().view(B, L, H, D) for i in range(3))
+    for b, (sl, r) in enumerate(zip(segs, ratios)):
+        o_ref, l_ref = orc.branch_attention(q, k, v, sl, r)        # [B, nseg, H, m, D], [B, nseg, H, m]
+        geo = orc.branch_geometry(L, sl, r, H)
+        nseg, m = geo["nseg"], geo["m"]
+        o = outs[b].float().cpu().view(B, nseg, m, H, D).permute(0, 1, 3, 2, 4)
+        l = lses[b].cpu().view(B, nseg, H, m)
+        need = _rows_needed(L, sl, r, H)
+        mask = torch.from_numpy(np.arange(m)[None, None, :] < need[:, :, None])  # [nseg, H, m]
+        mask = mask.unsqueeze(0).expand(B, -1, -1, -1)
+        assert torch.isfinite(o[mask]).all() and torch.isfinite(l[mask]).all(), (name, b)
+        do = (o - o_ref).abs()[mask].max().item()
+        dl = (l - l_ref).abs()[mask].max().item()
+        assert do <= 1.2e-2 * max(1.0, o_ref.abs().max().item()), (name, b, do)
+        assert dl <= 2e-4 * max(1.0, l_ref.abs().max().item()), (name, b, dl)
+
+
+def test_attention_large_scores_and_empty_heads():
+    """Large-magnitude scores (online-softmax rescale path) and a segment with no valid keys."""
+    h = _hip()
+    B, L, H, D = 1, 300, 16, 48
+    E = H * D
+    qkv = _rand_qkv(B, L, E, seed=9, scale=4.0)
+    qkv[150:, :] *= 3.0                           # score jump mid-sequence forces rescales
+    # branch 0: last segment of 44 tokens; branch 1: s = 8 < r = 16, so heads 8..15 of every
+    # non-last segment see no real token (pad query over one zero key: out 0, lse 0 -> -1e8)
+    segs, ratios = [256, 8, 300], [1, 16, 16]
+    outs, lses = _run_attn(h, qkv, B, L, H, D, segs, ratios)
+    q, k, v = (qkv[:, i * E:(i + 1) * E].float().view(B, L, H, D) for i in range(3))
+    for b, (sl, r) in enumerate(zip(segs, ratios)):
+        o_ref, l_ref = orc.branch_attention(q, k, v, sl, r)
+        geo = orc.branch_geometry(L, sl, r, H)
+        o = outs[b].float().cpu().view(B, geo["nseg"], geo["m"], H, D).permute(0, 1, 3, 2, 4)
+        l = lses[b].cpu().view(B, geo["nseg"], H, geo["m"])
+        need = _rows_needed(L, sl, r, H)
+        mask = torch.from_numpy(np.arange(geo["m"])[None, None, :] < need[:, :, None]).unsqueeze(0)
+        mask = mask.expand(B, -1, -1, -1)
+        rel = ((o - o_ref).abs()[mask].max() / o_ref.abs()[mask].max()).item()
+        assert rel <= 1.5e-2, (b, rel)
+        assert ((l - l_ref).abs()[mask].max() / l_ref.abs()[mask].max()).item() <= 1e-4
+
+
+def test_seg_attn_fwd_operator_seam():
+    """gp_seg_attn_fwd == flash_attn_func(q, k, v) semantics: [B, L, H, D] in, (out, lse[B, H, L]) out."""
+    _hip()
+    from gigapath.torchscale.component.flash_attention import flash_attn_func
+    rng = np.random.default_rng(1)
+    B, L, H, D = 3, 517, 16, 48
+    q, k, v = (torch.from_numpy(rng.standard_normal((B, L, H, D)).astype(np.float32)).bfloat16() for _ in range(3))
+    out, lse = flash_attn_func(q.to(DEV), k.to(DEV), v.to(DEV))
+    s = torch.einsum("blhd,bmhd->bhlm", q.float(), k.float()) * D ** -0.5
+    l_ref = torch.logsumexp(s, -1)
+    o_ref = torch.einsum("bhlm,bmhd->blhd", torch.softmax(s, -1), v.float())
+    assert (out.float().cpu() - o_ref).abs().max().item() <= 1e-2
+    assert (lse.cpu() - l_ref).abs().max().item() <= 2e-4
+
+
+@pytest.mark.parametrize("D", [64, 96])
+def test_attention_other_head_dims(D):
+    """24L1024d (D=64) and 12L1536d (D=96) head dims."""
+    h = _hip()
+    B, L, H = 1, 600, 16
+    E = H * D
+    segs, ratios = [128, 256, 600], [1, 2, 4]
+    qkv = _rand_qkv(B, L, E, seed=D)
+    outs, lses = _run_attn(h, qkv, B, L, H, D, segs, ratios)
+    q, k, v = (qkv[:, i * E:(i + 1) * E].float().view(B, L, H, D) for i in range(3))
+    for b, (sl, r) in enumerate(zip(segs, ratios)):
+        o_ref, l_ref = orc.branch_attention(q, k, v, sl, r)
+        geo = orc.branch_geometry(L, sl, r, H)
+        o = outs[b].float().cpu().view(B, geo["nseg"], geo["m"], H, D).permute(0, 1, 3, 2, 4)
+        need = _rows_needed(L, sl, r, H)
+        mask = torch.from_numpy(np.arange(geo["m"])[None, None, :] < need[:, :, None]).unsqueeze(0)
+        assert (o - o_ref).abs()[mask.expand(B, -1, -1, -1)].max().item() <= 1.2e-2
+
+
+# ------------------------------------------------------------------ branch merge
+@pytest.mark.parametrize("name,B,L,segs,ratios", ATTN_CASES[:4])
+@pytest.mark.parametrize("with_ln", [False, True])
+def test_branch_merge_vs_oracle(name, B, L, segs, ratios, with_ln):
+    h = _hip()
+    H, D = 16, 48
+    E = H * D
+    rng = np.random.default_rng(L)
+    outs, lses, outs_ref, lses_ref = [], [], [], []
+    for sl, r in zip(segs, ratios):
+        geo = orc.branch_geometry(L, sl, r, H)
+        o = torch.from_numpy(rng.standard_normal((B, geo["nseg"], geo["m"], H, D)).astype(np.float32)).bfloat16()
+        l = torch.from_numpy((3 * rng.standard_normal((B, geo["nseg"], H, geo["m"]))).astype(np.float32))
+        l.view(-1)[::97] = 0.0                       # exercise lse == 0 -> -1e8 (dilated_attention.py:46)
+        outs.append(o.to(DEV).contiguous())
+        lses.append(l.to(DEV).contiguous())
+        outs_ref.append(o.float().permute(0, 1, 3, 2, 4))   # oracle layout [B, nseg, H, m, D]
+        lses_ref.append(l)
+    lw = torch.from_numpy((1 + 0.1 * rng.standard_normal(E)).astype(np.float32))
+    lb = torch.from_numpy((0.1 * rng.standard_normal(E)).astype(np.float32))
+    out = torch.empty(B * L, E, dtype=torch.bfloat16, device=DEV)
+    h.branch_merge_ln(outs, lses, segs, ratios, B, L, H, D, lw.to(DEV) if with_ln else None,
+                      lb.to(DEV) if with_ln else None, 1e-5, out)
+    ref = orc.merge_branches(outs_ref, lses_ref, L, segs, ratios)
+    if with_ln:
+        ref = torch.nn.functional.layer_norm(ref, (E,), lw, lb, 1e-5)
+    got = out.float().cpu().view(B, L, E)
+    assert (got - ref).abs().max().item() <= 2 ** -7 * max(1.0, ref.abs().max().item())
+
+
+# ------------------------------------------------------------------ row kernels
+def test_residual_gelu_layernorm_kernels():
+    h = _hip()
+    rng = np.random.default_rng(0)
+    M, E, F = 333, 768, 3072
+    x = torch.from_numpy(rng.standard_normal((M, E)).astype(np.float32))
+    y = torch.from_numpy(rng.standard_normal((M, E)).astype(np.float32)).bfloat16()
+    bias = torch.from_numpy(rng.standard_normal(E).astype(np.float32))
+    w = torch.from_numpy((1 + 0.1 * rng.standard_normal(E)).astype(np.float32))
+    b = torch.from_numpy((0.1 * rng.standard_normal(E)).astype(np.float32))
+    xd = x.to(DEV)
+    ln = torch.empty(M, E, dtype=torch.bfloat16, device=DEV)
+    h.residual_layernorm(xd, y.to(DEV), bias.to(DEV), w.to(DEV), b.to(DEV), 1e-5, ln, M, E)
+    x_ref = x + (y.float() + bias)
+    assert torch.equal(xd.cpu(), x_ref)
+    ln_ref = torch.nn.functional.layer_norm(x_ref, (E,), w, b, 1e-5)
+    assert (ln.float().cpu() - ln_ref).abs().max().item() <= 2 ** -7 * ln_ref.abs().max().item()
+
+    f = torch.from_numpy(rng.standard_normal((M, F)).astype(np.float32)).bfloat16()
+    fw = torch.from_numpy((1 + 0.1 * rng.standard_normal(F)).astype(np.float32))
+    fb = torch.from_numpy((0.1 * rng.standard_normal(F)).astype(np.float32))
+    fd = f.to(DEV)
+    h.gelu_layernorm(fd, fw.to(DEV), fb.to(DEV), 1e-5, fd, M, F)     # in place
+    f_ref = torch.nn.functional.layer_norm(torch.nn.functional.gelu(f.float()), (F,), fw, fb, 1e-5)
+    assert (fd.float().cpu() - f_ref).abs().max().item() <= 2 ** -7 * f_ref.abs().max().item()
+
+    out = torch.empty(4, E, dtype=torch.float32, device=DEV)
+    h.layernorm_f32(xd, 80 * E, w.to(DEV), b.to(DEV), 1e-6, out, 4, E)       # rows 0, 80, 160, 240
+    ref = torch.nn.functional.layer_norm(x_ref[::80][:4], (E,), w, b, 1e-6)
+    assert (out.cpu() - ref).abs().max().item() <= 1e-5
+
+    mt = torch.empty(1, E, dtype=torch.float32, device=DEV)
+    h.mean_tokens(xd, 1, M, E, 1, mt)
+    assert (mt.cpu()[0] - x_ref[1:].mean(0)).abs().max().item() <= 1e-5
