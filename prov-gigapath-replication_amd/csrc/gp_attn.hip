@@ -16,6 +16,7 @@
 //   * the reference's zero-padded keys (dilated_attention.py:85-91, unmasked in flash-attn)
 //     are added analytically at the end: n_pad * exp(0 - max) in the denominator.
 #include <math.h>
+#include <stdlib.h>
 
 #include "gp_api.h"
 #include "gp_common.h"
@@ -277,6 +278,251 @@ __global__ __launch_bounds__(256, 2) void dilated_attn_kernel(const AttnArgs a) 
 }
 
 // ---------------------------------------------------------------------------------------
+// v2: 32x32x16 MFMA formulation (D in {48, 64}).
+//   * S^T[32 keys][32 q] = K.Q^T in D/16 k-steps of v_mfma_f32_32x32x16_bf16 (no d padding);
+//     a lane owns 16 scores of ONE query per 32-key sub-tile, so the row max needs one
+//     v_permlane32_swap per tile and no LDS traffic;
+//   * O^T[d][q] += V^T[d][key] . P^T[key][q], P^T taken straight from the S^T accumulator
+//     registers (k-step s = registers 8s..8s+7), V^T from two ds_read_b64_tr_b16 per k-step;
+//     the d-tile is 64 rows: for D = 48 rows 48..63 read a constant block of bf16 ones that the
+//     V image carries, so the MFMA also produces the softmax row sum (no VALU adds);
+//   * lazy rescale (defer-max): O is rescaled only when a query's running max grows by more
+//     than 2^8 (log2 domain), so P stays <= 256 (exact in fp32 sums, bf16 relative precision);
+//   * V image: 128-byte rows of four 32-byte blocks, block b of row r stored at b ^ (r & 3),
+//     which makes the transposed reads bank-conflict free; K image: 16-byte row padding
+//     (112 / 144-byte rows) makes the 32-row ds_read_b128 fragment reads conflict free.
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+GP_DEV float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+template <int D>
+__global__ __launch_bounds__(256, 2) void dilated_attn32_kernel(const AttnArgs a) {
+  static_assert(D == 48 || D == 64, "v2 kernel covers D = 48 and 64");
+  constexpr int KS = D / 16;                 // k-steps of Q.K^T
+  constexpr bool kOnes = (D % 32) != 0;      // spare d rows carry the row-sum ones
+  constexpr int KROWB = D * 2 + 16;          // K image row bytes (padded)
+  constexpr int VROWB = 128;                 // V image row bytes (64 bf16, swizzled 32-B blocks)
+  constexpr int KTILE = kKB * KROWB;
+  constexpr int VTILE = kKB * VROWB;
+  constexpr int BUF = KTILE + VTILE;
+  constexpr int CH = D / 8;                  // 16-byte chunks per K/V row in HBM
+  constexpr int LPT = 2 * kKB * CH / 256;
+  static_assert((2 * kKB * CH) % 256 == 0, "");
+  constexpr float kThr = 8.0f;               // lazy-rescale threshold (log2 units)
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+
+  const int64_t item = xcd_group(blockIdx.x, gridDim.x);
+  int bi = 0;
+#pragma unroll
+  for (int t = 1; t < GP_MAX_BRANCHES; ++t)
+    if (t < a.nbranch && item >= a.br[t].item_begin) bi = t;
+  const GpBranch g = a.br[bi].g;
+  int64_t local = item - a.br[bi].item_begin;
+  const int nqb = a.br[bi].nqb;
+  const int qb = (int)(local % nqb);
+  local /= nqb;
+  const int hh = (int)(local % a.H);
+  const int64_t bn = local / a.H;
+  const int64_t bidx = bn / g.nseg;
+  const int n = (int)(bn % g.nseg);
+  const int j = hh / g.hpg;
+  const int c = gp_valid_rows(g, a.L, n, j);
+  const int rows_needed = (n < g.nseg - 1) ? g.m : c;
+  const int q0 = qb * kQB;
+  if (q0 >= rows_needed) return;
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int l32 = lane & 31, h = lane >> 5;
+  const int64_t tok0 = bidx * a.L + (int64_t)n * g.s + j;
+  const int64_t rstride = (int64_t)g.r * a.row_stride;
+  const uint16_t* qbase = a.q + tok0 * a.row_stride + hh * D;
+  const uint16_t* kbase = a.k + tok0 * a.row_stride + hh * D;
+  const uint16_t* vbase = a.v + tok0 * a.row_stride + hh * D;
+
+  // V images: the d-columns >= D of every row (block 3 for D = 48) hold bf16 1.0
+  if constexpr (kOnes) {
+    for (int idx = threadIdx.x; idx < 2 * kKB * 2; idx += 256) {   // 2 bufs x 64 rows x 2 chunks
+      const int buf = idx / (2 * kKB), rem = idx % (2 * kKB), row = rem >> 1, half = rem & 1;
+      const uint4 ones = make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
+      *reinterpret_cast<uint4*>(smem + buf * BUF + KTILE + row * VROWB + 32 * (3 ^ (row & 3)) + 16 * half) = ones;
+    }
+  }
+
+  // Q fragments (B operand): lane holds Q[q = l32][d = 16ks + 8h .. +7]
+  bf16x8 qf[KS];
+  {
+    const int i = q0 + w * 32 + l32;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      bf16x8 z = {};
+      if (i < c) z = *reinterpret_cast<const bf16x8*>(qbase + (int64_t)i * rstride + 16 * ks + 8 * h);
+      qf[ks] = z;
+    }
+  }
+
+  uint4 stage[LPT];
+  auto load_tile = [&](int kv0) {
+#pragma unroll
+    for (int u = 0; u < LPT; ++u) {
+      const int idx = threadIdx.x + 256 * u;
+      const int tsel = idx / (kKB * CH);
+      const int rem = idx % (kKB * CH);
+      const int row = rem / CH, ch = rem % CH;
+      const int key = kv0 + row;
+      uint4 z = make_uint4(0, 0, 0, 0);
+      if (key < c) z = *reinterpret_cast<const uint4*>((tsel ? vbase : kbase) + (int64_t)key * rstride + ch * 8);
+      stage[u] = z;
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < LPT; ++u) {
+      const int idx = threadIdx.x + 256 * u;
+      const int tsel = idx / (kKB * CH);
+      const int rem = idx % (kKB * CH);
+      const int row = rem / CH, ch = rem % CH;
+      const int off = tsel ? KTILE + row * VROWB + 32 * ((ch >> 1) ^ (row & 3)) + 16 * (ch & 1)
+                           : row * KROWB + ch * 16;
+      *reinterpret_cast<uint4*>(smem + buf * BUF + off) = stage[u];
+    }
+  };
+
+  float m_run = -INFINITY;   // running max, log2 domain, of query l32
+  float lsum = 0.f;          // row sum (VALU path, D % 32 == 0 only)
+  f32x16 oacc[2];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) oacc[mt][r] = 0.f;
+
+  const int ntiles = (c + kKB - 1) / kKB;
+  if (ntiles > 0) {
+    load_tile(0);
+    store_tile(0);
+  }
+  __syncthreads();
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int kv0 = t * kKB;
+    if (t + 1 < ntiles) load_tile(kv0 + kKB);
+    const char* Kb = smem + (t & 1) * BUF;
+    const char* Vb = Kb + KTILE;
+
+    // ---- S^T for two 32-key sub-tiles
+    f32x16 sacc[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Kb + (32 * u + l32) * KROWB + 32 * ks + 16 * h);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], acc, 0, 0, 0);
+      }
+      sacc[u] = acc;
+    }
+    if (kv0 + kKB > c) {      // keys >= c are zero pads (added analytically at the end)
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (kv0 + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * h >= c) sacc[u][r] = -INFINITY;
+    }
+
+    // ---- online softmax with deferred rescale
+    float mx = sacc[0][0];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[u][r]);
+    {
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+      mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+    }
+    const float tm = mx * a.c_log2;
+    const bool need = tm > m_run + kThr;
+    if (__builtin_amdgcn_ballot_w64(need)) {
+      const float m_new = need ? tm : m_run;
+      const float alpha = fast_exp2(m_run - m_new);
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) oacc[mt][r] *= alpha;
+      lsum *= alpha;
+      m_run = m_new;
+    }
+    bf16x8 pf[2][2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float p = fast_exp2(fmaf(sacc[u][8 * s + e], a.c_log2, -m_run));
+          if constexpr (!kOnes) lsum += p;
+          pf[u][s][e] = (__bf16)p;
+        }
+
+    // ---- O^T += V^T . P^T  (2 sub-tiles x 2 k-steps x 2 d-tiles)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int row = 32 * u + 16 * s + 4 * (lane >> 5) + ((lane >> 2) & 3);
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          const int blk = 2 * mt + ((lane >> 4) & 1);
+          const char* p0 = Vb + row * VROWB + 32 * (blk ^ (row & 3)) + 8 * (lane & 3);
+          const char* p1 = p0 + 8 * VROWB;   // rows + 8 keep (row & 3)
+          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
+          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p1);
+          const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+          oacc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[u][s], oacc[mt], 0, 0, 0);
+        }
+      }
+
+    if (t + 1 < ntiles) store_tile((t + 1) & 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue
+  float l;
+  if constexpr (kOnes) {
+    l = oacc[1][8];                       // d-row 48 (+4h): the ones row = sum_k P
+  } else {
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(lsum), __float_as_uint(lsum), false, false);
+    l = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+  }
+  const int npad = g.m - c;
+  float mr = m_run, so = 1.f;
+  if (npad > 0) {
+    const float mf = fmaxf(mr, 0.f);
+    so = fast_exp2(mr - mf);
+    l = l * so + (float)npad * fast_exp2(-mf);
+    mr = mf;
+  }
+  const float inv = so / l;
+  const int i = q0 + w * 32 + l32;
+  AttnBranch br = a.br[bi];
+  if (i < rows_needed) {
+    uint16_t* orow = br.o + ((bn * g.m + i) * a.H + hh) * (int64_t)D;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        const int d0 = 32 * mt + 8 * rg + 4 * h;
+        if (d0 < D) {
+          float vv[4] = {oacc[mt][4 * rg] * inv, oacc[mt][4 * rg + 1] * inv, oacc[mt][4 * rg + 2] * inv,
+                         oacc[mt][4 * rg + 3] * inv};
+          store_bf16<4>(orow + d0, vv);
+        }
+      }
+    if (h == 0) br.lse[(bn * a.H + hh) * (int64_t)g.m + i] = (mr + __builtin_amdgcn_logf(l)) * 0.69314718055994530942f;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 struct MergeBranch {
   GpBranch g;
   const uint16_t* o;
@@ -435,10 +681,19 @@ extern "C" int gp_dilated_attn_fwd(const uint16_t* q, const uint16_t* k, const u
   a.total_items = items;
   GP_REQUIRE(items < (int64_t)0x7fffffff, "gp_dilated_attn_fwd: too many work items");
   hipStream_t s = gp_stream(stream);
-  switch (D) {
-    case 48: dilated_attn_kernel<48><<<(unsigned)items, 256, 0, s>>>(a); break;
-    case 64: dilated_attn_kernel<64><<<(unsigned)items, 256, 0, s>>>(a); break;
-    case 96: dilated_attn_kernel<96><<<(unsigned)items, 256, 0, s>>>(a); break;
+  const char* impl_env = getenv("GP_ATTN_IMPL");   // A/B switch for benchmarking (default: v2)
+  const int impl = impl_env ? atoi(impl_env) : 2;
+  if (impl == 1 || D == 96) {
+    switch (D) {
+      case 48: dilated_attn_kernel<48><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 64: dilated_attn_kernel<64><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 96: dilated_attn_kernel<96><<<(unsigned)items, 256, 0, s>>>(a); break;
+    }
+  } else {
+    switch (D) {
+      case 48: dilated_attn32_kernel<48><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 64: dilated_attn32_kernel<64><<<(unsigned)items, 256, 0, s>>>(a); break;
+    }
   }
   return gp_check_launch("gp_dilated_attn_fwd");
 }

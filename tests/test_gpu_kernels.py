@@ -163,7 +163,12 @@ def test_dilated_attention_vs_oracle(name, B, L, segs, ratios):
         do = (o - o_ref).abs()[mask].max().item()
         dl = (l - l_ref).abs()[mask].max().item()
         assert do <= 1.2e-2 * max(1.0, o_ref.abs().max().item()), (name, b, do)
-        assert dl <= 2e-4 * max(1.0, l_ref.abs().max().item()), (name, b, dl)
+        # LSE: the softmax row sum is accumulated by the MFMA from the bf16-rounded P it also
+        # uses for P.V (relative error <= 2^-9 per term) -> |d lse| <= ~2e-3
+        assert dl <= LSE_ATOL, (name, b, dl)
+
+
+LSE_ATOL = 2.5e-3
 
 
 def test_attention_large_scores_and_empty_heads():
@@ -188,7 +193,8 @@ def test_attention_large_scores_and_empty_heads():
         mask = mask.expand(B, -1, -1, -1)
         rel = ((o - o_ref).abs()[mask].max() / o_ref.abs()[mask].max()).item()
         assert rel <= 1.5e-2, (b, rel)
-        assert ((l - l_ref).abs()[mask].max() / l_ref.abs()[mask].max()).item() <= 1e-4
+        # fp32 scores of magnitude ~1e2 differ by ~1e-5 relative between summation orders
+        assert (l - l_ref).abs()[mask].max().item() <= LSE_ATOL + 1e-4 * l_ref.abs()[mask].max().item()
 
 
 def test_seg_attn_fwd_operator_seam():
@@ -203,7 +209,7 @@ def test_seg_attn_fwd_operator_seam():
     l_ref = torch.logsumexp(s, -1)
     o_ref = torch.einsum("bhlm,bmhd->blhd", torch.softmax(s, -1), v.float())
     assert (out.float().cpu() - o_ref).abs().max().item() <= 1e-2
-    assert (lse.cpu() - l_ref).abs().max().item() <= 2e-4
+    assert (lse.cpu() - l_ref).abs().max().item() <= LSE_ATOL
 
 
 @pytest.mark.parametrize("D", [64, 96])

@@ -1,0 +1,45 @@
+"""A/B timing of gp_dilated_attn_fwd implementations on one layer's worth of random QKV.
+
+    python tools/attn_bench.py [--L 70001] [--iters 10]
+Interleaves implementations (GP_ATTN_IMPL=1/2) in one process; reports TFLOP/s on the
+algorithmic (valid-token) FLOPs of SURVEY §8(d)."""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "prov-gigapath-replication_amd"))
+import torch  # noqa: E402
+
+from gigapath import _hip, runtime  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--L", type=int, default=70001)
+ap.add_argument("--iters", type=int, default=10)
+ap.add_argument("--impls", default="1,2")
+ap.add_argument("--D", type=int, default=48)
+args = ap.parse_args()
+H, D = 16, args.D
+E = H * D
+L = args.L
+segs, ratios = [1024, 5792, 32768, 185363, 1048576], [1, 2, 4, 8, 16]
+g = torch.Generator(device="cuda").manual_seed(0)
+qkv = torch.randn(L, 3 * E, device="cuda", generator=g).to(torch.bfloat16)
+sc = runtime.AttentionScratch(torch.device("cuda"), 1, L, H, D, segs, ratios)
+flops = runtime.attention_valid_flops(L, segs, ratios, H, D)
+res = {}
+for rnd in range(args.iters):
+    for impl in args.impls.split(","):
+        os.environ["GP_ATTN_IMPL"] = impl
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        _hip.dilated_attn_fwd(qkv, qkv[:, E:], qkv[:, 2 * E:], 3 * E, 1, L, H, D, segs, ratios, sc.outs, sc.lses)
+        e1.record()
+        torch.cuda.synchronize()
+        if rnd > 0:
+            res.setdefault(impl, []).append(e0.elapsed_time(e1))
+for impl, ts in res.items():
+    ts.sort()
+    med = ts[len(ts) // 2]
+    print("impl %s: median %.3f ms  min %.3f ms  -> %.1f TFLOP/s (valid)  %.1f%% of 2.5 PF"
+          % (impl, med, ts[0], flops / med / 1e9, 100 * flops / med / 1e9 / 2500))
