@@ -75,11 +75,15 @@ int gp_dilated_gather(const uint16_t* src, int64_t row_stride, int64_t col_off, 
  *   o_out[b]:   [B*nseg_b, m_b, H, D] bf16   (flash_attn's "out" layout per segment)
  *   lse_out[b]: [B*nseg_b, H, m_b]    fp32   (natural-log LSE, flash_attn's softmax_lse)
  * Rows whose values the merge can never read (beyond the last segment's tokens) are left
- * unwritten.  softmax_scale <= 0 selects D^-0.5.  D in {48, 64, 96}. */
+ * unwritten.  softmax_scale <= 0 selects D^-0.5.  D in {48, 64, 96}.
+ * q_log2_prescaled != 0: the caller already multiplied q by softmax_scale*log2(e) (e.g. folded
+ * into the Q projection), softmax_scale is ignored and scores are used as log2-domain logits
+ * (D in {48, 64}); outputs keep the same meaning (lse stays natural-log). */
 int gp_dilated_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, int64_t row_stride,
                         int64_t B, int64_t L, int H, int D, const int32_t* seg_len,
                         const int32_t* ratios, int nbranch, uint16_t* const* o_out,
-                        float* const* lse_out, float softmax_scale, void* stream);
+                        float* const* lse_out, float softmax_scale, int q_log2_prescaled,
+                        void* stream);
 
 /* Drop-in for the operator seam flash_attn_func(q, k, v, 0.0, None, scale, False)
  * (torchscale/component/flash_attention.py:13-16): non-causal, no mask, dropout 0.

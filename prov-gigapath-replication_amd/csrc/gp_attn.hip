@@ -295,7 +295,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 GP_DEV float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
-template <int D>
+template <int D, bool kPre>
 __global__ __launch_bounds__(256, 2) void dilated_attn32_kernel(const AttnArgs a) {
   static_assert(D == 48 || D == 64, "v2 kernel covers D = 48 and 64");
   constexpr int KS = D / 16;                 // k-steps of Q.K^T
@@ -311,20 +311,21 @@ __global__ __launch_bounds__(256, 2) void dilated_attn32_kernel(const AttnArgs a
   constexpr float kThr = 8.0f;               // lazy-rescale threshold (log2 units)
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
 
-  const int64_t item = xcd_group(blockIdx.x, gridDim.x);
+  // ---- work item (32-bit index math: items < 2^31, checked on the host)
+  const int item = (int)xcd_group(blockIdx.x, gridDim.x);
   int bi = 0;
 #pragma unroll
   for (int t = 1; t < GP_MAX_BRANCHES; ++t)
-    if (t < a.nbranch && item >= a.br[t].item_begin) bi = t;
+    if (t < a.nbranch && item >= (int)a.br[t].item_begin) bi = t;
   const GpBranch g = a.br[bi].g;
-  int64_t local = item - a.br[bi].item_begin;
   const int nqb = a.br[bi].nqb;
-  const int qb = (int)(local % nqb);
+  int local = item - (int)a.br[bi].item_begin;
+  const int qb = local % nqb;
   local /= nqb;
-  const int hh = (int)(local % a.H);
-  const int64_t bn = local / a.H;
-  const int64_t bidx = bn / g.nseg;
-  const int n = (int)(bn % g.nseg);
+  const int hh = local % a.H;
+  const int bn = local / a.H;
+  const int bidx = bn / g.nseg;
+  const int n = bn - bidx * g.nseg;
   const int j = hh / g.hpg;
   const int c = gp_valid_rows(g, a.L, n, j);
   const int rows_needed = (n < g.nseg - 1) ? g.m : c;
@@ -333,7 +334,7 @@ __global__ __launch_bounds__(256, 2) void dilated_attn32_kernel(const AttnArgs a
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int l32 = lane & 31, h = lane >> 5;
-  const int64_t tok0 = bidx * a.L + (int64_t)n * g.s + j;
+  const int64_t tok0 = (int64_t)bidx * a.L + (int64_t)n * g.s + j;
   const int64_t rstride = (int64_t)g.r * a.row_stride;
   const uint16_t* qbase = a.q + tok0 * a.row_stride + hh * D;
   const uint16_t* kbase = a.k + tok0 * a.row_stride + hh * D;
@@ -408,13 +409,15 @@ __global__ __launch_bounds__(256, 2) void dilated_attn32_kernel(const AttnArgs a
     const char* Kb = smem + (t & 1) * BUF;
     const char* Vb = Kb + KTILE;
 
-    // ---- S^T for two 32-key sub-tiles
+    // ---- S^T for two 32-key sub-tiles.  kPre (q pre-multiplied by scale*log2 e): the
+    // accumulator starts at -m_run, so it already holds log2-domain scores minus the max.
     f32x16 sacc[2];
+    const float init = (kPre && t > 0) ? -m_run : 0.f;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       f32x16 acc;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+      for (int r = 0; r < 16; ++r) acc[r] = init;
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Kb + (32 * u + l32) * KROWB + 32 * ks + 16 * h);
@@ -423,6 +426,7 @@ __global__ __launch_bounds__(256, 2) void dilated_attn32_kernel(const AttnArgs a
       sacc[u] = acc;
     }
     if (kv0 + kKB > c) {      // keys >= c are zero pads (added analytically at the end)
+      // (the -inf below also holds for the kPre accumulator offset)
 #pragma unroll
       for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -430,39 +434,73 @@ __global__ __launch_bounds__(256, 2) void dilated_attn32_kernel(const AttnArgs a
           if (kv0 + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * h >= c) sacc[u][r] = -INFINITY;
     }
 
-    // ---- online softmax with deferred rescale
-    float mx = sacc[0][0];
+    // ---- online softmax with deferred rescale (two independent max chains)
+    float mxa = sacc[0][0], mxb = sacc[1][0];
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[u][r]);
+    for (int r = 1; r < 16; ++r) {
+      mxa = fmaxf(mxa, sacc[0][r]);
+      mxb = fmaxf(mxb, sacc[1][r]);
+    }
+    float mx = fmaxf(mxa, mxb);
     {
       const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
       mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
     }
-    const float tm = mx * a.c_log2;
-    const bool need = tm > m_run + kThr;
-    if (__builtin_amdgcn_ballot_w64(need)) {
-      const float m_new = need ? tm : m_run;
-      const float alpha = fast_exp2(m_run - m_new);
-#pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) oacc[mt][r] *= alpha;
-      lsum *= alpha;
-      m_run = m_new;
-    }
     bf16x8 pf[2][2];
+    if constexpr (kPre) {
+      // scores are s*c - m_run; rescale only when a query's max moved up by > kThr
+      // (tile 0: always, which sets m_run to that tile's exact max)
+      const bool need = (t == 0) || (mx > kThr);
+      if (__builtin_amdgcn_ballot_w64(need)) {
+        const float delta = need ? mx : 0.f;
+        const float alpha = fast_exp2(-delta);
+        if (t > 0) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+          for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float p = fast_exp2(fmaf(sacc[u][8 * s + e], a.c_log2, -m_run));
-          if constexpr (!kOnes) lsum += p;
-          pf[u][s][e] = (__bf16)p;
+            for (int r = 0; r < 16; ++r) oacc[mt][r] *= alpha;
+          lsum *= alpha;
         }
+        m_run = (t == 0) ? delta : m_run + delta;
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) sacc[u][r] -= delta;
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float p = fast_exp2(sacc[u][8 * s + e]);
+            if constexpr (!kOnes) lsum += p;
+            pf[u][s][e] = (__bf16)p;
+          }
+    } else {
+      const float tm = mx * a.c_log2;
+      const bool need = tm > m_run + kThr;
+      if (__builtin_amdgcn_ballot_w64(need)) {
+        const float m_new = need ? tm : m_run;
+        const float alpha = fast_exp2(m_run - m_new);
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) oacc[mt][r] *= alpha;
+        lsum *= alpha;
+        m_run = m_new;
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float p = fast_exp2(fmaf(sacc[u][8 * s + e], a.c_log2, -m_run));
+            if constexpr (!kOnes) lsum += p;
+            pf[u][s][e] = (__bf16)p;
+          }
+    }
 
     // ---- O^T += V^T . P^T  (2 sub-tiles x 2 k-steps x 2 d-tiles)
 #pragma unroll
@@ -506,7 +544,7 @@ __global__ __launch_bounds__(256, 2) void dilated_attn32_kernel(const AttnArgs a
   const int i = q0 + w * 32 + l32;
   AttnBranch br = a.br[bi];
   if (i < rows_needed) {
-    uint16_t* orow = br.o + ((bn * g.m + i) * a.H + hh) * (int64_t)D;
+    uint16_t* orow = br.o + (((int64_t)bn * g.m + i) * a.H + hh) * (int64_t)D;
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
@@ -518,7 +556,7 @@ __global__ __launch_bounds__(256, 2) void dilated_attn32_kernel(const AttnArgs a
           store_bf16<4>(orow + d0, vv);
         }
       }
-    if (h == 0) br.lse[(bn * a.H + hh) * (int64_t)g.m + i] = (mr + __builtin_amdgcn_logf(l)) * 0.69314718055994530942f;
+    if (h == 0) br.lse[((int64_t)bn * a.H + hh) * g.m + i] = (mr + __builtin_amdgcn_logf(l)) * 0.69314718055994530942f;
   }
 }
 
@@ -638,7 +676,7 @@ extern "C" int gp_dilated_gather(const uint16_t* src, int64_t row_stride, int64_
 extern "C" int gp_dilated_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, int64_t row_stride,
                                    int64_t B, int64_t L, int H, int D, const int32_t* seg_len, const int32_t* ratios,
                                    int nbranch, uint16_t* const* o_out, float* const* lse_out, float softmax_scale,
-                                   void* stream) {
+                                   int q_log2_prescaled, void* stream) {
   GP_REQUIRE(D == 48 || D == 64 || D == 96, "gp_dilated_attn_fwd: head dim %d unsupported (48, 64, 96)", D);
   GP_REQUIRE(nbranch >= 1 && nbranch <= GP_MAX_BRANCHES, "gp_dilated_attn_fwd: nbranch must be 1..%d", GP_MAX_BRANCHES);
   GP_REQUIRE(B > 0 && L > 0 && H > 0 && row_stride >= (int64_t)H * D && row_stride % 8 == 0,
@@ -652,7 +690,7 @@ extern "C" int gp_dilated_attn_fwd(const uint16_t* q, const uint16_t* k, const u
   a.H = H;
   a.nbranch = nbranch;
   const float scale = softmax_scale > 0.f ? softmax_scale : 1.0f / sqrtf((float)D);
-  a.c_log2 = scale * 1.44269504088896340736f;
+  a.c_log2 = q_log2_prescaled ? 1.0f : scale * 1.44269504088896340736f;
   // order branches by keys per work item (descending) so the longest items start first
   int order[GP_MAX_BRANCHES];
   GpBranch geo[GP_MAX_BRANCHES];
@@ -683,6 +721,7 @@ extern "C" int gp_dilated_attn_fwd(const uint16_t* q, const uint16_t* k, const u
   hipStream_t s = gp_stream(stream);
   const char* impl_env = getenv("GP_ATTN_IMPL");   // A/B switch for benchmarking (default: v2)
   const int impl = impl_env ? atoi(impl_env) : 2;
+  GP_REQUIRE(!q_log2_prescaled || (impl != 1 && D != 96), "gp_dilated_attn_fwd: q_log2_prescaled needs D in {48, 64}");
   if (impl == 1 || D == 96) {
     switch (D) {
       case 48: dilated_attn_kernel<48><<<(unsigned)items, 256, 0, s>>>(a); break;
@@ -690,9 +729,12 @@ extern "C" int gp_dilated_attn_fwd(const uint16_t* q, const uint16_t* k, const u
       case 96: dilated_attn_kernel<96><<<(unsigned)items, 256, 0, s>>>(a); break;
     }
   } else {
-    switch (D) {
-      case 48: dilated_attn32_kernel<48><<<(unsigned)items, 256, 0, s>>>(a); break;
-      case 64: dilated_attn32_kernel<64><<<(unsigned)items, 256, 0, s>>>(a); break;
+    if (q_log2_prescaled) {
+      if (D == 48) dilated_attn32_kernel<48, true><<<(unsigned)items, 256, 0, s>>>(a);
+      else dilated_attn32_kernel<64, true><<<(unsigned)items, 256, 0, s>>>(a);
+    } else {
+      if (D == 48) dilated_attn32_kernel<48, false><<<(unsigned)items, 256, 0, s>>>(a);
+      else dilated_attn32_kernel<64, false><<<(unsigned)items, 256, 0, s>>>(a);
     }
   }
   return gp_check_launch("gp_dilated_attn_fwd");
@@ -704,7 +746,7 @@ extern "C" int gp_seg_attn_fwd(const uint16_t* q, const uint16_t* k, const uint1
   GP_REQUIRE(seqlen > 0 && seqlen < (int64_t)0x7fffffff, "gp_seg_attn_fwd: bad seqlen");
   const int32_t sl = (int32_t)seqlen, r = 1;
   return gp_dilated_attn_fwd(q, k, v, (int64_t)H * D, nbatch, seqlen, H, D, &sl, &r, 1, &o, &lse, softmax_scale,
-                             stream);
+                             0, stream);
 }
 
 extern "C" int gp_branch_merge_ln(const uint16_t* const* o_in, const float* const* lse_in, const int32_t* seg_len,

@@ -28,7 +28,7 @@ SIGNATURES = {
     "gp_posembed_cls_ln": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp],
     "gp_dilated_gather": [c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp],
     "gp_dilated_attn_fwd": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp,
-                            c_f32, c_vp],
+                            c_f32, c_i32, c_vp],
     "gp_seg_attn_fwd": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i32, c_f32, c_vp, c_vp, c_vp],
     "gp_branch_merge_ln": [c_vp, c_vp, c_vp, c_vp, c_i32, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_f32, c_vp, c_vp],
     "gp_residual_layernorm": [c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_vp, c_i64, c_i32, c_vp],
@@ -130,14 +130,16 @@ def dilated_gather(src, row_stride, col_off, B, L, H, D, sl, r, dst):
            "gp_dilated_gather")
 
 
-def dilated_attn_fwd(q, k, v, row_stride, B, L, H, D, segs, ratios, outs, lses, softmax_scale=0.0):
+def dilated_attn_fwd(q, k, v, row_stride, B, L, H, D, segs, ratios, outs, lses, softmax_scale=0.0,
+                     q_log2_prescaled=False):
     lib = load_library()
     for t in (q, k, v):
         if not t.is_cuda or t.dtype != torch.bfloat16:
             raise TypeError("q/k/v must be bf16 device tensors")
     oa, la = _ptr_array(outs), _ptr_array(lses)
     _check(lib.gp_dilated_attn_fwd(_ptr(q), _ptr(k), _ptr(v), row_stride, B, L, H, D, _i32_array(segs),
-                                   _i32_array(ratios), len(segs), oa, la, float(softmax_scale), _stream()),
+                                   _i32_array(ratios), len(segs), oa, la, float(softmax_scale),
+                                   int(bool(q_log2_prescaled)), _stream()),
            "gp_dilated_attn_fwd")
 
 

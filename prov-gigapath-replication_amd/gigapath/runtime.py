@@ -110,14 +110,20 @@ def _f32(t: torch.Tensor, dev) -> torch.Tensor:
     return t.detach().to(device=dev, dtype=torch.float32).contiguous()
 
 
+LOG2E = 1.4426950408889634
+
+
 @dataclass
 class PackedAttention:
+    """Packed DilatedAttention weights.  The softmax scale D^-0.5 and log2(e) are folded into the
+    Q rows of the fused projection (in fp32, before the single bf16 rounding of the GEMM output),
+    so the attention kernel consumes log2-domain logits (gp_dilated_attn_fwd q_log2_prescaled)."""
     E: int
     H: int
     D: int
     segs: List[int]
     ratios: List[int]
-    w_qkv: torch.Tensor      # [3E, E] bf16 (q | k | v rows)
+    w_qkv: torch.Tensor      # [3E, E] bf16 (q * scale*log2e | k | v rows)
     b_qkv: torch.Tensor      # [3E] bf16
     w_o: torch.Tensor        # [E, E] bf16
     b_o: torch.Tensor        # [E] fp32 (added in the residual kernel)
@@ -126,16 +132,22 @@ class PackedAttention:
     ln_b: torch.Tensor
     ln_eps: float
 
+    prescaled: bool = True
+
     @staticmethod
     def from_module(m, dev) -> "PackedAttention":
         E, H = m.embed_dim, m.num_heads
+        D = E // H
+        qs = (D ** -0.5) * LOG2E if D in (48, 64) else 1.0   # D=96 uses the generic kernel
+        wq = m.q_proj.weight.detach().to(device=dev, dtype=torch.float32) * qs
+        bq = m.q_proj.bias.detach().to(device=dev, dtype=torch.float32) * qs
         return PackedAttention(
-            E=E, H=H, D=E // H, segs=list(m.args.segment_length), ratios=list(m.args.dilated_ratio),
-            w_qkv=_bf16(torch.cat([m.q_proj.weight, m.k_proj.weight, m.v_proj.weight], 0), dev),
-            b_qkv=_bf16(torch.cat([m.q_proj.bias, m.k_proj.bias, m.v_proj.bias], 0), dev),
+            E=E, H=H, D=D, segs=list(m.args.segment_length), ratios=list(m.args.dilated_ratio),
+            w_qkv=_bf16(torch.cat([wq, _f32(m.k_proj.weight, dev), _f32(m.v_proj.weight, dev)], 0), dev),
+            b_qkv=_bf16(torch.cat([bq, _f32(m.k_proj.bias, dev), _f32(m.v_proj.bias, dev)], 0), dev),
             w_o=_bf16(m.out_proj.weight, dev), b_o=_f32(m.out_proj.bias, dev), b_o_bf16=_bf16(m.out_proj.bias, dev),
             ln_w=_f32(m.inner_attn_ln.weight, dev), ln_b=_f32(m.inner_attn_ln.bias, dev),
-            ln_eps=float(m.inner_attn_ln.eps))
+            ln_eps=float(m.inner_attn_ln.eps), prescaled=D in (48, 64))
 
 
 @dataclass
@@ -194,7 +206,7 @@ def dilated_attention_core(pa: PackedAttention, qkv: torch.Tensor, B: int, L: in
     E, H, D = pa.E, pa.H, pa.D
     with TIMER.span("attn"):
         _hip.dilated_attn_fwd(qkv, qkv[:, E:], qkv[:, 2 * E:], 3 * E, B, L, H, D, pa.segs, pa.ratios,
-                              scratch.outs, scratch.lses)
+                              scratch.outs, scratch.lses, 0.0, pa.prescaled)
     with TIMER.span("merge"):
         _hip.branch_merge_ln(scratch.outs, scratch.lses, pa.segs, pa.ratios, B, L, H, D,
                              pa.ln_w if inner_ln else None, pa.ln_b if inner_ln else None, pa.ln_eps, out)

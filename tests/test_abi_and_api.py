@@ -63,7 +63,7 @@ def test_argument_errors_are_reported_without_gpu():
     _lib_path()
     from gigapath import _hip
     lib = _hip.load_library()
-    rc = lib.gp_dilated_attn_fwd(None, None, None, 0, 1, 10, 16, 40, None, None, 1, None, None, 0.0, None)
+    rc = lib.gp_dilated_attn_fwd(None, None, None, 0, 1, 10, 16, 40, None, None, 1, None, None, 0.0, 0, None)
     assert rc == -1
     assert b"head dim 40" in lib.gp_last_error_string()
     rc = lib.gp_residual_layernorm(None, None, None, None, None, 1e-5, None, 4, 100, None)

@@ -111,7 +111,7 @@ def _rand_qkv(B, L, E, seed, scale=1.0):
     return torch.from_numpy((scale * rng.standard_normal((B * L, 3 * E))).astype(np.float32)).bfloat16()
 
 
-def _run_attn(h, qkv, B, L, H, D, segs, ratios):
+def _run_attn(h, qkv, B, L, H, D, segs, ratios, prescaled=False):
     E = H * D
     outs, lses = [], []
     for sl, r in zip(segs, ratios):
@@ -119,7 +119,7 @@ def _run_attn(h, qkv, B, L, H, D, segs, ratios):
         outs.append(torch.full((B * geo["nseg"] * geo["m"] * H * D,), float("nan"), dtype=torch.bfloat16, device=DEV))
         lses.append(torch.full((B * geo["nseg"] * H * geo["m"],), float("nan"), dtype=torch.float32, device=DEV))
     q = qkv.to(DEV)
-    h.dilated_attn_fwd(q, q[:, E:], q[:, 2 * E:], 3 * E, B, L, H, D, segs, ratios, outs, lses)
+    h.dilated_attn_fwd(q, q[:, E:], q[:, 2 * E:], 3 * E, B, L, H, D, segs, ratios, outs, lses, 0.0, prescaled)
     torch.cuda.synchronize()
     return outs, lses
 
@@ -169,6 +169,30 @@ def test_dilated_attention_vs_oracle(name, B, L, segs, ratios):
 
 
 LSE_ATOL = 2.5e-3
+
+
+@pytest.mark.parametrize("name,B,L,segs,ratios", ATTN_CASES)
+def test_dilated_attention_prescaled_q(name, B, L, segs, ratios):
+    """Product path: q pre-multiplied by D^-0.5 * log2(e) (folded into the Q projection)."""
+    h = _hip()
+    H, D = 16, 48
+    E = H * D
+    qkv = _rand_qkv(B, L, E, seed=L + 1).float()
+    qkv[:, :E] *= D ** -0.5 * 1.4426950408889634
+    qkv = qkv.bfloat16()
+    outs, lses = _run_attn(h, qkv, B, L, H, D, segs, ratios, prescaled=True)
+    q, k, v = (qkv[:, i * E:(i + 1) * E].float().view(B, L, H, D) for i in range(3))
+    for b, (sl, r) in enumerate(zip(segs, ratios)):
+        o_ref, l_ref = orc.branch_attention(q, k, v, sl, r, scale=0.6931471805599453)
+        geo = orc.branch_geometry(L, sl, r, H)
+        o = outs[b].float().cpu().view(B, geo["nseg"], geo["m"], H, D).permute(0, 1, 3, 2, 4)
+        l = lses[b].cpu().view(B, geo["nseg"], H, geo["m"])
+        need = _rows_needed(L, sl, r, H)
+        mask = torch.from_numpy(np.arange(geo["m"])[None, None, :] < need[:, :, None]).unsqueeze(0)
+        mask = mask.expand(B, -1, -1, -1)
+        assert torch.isfinite(o[mask]).all() and torch.isfinite(l[mask]).all(), (name, b)
+        assert (o - o_ref).abs()[mask].max().item() <= 1.2e-2 * max(1.0, o_ref.abs().max().item()), (name, b)
+        assert (l - l_ref).abs()[mask].max().item() <= LSE_ATOL, (name, b)
 
 
 def test_attention_large_scores_and_empty_heads():

@@ -16,7 +16,7 @@ from gigapath import _hip, runtime  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--L", type=int, default=70001)
 ap.add_argument("--iters", type=int, default=10)
-ap.add_argument("--impls", default="1,2")
+ap.add_argument("--impls", default="1,2,2p")
 ap.add_argument("--D", type=int, default=48)
 args = ap.parse_args()
 H, D = 16, args.D
@@ -24,16 +24,19 @@ E = H * D
 L = args.L
 segs, ratios = [1024, 5792, 32768, 185363, 1048576], [1, 2, 4, 8, 16]
 g = torch.Generator(device="cuda").manual_seed(0)
-qkv = torch.randn(L, 3 * E, device="cuda", generator=g).to(torch.bfloat16)
+qkv = torch.randn(L, 3 * E, device="cuda", generator=g)
+qkv[:, :E] *= 0.35      # typical projected-q scale so pre-scaled logits stay in a realistic range
+qkv = qkv.to(torch.bfloat16)
 sc = runtime.AttentionScratch(torch.device("cuda"), 1, L, H, D, segs, ratios)
 flops = runtime.attention_valid_flops(L, segs, ratios, H, D)
 res = {}
 for rnd in range(args.iters):
     for impl in args.impls.split(","):
-        os.environ["GP_ATTN_IMPL"] = impl
+        os.environ["GP_ATTN_IMPL"] = impl.rstrip("p")
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        _hip.dilated_attn_fwd(qkv, qkv[:, E:], qkv[:, 2 * E:], 3 * E, 1, L, H, D, segs, ratios, sc.outs, sc.lses)
+        _hip.dilated_attn_fwd(qkv, qkv[:, E:], qkv[:, 2 * E:], 3 * E, 1, L, H, D, segs, ratios, sc.outs, sc.lses,
+                              0.0, impl.endswith("p"))
         e1.record()
         torch.cuda.synchronize()
         if rnd > 0:
