@@ -295,19 +295,23 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 GP_DEV float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
-template <int D, bool kPre>
-__global__ __launch_bounds__(256, 2) void dilated_attn32_kernel(const AttnArgs a) {
+template <int D, bool kPre, int NW>
+__global__ __launch_bounds__(NW * 64, 2) void dilated_attn32_kernel(const AttnArgs a) {
   static_assert(D == 48 || D == 64, "v2 kernel covers D = 48 and 64");
+  static_assert(NW == 4 || NW == 8, "");
+  constexpr int NT = NW * 64;                // threads
+  constexpr int QB = NW * 32;                // query rows per workgroup
+  constexpr int KT = 16 * NW;                // keys per staged tile (64 or 128): 3 chunks / thread
   constexpr int KS = D / 16;                 // k-steps of Q.K^T
   constexpr bool kOnes = (D % 32) != 0;      // spare d rows carry the row-sum ones
   constexpr int KROWB = D * 2 + 16;          // K image row bytes (padded)
   constexpr int VROWB = 128;                 // V image row bytes (64 bf16, swizzled 32-B blocks)
-  constexpr int KTILE = kKB * KROWB;
-  constexpr int VTILE = kKB * VROWB;
+  constexpr int KTILE = KT * KROWB;
+  constexpr int VTILE = KT * VROWB;
   constexpr int BUF = KTILE + VTILE;
   constexpr int CH = D / 8;                  // 16-byte chunks per K/V row in HBM
-  constexpr int LPT = 2 * kKB * CH / 256;
-  static_assert((2 * kKB * CH) % 256 == 0, "");
+  constexpr int LPT = 2 * KT * CH / NT;
+  static_assert((2 * KT * CH) % NT == 0, "");
   constexpr float kThr = 8.0f;               // lazy-rescale threshold (log2 units)
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
 
@@ -329,7 +333,7 @@ __global__ __launch_bounds__(256, 2) void dilated_attn32_kernel(const AttnArgs a
   const int j = hh / g.hpg;
   const int c = gp_valid_rows(g, a.L, n, j);
   const int rows_needed = (n < g.nseg - 1) ? g.m : c;
-  const int q0 = qb * kQB;
+  const int q0 = qb * QB;
   if (q0 >= rows_needed) return;
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -342,8 +346,8 @@ __global__ __launch_bounds__(256, 2) void dilated_attn32_kernel(const AttnArgs a
 
   // V images: the d-columns >= D of every row (block 3 for D = 48) hold bf16 1.0
   if constexpr (kOnes) {
-    for (int idx = threadIdx.x; idx < 2 * kKB * 2; idx += 256) {   // 2 bufs x 64 rows x 2 chunks
-      const int buf = idx / (2 * kKB), rem = idx % (2 * kKB), row = rem >> 1, half = rem & 1;
+    for (int idx = threadIdx.x; idx < 2 * KT * 2; idx += NT) {   // 2 bufs x KT rows x 2 chunks
+      const int buf = idx / (2 * KT), rem = idx % (2 * KT), row = rem >> 1, half = rem & 1;
       const uint4 ones = make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
       *reinterpret_cast<uint4*>(smem + buf * BUF + KTILE + row * VROWB + 32 * (3 ^ (row & 3)) + 16 * half) = ones;
     }
@@ -365,9 +369,9 @@ __global__ __launch_bounds__(256, 2) void dilated_attn32_kernel(const AttnArgs a
   auto load_tile = [&](int kv0) {
 #pragma unroll
     for (int u = 0; u < LPT; ++u) {
-      const int idx = threadIdx.x + 256 * u;
-      const int tsel = idx / (kKB * CH);
-      const int rem = idx % (kKB * CH);
+      const int idx = threadIdx.x + NT * u;
+      const int tsel = idx / (KT * CH);
+      const int rem = idx % (KT * CH);
       const int row = rem / CH, ch = rem % CH;
       const int key = kv0 + row;
       uint4 z = make_uint4(0, 0, 0, 0);
@@ -378,9 +382,9 @@ __global__ __launch_bounds__(256, 2) void dilated_attn32_kernel(const AttnArgs a
   auto store_tile = [&](int buf) {
 #pragma unroll
     for (int u = 0; u < LPT; ++u) {
-      const int idx = threadIdx.x + 256 * u;
-      const int tsel = idx / (kKB * CH);
-      const int rem = idx % (kKB * CH);
+      const int idx = threadIdx.x + NT * u;
+      const int tsel = idx / (KT * CH);
+      const int rem = idx % (KT * CH);
       const int row = rem / CH, ch = rem % CH;
       const int off = tsel ? KTILE + row * VROWB + 32 * ((ch >> 1) ^ (row & 3)) + 16 * (ch & 1)
                            : row * KROWB + ch * 16;
@@ -396,7 +400,7 @@ __global__ __launch_bounds__(256, 2) void dilated_attn32_kernel(const AttnArgs a
 #pragma unroll
     for (int r = 0; r < 16; ++r) oacc[mt][r] = 0.f;
 
-  const int ntiles = (c + kKB - 1) / kKB;
+  const int ntiles = (c + KT - 1) / KT;
   if (ntiles > 0) {
     load_tile(0);
     store_tile(0);
@@ -404,121 +408,125 @@ __global__ __launch_bounds__(256, 2) void dilated_attn32_kernel(const AttnArgs a
   __syncthreads();
 
   for (int t = 0; t < ntiles; ++t) {
-    const int kv0 = t * kKB;
-    if (t + 1 < ntiles) load_tile(kv0 + kKB);
-    const char* Kb = smem + (t & 1) * BUF;
-    const char* Vb = Kb + KTILE;
-
-    // ---- S^T for two 32-key sub-tiles.  kPre (q pre-multiplied by scale*log2 e): the
-    // accumulator starts at -m_run, so it already holds log2-domain scores minus the max.
-    f32x16 sacc[2];
-    const float init = (kPre && t > 0) ? -m_run : 0.f;
+    if (t + 1 < ntiles) load_tile((t + 1) * KT);
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      f32x16 acc;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] = init;
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Kb + (32 * u + l32) * KROWB + 32 * ks + 16 * h);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], acc, 0, 0, 0);
+    for (int hf = 0; hf < KT / 64; ++hf) {
+      // 64-key sub-tile; a sub-tile past c (only in the last tile) is fully masked: p = 0
+      const int sub = t * (KT / 64) + hf;
+      const int kv0 = sub * 64;
+      const char* Kb = smem + (t & 1) * BUF + hf * 64 * KROWB;
+      const char* Vb = smem + (t & 1) * BUF + KTILE + hf * 64 * VROWB;
+      // ---- S^T for two 32-key sub-tiles.  kPre (q pre-multiplied by scale*log2 e): the
+      // accumulator starts at -m_run, so it already holds log2-domain scores minus the max.
+      f32x16 sacc[2];
+      const float init = (kPre && sub > 0) ? -m_run : 0.f;
+  #pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        f32x16 acc;
+  #pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = init;
+  #pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Kb + (32 * u + l32) * KROWB + 32 * ks + 16 * h);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], acc, 0, 0, 0);
+        }
+        sacc[u] = acc;
       }
-      sacc[u] = acc;
-    }
-    if (kv0 + kKB > c) {      // keys >= c are zero pads (added analytically at the end)
-      // (the -inf below also holds for the kPre accumulator offset)
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (kv0 + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * h >= c) sacc[u][r] = -INFINITY;
-    }
+      if (kv0 + 64 > c) {      // keys >= c are zero pads (added analytically at the end)
+        // (the -inf below also holds for the kPre accumulator offset)
+  #pragma unroll
+        for (int u = 0; u < 2; ++u)
+  #pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (kv0 + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * h >= c) sacc[u][r] = -INFINITY;
+      }
 
-    // ---- online softmax with deferred rescale (two independent max chains)
-    float mxa = sacc[0][0], mxb = sacc[1][0];
-#pragma unroll
-    for (int r = 1; r < 16; ++r) {
-      mxa = fmaxf(mxa, sacc[0][r]);
-      mxb = fmaxf(mxb, sacc[1][r]);
-    }
-    float mx = fmaxf(mxa, mxb);
-    {
-      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-      mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
-    }
-    bf16x8 pf[2][2];
-    if constexpr (kPre) {
-      // scores are s*c - m_run; rescale only when a query's max moved up by > kThr
-      // (tile 0: always, which sets m_run to that tile's exact max)
-      const bool need = (t == 0) || (mx > kThr);
-      if (__builtin_amdgcn_ballot_w64(need)) {
-        const float delta = need ? mx : 0.f;
-        const float alpha = fast_exp2(-delta);
-        if (t > 0) {
-#pragma unroll
+      // ---- online softmax with deferred rescale (two independent max chains)
+      float mxa = sacc[0][0], mxb = sacc[1][0];
+  #pragma unroll
+      for (int r = 1; r < 16; ++r) {
+        mxa = fmaxf(mxa, sacc[0][r]);
+        mxb = fmaxf(mxb, sacc[1][r]);
+      }
+      float mx = fmaxf(mxa, mxb);
+      {
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+        mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+      }
+      bf16x8 pf[2][2];
+      if constexpr (kPre) {
+        // scores are s*c - m_run; rescale only when a query's max moved up by > kThr
+        // (tile 0: always, which sets m_run to that tile's exact max)
+        const bool need = (sub == 0) || (mx > kThr);
+        if (__builtin_amdgcn_ballot_w64(need)) {
+          const float delta = need ? mx : 0.f;
+          const float alpha = fast_exp2(-delta);
+          if (sub > 0) {
+  #pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+  #pragma unroll
+              for (int r = 0; r < 16; ++r) oacc[mt][r] *= alpha;
+            lsum *= alpha;
+          }
+          m_run = (sub == 0) ? delta : m_run + delta;
+  #pragma unroll
+          for (int u = 0; u < 2; ++u)
+  #pragma unroll
+            for (int r = 0; r < 16; ++r) sacc[u][r] -= delta;
+        }
+  #pragma unroll
+        for (int u = 0; u < 2; ++u)
+  #pragma unroll
+          for (int s = 0; s < 2; ++s)
+  #pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float p = fast_exp2(sacc[u][8 * s + e]);
+              if constexpr (!kOnes) lsum += p;
+              pf[u][s][e] = (__bf16)p;
+            }
+      } else {
+        const float tm = mx * a.c_log2;
+        const bool need = tm > m_run + kThr;
+        if (__builtin_amdgcn_ballot_w64(need)) {
+          const float m_new = need ? tm : m_run;
+          const float alpha = fast_exp2(m_run - m_new);
+  #pragma unroll
           for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
+  #pragma unroll
             for (int r = 0; r < 16; ++r) oacc[mt][r] *= alpha;
           lsum *= alpha;
+          m_run = m_new;
         }
-        m_run = (t == 0) ? delta : m_run + delta;
-#pragma unroll
+  #pragma unroll
         for (int u = 0; u < 2; ++u)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) sacc[u][r] -= delta;
+  #pragma unroll
+          for (int s = 0; s < 2; ++s)
+  #pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float p = fast_exp2(fmaf(sacc[u][8 * s + e], a.c_log2, -m_run));
+              if constexpr (!kOnes) lsum += p;
+              pf[u][s][e] = (__bf16)p;
+            }
       }
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float p = fast_exp2(sacc[u][8 * s + e]);
-            if constexpr (!kOnes) lsum += p;
-            pf[u][s][e] = (__bf16)p;
-          }
-    } else {
-      const float tm = mx * a.c_log2;
-      const bool need = tm > m_run + kThr;
-      if (__builtin_amdgcn_ballot_w64(need)) {
-        const float m_new = need ? tm : m_run;
-        const float alpha = fast_exp2(m_run - m_new);
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) oacc[mt][r] *= alpha;
-        lsum *= alpha;
-        m_run = m_new;
-      }
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float p = fast_exp2(fmaf(sacc[u][8 * s + e], a.c_log2, -m_run));
-            if constexpr (!kOnes) lsum += p;
-            pf[u][s][e] = (__bf16)p;
-          }
-    }
 
-    // ---- O^T += V^T . P^T  (2 sub-tiles x 2 k-steps x 2 d-tiles)
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int row = 32 * u + 16 * s + 4 * (lane >> 5) + ((lane >> 2) & 3);
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
-          const int blk = 2 * mt + ((lane >> 4) & 1);
-          const char* p0 = Vb + row * VROWB + 32 * (blk ^ (row & 3)) + 8 * (lane & 3);
-          const char* p1 = p0 + 8 * VROWB;   // rows + 8 keep (row & 3)
-          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
-          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p1);
-          const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-          oacc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[u][s], oacc[mt], 0, 0, 0);
+      // ---- O^T += V^T . P^T  (2 sub-tiles x 2 k-steps x 2 d-tiles)
+  #pragma unroll
+      for (int u = 0; u < 2; ++u)
+  #pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const int row = 32 * u + 16 * s + 4 * (lane >> 5) + ((lane >> 2) & 3);
+  #pragma unroll
+          for (int mt = 0; mt < 2; ++mt) {
+            const int blk = 2 * mt + ((lane >> 4) & 1);
+            const char* p0 = Vb + row * VROWB + 32 * (blk ^ (row & 3)) + 8 * (lane & 3);
+            const char* p1 = p0 + 8 * VROWB;   // rows + 8 keep (row & 3)
+            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
+            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p1);
+            const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+            oacc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[u][s], oacc[mt], 0, 0, 0);
+          }
         }
-      }
+    }
 
     if (t + 1 < ntiles) store_tile((t + 1) & 1);
     __syncthreads();
@@ -704,12 +712,17 @@ extern "C" int gp_dilated_attn_fwd(const uint16_t* q, const uint16_t* k, const u
     for (int y = x; y > 0 && geo[order[y]].m > geo[order[y - 1]].m; --y) {
       int tmp = order[y]; order[y] = order[y - 1]; order[y - 1] = tmp;
     }
+  const char* impl_env = getenv("GP_ATTN_IMPL");   // A/B switch for benchmarking
+  const int impl = (D == 96) ? 1 : (impl_env ? atoi(impl_env) : 2);
+  GP_REQUIRE(impl == 1 || impl == 2 || impl == 4, "gp_dilated_attn_fwd: GP_ATTN_IMPL must be 1, 2 or 4");
+  GP_REQUIRE(!q_log2_prescaled || impl != 1, "gp_dilated_attn_fwd: q_log2_prescaled needs D in {48, 64}");
+  const int qblk = (impl == 4) ? 256 : 128;       // query rows per workgroup
   int64_t items = 0;
   for (int x = 0; x < nbranch; ++x) {
     const int b = order[x];
     AttnBranch& e = a.br[x];
     e.g = geo[b];
-    e.nqb = (geo[b].m + kQB - 1) / kQB;
+    e.nqb = (geo[b].m + qblk - 1) / qblk;
     e.item_begin = items;
     e.o = o_out[b];
     e.lse = lse_out[b];
@@ -719,22 +732,27 @@ extern "C" int gp_dilated_attn_fwd(const uint16_t* q, const uint16_t* k, const u
   a.total_items = items;
   GP_REQUIRE(items < (int64_t)0x7fffffff, "gp_dilated_attn_fwd: too many work items");
   hipStream_t s = gp_stream(stream);
-  const char* impl_env = getenv("GP_ATTN_IMPL");   // A/B switch for benchmarking (default: v2)
-  const int impl = impl_env ? atoi(impl_env) : 2;
-  GP_REQUIRE(!q_log2_prescaled || (impl != 1 && D != 96), "gp_dilated_attn_fwd: q_log2_prescaled needs D in {48, 64}");
-  if (impl == 1 || D == 96) {
+  if (impl == 1) {
     switch (D) {
       case 48: dilated_attn_kernel<48><<<(unsigned)items, 256, 0, s>>>(a); break;
       case 64: dilated_attn_kernel<64><<<(unsigned)items, 256, 0, s>>>(a); break;
       case 96: dilated_attn_kernel<96><<<(unsigned)items, 256, 0, s>>>(a); break;
     }
+  } else if (impl == 2) {
+    if (q_log2_prescaled) {
+      if (D == 48) dilated_attn32_kernel<48, true, 4><<<(unsigned)items, 256, 0, s>>>(a);
+      else dilated_attn32_kernel<64, true, 4><<<(unsigned)items, 256, 0, s>>>(a);
+    } else {
+      if (D == 48) dilated_attn32_kernel<48, false, 4><<<(unsigned)items, 256, 0, s>>>(a);
+      else dilated_attn32_kernel<64, false, 4><<<(unsigned)items, 256, 0, s>>>(a);
+    }
   } else {
     if (q_log2_prescaled) {
-      if (D == 48) dilated_attn32_kernel<48, true><<<(unsigned)items, 256, 0, s>>>(a);
-      else dilated_attn32_kernel<64, true><<<(unsigned)items, 256, 0, s>>>(a);
+      if (D == 48) dilated_attn32_kernel<48, true, 8><<<(unsigned)items, 512, 0, s>>>(a);
+      else dilated_attn32_kernel<64, true, 8><<<(unsigned)items, 512, 0, s>>>(a);
     } else {
-      if (D == 48) dilated_attn32_kernel<48, false><<<(unsigned)items, 256, 0, s>>>(a);
-      else dilated_attn32_kernel<64, false><<<(unsigned)items, 256, 0, s>>>(a);
+      if (D == 48) dilated_attn32_kernel<48, false, 8><<<(unsigned)items, 512, 0, s>>>(a);
+      else dilated_attn32_kernel<64, false, 8><<<(unsigned)items, 512, 0, s>>>(a);
     }
   }
   return gp_check_launch("gp_dilated_attn_fwd");

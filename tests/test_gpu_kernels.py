@@ -142,8 +142,14 @@ ATTN_CASES = [
 ]
 
 
+@pytest.fixture(params=["1", "2", "4"])
+def attn_impl(request, monkeypatch):
+    monkeypatch.setenv("GP_ATTN_IMPL", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("name,B,L,segs,ratios", ATTN_CASES)
-def test_dilated_attention_vs_oracle(name, B, L, segs, ratios):
+def test_dilated_attention_vs_oracle(name, B, L, segs, ratios, attn_impl):
     h = _hip()
     H, D = 16, 48
     E = H * D
@@ -171,8 +177,10 @@ def test_dilated_attention_vs_oracle(name, B, L, segs, ratios):
 LSE_ATOL = 2.5e-3
 
 
+@pytest.mark.parametrize("impl", ["2", "4"])
 @pytest.mark.parametrize("name,B,L,segs,ratios", ATTN_CASES)
-def test_dilated_attention_prescaled_q(name, B, L, segs, ratios):
+def test_dilated_attention_prescaled_q(name, B, L, segs, ratios, impl, monkeypatch):
+    monkeypatch.setenv("GP_ATTN_IMPL", impl)
     """Product path: q pre-multiplied by D^-0.5 * log2(e) (folded into the Q projection)."""
     h = _hip()
     H, D = 16, 48
@@ -195,7 +203,7 @@ def test_dilated_attention_prescaled_q(name, B, L, segs, ratios):
         assert (l - l_ref).abs()[mask].max().item() <= LSE_ATOL, (name, b)
 
 
-def test_attention_large_scores_and_empty_heads():
+def test_attention_large_scores_and_empty_heads(attn_impl):
     """Large-magnitude scores (online-softmax rescale path) and a segment with no valid keys."""
     h = _hip()
     B, L, H, D = 1, 300, 16, 48
@@ -237,7 +245,7 @@ def test_seg_attn_fwd_operator_seam():
 
 
 @pytest.mark.parametrize("D", [64, 96])
-def test_attention_other_head_dims(D):
+def test_attention_other_head_dims(D, attn_impl):
     """24L1024d (D=64) and 12L1536d (D=96) head dims."""
     h = _hip()
     B, L, H = 1, 600, 16

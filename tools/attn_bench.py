@@ -16,7 +16,7 @@ from gigapath import _hip, runtime  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--L", type=int, default=70001)
 ap.add_argument("--iters", type=int, default=10)
-ap.add_argument("--impls", default="1,2,2p")
+ap.add_argument("--impls", default="2p,4p")
 ap.add_argument("--D", type=int, default=48)
 args = ap.parse_args()
 H, D = 16, args.D
