@@ -585,59 +585,64 @@ struct MergeArgs {
   uint16_t* out;
 };
 
+// One wave per token; lane l owns the EPL = E/64 contiguous elements [l*EPL, (l+1)*EPL) of
+// head l*EPL/D (EPL divides D).  Everything that depends only on the token (segment n, sparse
+// row i, dilation phase of each branch) is wave-uniform 32-bit scalar math; only the
+// coverage test "head/hpg == phase" is per lane.
 template <int EPL>
 __global__ __launch_bounds__(256) void branch_merge_kernel(const MergeArgs a) {
   const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= a.B * a.L) return;
-  const int64_t bidx = row / a.L, p = row % a.L;
+  const int row = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + (int)(threadIdx.x >> 6));
+  if (row >= (int)(a.B * a.L)) return;
+  const int L = (int)a.L;
+  const int bidx = row / L, p = row - bidx * L;
   const int col0 = lane * EPL;
-  const int hh = col0 / a.D, dcol = col0 % a.D;
+  const int hh = col0 / a.D;
 
   float lse[GP_MAX_BRANCHES];
-  int64_t off[GP_MAX_BRANCHES];
   float mx = -INFINITY;
 #pragma unroll
   for (int b = 0; b < GP_MAX_BRANCHES; ++b) {
     lse[b] = -1e8f;
-    off[b] = -1;
     if (b < a.nbranch) {
       const GpBranch g = a.br[b].g;
-      const int64_t n = p / g.g, t = p % g.g;
-      const int64_t i = t / g.r;
-      const int jj = (int)(t % g.r);
-      if (hh / g.hpg == jj) {   // sparse_to_dense: covered heads of this dense slot
-        const int64_t sn = bidx * g.nseg + n;
-        float v = a.br[b].lse[(sn * a.H + hh) * (int64_t)g.m + i];
-        lse[b] = (v == 0.f) ? -1e8f : v;      // dilated_attention.py:46
-        off[b] = ((sn * g.m + i) * a.H + hh) * (int64_t)a.D + dcol;
+      const int n = p / g.g, t = p - n * g.g;       // sparse_to_dense slot of token p
+      const int i = t / g.r, jj = t - i * g.r;
+      if (hh / g.hpg == jj) {
+        const float v = a.br[b].lse[((int64_t)(bidx * g.nseg + n) * a.H + hh) * g.m + i];
+        lse[b] = (v == 0.f) ? -1e8f : v;             // dilated_attention.py:46
       }
       mx = fmaxf(mx, lse[b]);
     }
   }
   float wsum = 0.f;
 #pragma unroll
-  for (int b = 0; b < GP_MAX_BRANCHES; ++b) {
+  for (int b = 0; b < GP_MAX_BRANCHES; ++b)
     if (b < a.nbranch) {
       lse[b] = expf(lse[b] - mx);
       wsum += lse[b];
     }
-  }
+  const float inv = 1.0f / wsum;
   float acc[EPL];
 #pragma unroll
   for (int e = 0; e < EPL; ++e) acc[e] = 0.f;
 #pragma unroll
   for (int b = 0; b < GP_MAX_BRANCHES; ++b) {
-    if (b < a.nbranch && off[b] >= 0) {
-      const float wb = lse[b] / wsum;
-      float ov[EPL];
-      load_bf16<EPL>(a.br[b].o + off[b], ov);
+    if (b < a.nbranch) {
+      const GpBranch g = a.br[b].g;
+      const int n = p / g.g, t = p - n * g.g;
+      const int i = t / g.r, jj = t - i * g.r;
+      if (hh / g.hpg == jj) {
+        const float wb = lse[b] * inv;
+        float ov[EPL];
+        load_bf16<EPL>(a.br[b].o + ((int64_t)(bidx * g.nseg + n) * g.m + i) * (a.H * a.D) + col0, ov);
 #pragma unroll
-      for (int e = 0; e < EPL; ++e) acc[e] += ov[e] * wb;
+        for (int e = 0; e < EPL; ++e) acc[e] += ov[e] * wb;
+      }
     }
   }
   if (a.ln_w != nullptr) wave_layernorm<EPL>(acc, a.E, a.ln_w, a.ln_b, a.eps, col0);
-  store_bf16<EPL>(a.out + row * a.E + col0, acc);
+  store_bf16<EPL>(a.out + (int64_t)row * a.E + col0, acc);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -772,8 +777,8 @@ extern "C" int gp_branch_merge_ln(const uint16_t* const* o_in, const float* cons
                                   const float* ln_w, const float* ln_b, float eps, uint16_t* out, void* stream) {
   const int E = H * D;
   GP_REQUIRE(nbranch >= 1 && nbranch <= GP_MAX_BRANCHES, "gp_branch_merge_ln: nbranch must be 1..%d", GP_MAX_BRANCHES);
-  GP_REQUIRE(E % 64 == 0 && (E / 64 == 12 || E / 64 == 16 || E / 64 == 24) && D % (E / 64) == 0,
-             "gp_branch_merge_ln: H*D=%d unsupported", E);
+  GP_REQUIRE((E == 768 || E == 1024 || E == 1536) && D % (E / 64) == 0, "gp_branch_merge_ln: H*D=%d unsupported", E);
+  GP_REQUIRE(B * L < (int64_t)0x7fffffff, "gp_branch_merge_ln: B*L too large");
   GP_REQUIRE(B > 0 && L > 0, "gp_branch_merge_ln: bad sizes");
   GP_REQUIRE(o_in && lse_in && seg_len && ratios && out, "gp_branch_merge_ln: null pointer");
   GP_REQUIRE(ln_w == nullptr || ln_b != nullptr, "gp_branch_merge_ln: ln_w without ln_b");
@@ -787,12 +792,12 @@ extern "C" int gp_branch_merge_ln(const uint16_t* const* o_in, const float* cons
   }
   for (int b = nbranch; b < GP_MAX_BRANCHES; ++b) a.br[b] = a.br[nbranch - 1];
   a.ln_w = ln_w; a.ln_b = ln_b; a.eps = eps; a.out = out;
-  const unsigned nb = (unsigned)((B * L + 3) / 4);
+  const unsigned nb = (unsigned)((B * L + 3) / 4);   // one token per wave
   hipStream_t s = gp_stream(stream);
-  switch (E / 64) {
-    case 12: branch_merge_kernel<12><<<nb, 256, 0, s>>>(a); break;
-    case 16: branch_merge_kernel<16><<<nb, 256, 0, s>>>(a); break;
-    case 24: branch_merge_kernel<24><<<nb, 256, 0, s>>>(a); break;
+  switch (E) {
+    case 768: branch_merge_kernel<12><<<nb, 256, 0, s>>>(a); break;
+    case 1024: branch_merge_kernel<16><<<nb, 256, 0, s>>>(a); break;
+    case 1536: branch_merge_kernel<24><<<nb, 256, 0, s>>>(a); break;
   }
   return gp_check_launch("gp_branch_merge_ln");
 }

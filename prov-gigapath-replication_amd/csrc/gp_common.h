@@ -71,6 +71,89 @@ GP_DEV void store_f32(float* p, const float* v) {
   for (int i = 0; i < N / 4; ++i) q[i] = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
 }
 
+// Coalesced row mappings for one 64-lane wave.
+//   "x4":  lane owns elements k*256 + 4*lane + {0..3}, k < EPL/4 (fp32: 16-B, bf16: 8-B accesses;
+//          every wave-instruction touches one contiguous 1 KiB / 512 B span)
+//   "x8":  lane owns elements k*512 + 8*lane + {0..7}, k < EPL/8 (bf16: 16-B accesses)
+template <int EPL>
+GP_DEV void ld_x4_f32(const float* row, int lane, float* v) {
+#pragma unroll
+  for (int k = 0; k < EPL / 4; ++k) {
+    const float4 u = *reinterpret_cast<const float4*>(row + k * 256 + 4 * lane);
+    v[4 * k] = u.x; v[4 * k + 1] = u.y; v[4 * k + 2] = u.z; v[4 * k + 3] = u.w;
+  }
+}
+template <int EPL>
+GP_DEV void st_x4_f32(float* row, int lane, const float* v) {
+#pragma unroll
+  for (int k = 0; k < EPL / 4; ++k)
+    *reinterpret_cast<float4*>(row + k * 256 + 4 * lane) = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+}
+template <int EPL>
+GP_DEV void ld_x4_bf16(const uint16_t* row, int lane, float* v) {
+#pragma unroll
+  for (int k = 0; k < EPL / 4; ++k) load_bf16<4>(row + k * 256 + 4 * lane, v + 4 * k);
+}
+template <int EPL>
+GP_DEV void st_x4_bf16(uint16_t* row, int lane, const float* v) {
+#pragma unroll
+  for (int k = 0; k < EPL / 4; ++k) store_bf16<4>(row + k * 256 + 4 * lane, v + 4 * k);
+}
+template <int EPL>
+GP_DEV void ld_x8_bf16(const uint16_t* row, int lane, float* v) {
+#pragma unroll
+  for (int k = 0; k < EPL / 8; ++k) {
+    const uint4 u = *reinterpret_cast<const uint4*>(row + k * 512 + 8 * lane);
+    const uint32_t w4[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[8 * k + 2 * i] = __uint_as_float(w4[i] << 16);
+      v[8 * k + 2 * i + 1] = __uint_as_float(w4[i] & 0xffff0000u);
+    }
+  }
+}
+template <int EPL>
+GP_DEV void st_x8_bf16(uint16_t* row, int lane, const float* v) {
+#pragma unroll
+  for (int k = 0; k < EPL / 8; ++k) {
+    uint4 u;
+    u.x = (uint32_t)f2bf(v[8 * k + 0]) | ((uint32_t)f2bf(v[8 * k + 1]) << 16);
+    u.y = (uint32_t)f2bf(v[8 * k + 2]) | ((uint32_t)f2bf(v[8 * k + 3]) << 16);
+    u.z = (uint32_t)f2bf(v[8 * k + 4]) | ((uint32_t)f2bf(v[8 * k + 5]) << 16);
+    u.w = (uint32_t)f2bf(v[8 * k + 6]) | ((uint32_t)f2bf(v[8 * k + 7]) << 16);
+    *reinterpret_cast<uint4*>(row + k * 512 + 8 * lane) = u;
+  }
+}
+template <int EPL>
+GP_DEV void ld_x8_f32(const float* row, int lane, float* v) {
+#pragma unroll
+  for (int k = 0; k < EPL / 8; ++k) {
+    const float4 a = *reinterpret_cast<const float4*>(row + k * 512 + 8 * lane);
+    const float4 b = *reinterpret_cast<const float4*>(row + k * 512 + 8 * lane + 4);
+    v[8 * k] = a.x; v[8 * k + 1] = a.y; v[8 * k + 2] = a.z; v[8 * k + 3] = a.w;
+    v[8 * k + 4] = b.x; v[8 * k + 5] = b.y; v[8 * k + 6] = b.z; v[8 * k + 7] = b.w;
+  }
+}
+
+// LayerNorm statistics + affine on register-resident values (any lane mapping; w/b in the
+// same mapping as v).  torch semantics: biased variance, two-pass, fp32.
+template <int EPL>
+GP_DEV void wave_layernorm_regs(float* v, int cols, const float* w, const float* b, float eps) {
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) s += v[i];
+  const float mean = wave_sum(s) / (float)cols;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) {
+    const float d = v[i] - mean;
+    q += d * d;
+  }
+  const float rstd = rsqrtf(wave_sum(q) / (float)cols + eps);
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) v[i] = (v[i] - mean) * rstd * w[i] + b[i];
+}
+
 // LayerNorm of one row held as EPL values per lane across a 64-lane wave (torch semantics:
 // biased variance, y = (x - mean) / sqrt(var + eps) * w + b), fp32 throughout.
 template <int EPL>

@@ -37,39 +37,56 @@ __global__ void coords_to_pos_kernel(const T* __restrict__ coords, int64_t n, T 
 }
 
 // ---------------------------------------------------------------------------------------
+// Row kernels: one wave per row, "x4"/"x8" coalesced lane mappings (gp_common.h), grid-stride
+// over rows with the per-column parameters (LN affine, biases) held in registers.
+constexpr int kMaxRowBlocks = 1 << 20;   // one row per wave: loads of many rows in flight
+
+inline unsigned row_grid(int64_t rows) {
+  const int64_t nb = (rows + kRowsPerBlock - 1) / kRowsPerBlock;
+  return (unsigned)(nb < kMaxRowBlocks ? nb : kMaxRowBlocks);
+}
+
 template <int EPL>
 __global__ __launch_bounds__(256) void posembed_cls_ln_kernel(
     const uint16_t* __restrict__ xp, const int64_t* __restrict__ pos, const float* __restrict__ tab,
     const float* __restrict__ cls, int64_t B, int64_t N, int E, int G, const float* __restrict__ ln_w,
     const float* __restrict__ ln_b, float eps, float* __restrict__ x_out, uint16_t* __restrict__ ln_out) {
   const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
-  if (row >= B * (N + 1)) return;
-  const int64_t b = row / (N + 1), t = row % (N + 1);
-  const int col0 = lane * EPL;
-  float v[EPL];
-  if (t == 0) {
-    load_f32<EPL>(cls + col0, v);
-  } else {
-    load_bf16<EPL>(xp + ((b * N + t - 1) * E + col0), v);
-    int64_t p = pos[b * N + t - 1];
-    const int64_t nrows = (int64_t)G * G + 1;
-    if (p < 0) p += nrows;
-    if (p > 0 && p < nrows) {  // p == 0 is the all-zero CLS row; out of range was reported upstream
-      const int half = E / 2;
-      const int64_t q = p - 1;
-      const int64_t trow = (col0 < half) ? (q % G) : (q / G);
-      const int tcol = (col0 < half) ? col0 : col0 - half;
-      float tv[EPL];
-      load_f32<EPL>(tab + trow * half + tcol, tv);
-#pragma unroll
-      for (int i = 0; i < EPL; ++i) v[i] += tv[i];
-    }
-  }
-  store_f32<EPL>(x_out + row * E + col0, v);
+  const int half = E / 2;
+  float wv[EPL], bv[EPL];
   if (ln_w != nullptr) {
-    wave_layernorm<EPL>(v, E, ln_w, ln_b, eps, col0);
-    store_bf16<EPL>(ln_out + row * E + col0, v);
+    ld_x4_f32<EPL>(ln_w, lane, wv);
+    ld_x4_f32<EPL>(ln_b, lane, bv);
+  }
+  const int64_t rows = B * (N + 1);
+  for (int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6); row < rows;
+       row += (int64_t)gridDim.x * kRowsPerBlock) {
+    const int64_t b = row / (N + 1), t = row % (N + 1);
+    float v[EPL];
+    if (t == 0) {
+      ld_x4_f32<EPL>(cls, lane, v);
+    } else {
+      ld_x4_bf16<EPL>(xp + (b * N + t - 1) * E, lane, v);
+      int64_t p = pos[b * N + t - 1];
+      const int64_t nrows = (int64_t)G * G + 1;
+      if (p < 0) p += nrows;
+      if (p > 0 && p < nrows) {  // p == 0 is the all-zero CLS row; out of range was reported upstream
+        const int64_t q = p - 1;
+        const float* ty = tab + (q % G) * half;   // first E/2 columns: y index
+        const float* tx = tab + (q / G) * half - half;   // last E/2 columns: x index
+#pragma unroll
+        for (int k = 0; k < EPL / 4; ++k) {
+          const int e = k * 256 + 4 * lane;     // 4 columns, never straddling E/2
+          const float4 u = *reinterpret_cast<const float4*>((e < half ? ty : tx) + e);
+          v[4 * k] += u.x; v[4 * k + 1] += u.y; v[4 * k + 2] += u.z; v[4 * k + 3] += u.w;
+        }
+      }
+    }
+    st_x4_f32<EPL>(x_out + row * E, lane, v);
+    if (ln_w != nullptr) {
+      wave_layernorm_regs<EPL>(v, E, wv, bv, eps);
+      st_x4_bf16<EPL>(ln_out + row * E, lane, v);
+    }
   }
 }
 
@@ -82,42 +99,77 @@ __global__ __launch_bounds__(256) void residual_ln_kernel(float* __restrict__ x,
                                                           uint16_t* __restrict__ out, int64_t rows,
                                                           int cols) {
   const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  const int col0 = lane * EPL;
-  float v[EPL], yv[EPL];
-  load_f32<EPL>(x + row * cols + col0, v);
-  load_bf16<EPL>(y + row * cols + col0, yv);
-  if (bias != nullptr) {
-    float bv[EPL];
-    load_f32<EPL>(bias + col0, bv);
+  float bb[EPL], wv[EPL], bv[EPL];
+  if (bias != nullptr) ld_x4_f32<EPL>(bias, lane, bb);
+  else
 #pragma unroll
-    for (int i = 0; i < EPL; ++i) yv[i] += bv[i];
-  }
-#pragma unroll
-  for (int i = 0; i < EPL; ++i) v[i] += yv[i];
-  store_f32<EPL>(x + row * cols + col0, v);
+    for (int i = 0; i < EPL; ++i) bb[i] = 0.f;
   if (ln_w != nullptr) {
-    wave_layernorm<EPL>(v, cols, ln_w, ln_b, eps, col0);
-    store_bf16<EPL>(out + row * cols + col0, v);
+    ld_x4_f32<EPL>(ln_w, lane, wv);
+    ld_x4_f32<EPL>(ln_b, lane, bv);
+  }
+  for (int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6); row < rows;
+       row += (int64_t)gridDim.x * kRowsPerBlock) {
+    float v[EPL], yv[EPL];
+    ld_x4_f32<EPL>(x + row * cols, lane, v);
+    ld_x4_bf16<EPL>(y + row * cols, lane, yv);
+#pragma unroll
+    for (int i = 0; i < EPL; ++i) v[i] += yv[i] + bb[i];
+    st_x4_f32<EPL>(x + row * cols, lane, v);
+    if (ln_w != nullptr) {
+      wave_layernorm_regs<EPL>(v, cols, wv, bv, eps);
+      st_x4_bf16<EPL>(out + row * cols, lane, v);
+    }
   }
 }
 
 // ---------------------------------------------------------------------------------------
-template <int EPL>
+// GELU + LN over a 3072/4096/6144-wide bf16 row: one 256-thread block per row, thread t owns
+// elements k*1024 + 4t + {0..3} (k < EPT/4: each wave-instruction covers 512 contiguous bytes);
+// mean and variance through a 4-wave LDS reduction.  Small register footprint keeps many rows
+// in flight (the erf polynomial is VALU-heavy).
+template <int EPT>
 __global__ __launch_bounds__(256) void gelu_ln_kernel(const uint16_t* h, const float* __restrict__ ln_w,
                                                       const float* __restrict__ ln_b, float eps, uint16_t* out,
                                                       int64_t rows, int cols) {
-  const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  const int col0 = lane * EPL;
-  float v[EPL];
-  load_bf16<EPL>(h + row * cols + col0, v);
+  __shared__ float red[2][4];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int64_t row = blockIdx.x;
+  const uint16_t* src = h + row * cols;
+  float v[EPT];
 #pragma unroll
-  for (int i = 0; i < EPL; ++i) v[i] = 0.5f * v[i] * (1.0f + erff(v[i] * 0.70710678118654752440f));
-  wave_layernorm<EPL>(v, cols, ln_w, ln_b, eps, col0);
-  store_bf16<EPL>(out + row * cols + col0, v);
+  for (int k = 0; k < EPT / 4; ++k) load_bf16<4>(src + k * 1024 + 4 * t, v + 4 * k);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < EPT; ++i) {
+    v[i] = 0.5f * v[i] * (1.0f + erff(v[i] * 0.70710678118654752440f));
+    s += v[i];
+  }
+  s = wave_sum(s);
+  if (lane == 0) red[0][w] = s;
+  __syncthreads();
+  const float mean = (red[0][0] + red[0][1] + red[0][2] + red[0][3]) / (float)cols;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < EPT; ++i) {
+    const float d = v[i] - mean;
+    q += d * d;
+  }
+  q = wave_sum(q);
+  if (lane == 0) red[1][w] = q;
+  __syncthreads();
+  const float rstd = rsqrtf((red[1][0] + red[1][1] + red[1][2] + red[1][3]) / (float)cols + eps);
+#pragma unroll
+  for (int k = 0; k < EPT / 4; ++k) {
+    float wv[4], bv[4];
+    load_f32<4>(ln_w + k * 1024 + 4 * t, wv);
+    load_f32<4>(ln_b + k * 1024 + 4 * t, bv);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[4 * k + i] = (v[4 * k + i] - mean) * rstd * wv[i] + bv[i];
+  }
+  uint16_t* dst = out + row * cols;
+#pragma unroll
+  for (int k = 0; k < EPT / 4; ++k) store_bf16<4>(dst + k * 1024 + 4 * t, v + 4 * k);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -125,15 +177,18 @@ template <int EPL>
 __global__ __launch_bounds__(256) void layernorm_f32_kernel(const float* __restrict__ x, int64_t row_stride,
                                                             const float* __restrict__ ln_w,
                                                             const float* __restrict__ ln_b, float eps,
-                                                            float* __restrict__ out, int64_t rows, int cols) {
+                                                            float* out, int64_t rows, int cols) {
   const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  const int col0 = lane * EPL;
-  float v[EPL];
-  load_f32<EPL>(x + row * row_stride + col0, v);
-  wave_layernorm<EPL>(v, cols, ln_w, ln_b, eps, col0);
-  store_f32<EPL>(out + row * cols + col0, v);
+  float wv[EPL], bv[EPL];
+  ld_x4_f32<EPL>(ln_w, lane, wv);
+  ld_x4_f32<EPL>(ln_b, lane, bv);
+  for (int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6); row < rows;
+       row += (int64_t)gridDim.x * kRowsPerBlock) {
+    float v[EPL];
+    ld_x4_f32<EPL>(x + row * row_stride, lane, v);
+    wave_layernorm_regs<EPL>(v, cols, wv, bv, eps);
+    st_x4_f32<EPL>(out + row * cols, lane, v);
+  }
 }
 
 // One block per (batch, 64-column group); 16 waves stride over tokens, LDS tree at the end.
@@ -156,7 +211,6 @@ __global__ __launch_bounds__(1024) void mean_tokens_kernel(const float* __restri
   }
 }
 
-inline unsigned row_blocks(int64_t rows) { return (unsigned)((rows + kRowsPerBlock - 1) / kRowsPerBlock); }
 
 }  // namespace
 
@@ -191,9 +245,9 @@ extern "C" int gp_posembed_cls_ln(const uint16_t* xp, const int64_t* pos, const 
   const int64_t rows = B * (N + 1);
   hipStream_t s = gp_stream(stream);
   switch (E / 64) {
-    case 12: posembed_cls_ln_kernel<12><<<row_blocks(rows), 256, 0, s>>>(xp, pos, tab, cls, B, N, E, G, ln_w, ln_b, eps, x_out, ln_out); break;
-    case 16: posembed_cls_ln_kernel<16><<<row_blocks(rows), 256, 0, s>>>(xp, pos, tab, cls, B, N, E, G, ln_w, ln_b, eps, x_out, ln_out); break;
-    case 24: posembed_cls_ln_kernel<24><<<row_blocks(rows), 256, 0, s>>>(xp, pos, tab, cls, B, N, E, G, ln_w, ln_b, eps, x_out, ln_out); break;
+    case 12: posembed_cls_ln_kernel<12><<<row_grid(rows), 256, 0, s>>>(xp, pos, tab, cls, B, N, E, G, ln_w, ln_b, eps, x_out, ln_out); break;
+    case 16: posembed_cls_ln_kernel<16><<<row_grid(rows), 256, 0, s>>>(xp, pos, tab, cls, B, N, E, G, ln_w, ln_b, eps, x_out, ln_out); break;
+    case 24: posembed_cls_ln_kernel<24><<<row_grid(rows), 256, 0, s>>>(xp, pos, tab, cls, B, N, E, G, ln_w, ln_b, eps, x_out, ln_out); break;
   }
   return gp_check_launch("gp_posembed_cls_ln");
 }
@@ -208,9 +262,9 @@ extern "C" int gp_residual_layernorm(float* x, const uint16_t* y, const float* b
   GP_REQUIRE(ln_w == nullptr || (ln_b && ln_out), "gp_residual_layernorm: LN needs ln_b and ln_out");
   hipStream_t s = gp_stream(stream);
   switch (cols / 64) {
-    case 12: residual_ln_kernel<12><<<row_blocks(rows), 256, 0, s>>>(x, y, bias, ln_w, ln_b, eps, ln_out, rows, cols); break;
-    case 16: residual_ln_kernel<16><<<row_blocks(rows), 256, 0, s>>>(x, y, bias, ln_w, ln_b, eps, ln_out, rows, cols); break;
-    case 24: residual_ln_kernel<24><<<row_blocks(rows), 256, 0, s>>>(x, y, bias, ln_w, ln_b, eps, ln_out, rows, cols); break;
+    case 12: residual_ln_kernel<12><<<row_grid(rows), 256, 0, s>>>(x, y, bias, ln_w, ln_b, eps, ln_out, rows, cols); break;
+    case 16: residual_ln_kernel<16><<<row_grid(rows), 256, 0, s>>>(x, y, bias, ln_w, ln_b, eps, ln_out, rows, cols); break;
+    case 24: residual_ln_kernel<24><<<row_grid(rows), 256, 0, s>>>(x, y, bias, ln_w, ln_b, eps, ln_out, rows, cols); break;
   }
   return gp_check_launch("gp_residual_layernorm");
 }
@@ -223,10 +277,11 @@ extern "C" int gp_gelu_layernorm(const uint16_t* h, const float* ln_w, const flo
   if (rows == 0) return 0;
   GP_REQUIRE(h && ln_w && ln_b && out, "gp_gelu_layernorm: null pointer");
   hipStream_t s = gp_stream(stream);
-  switch (cols / 64) {
-    case 48: gelu_ln_kernel<48><<<row_blocks(rows), 256, 0, s>>>(h, ln_w, ln_b, eps, out, rows, cols); break;
-    case 64: gelu_ln_kernel<64><<<row_blocks(rows), 256, 0, s>>>(h, ln_w, ln_b, eps, out, rows, cols); break;
-    case 96: gelu_ln_kernel<96><<<row_blocks(rows), 256, 0, s>>>(h, ln_w, ln_b, eps, out, rows, cols); break;
+  GP_REQUIRE(rows < (int64_t)0x7fffffff, "gp_gelu_layernorm: too many rows");
+  switch (cols / 256) {
+    case 12: gelu_ln_kernel<12><<<(unsigned)rows, 256, 0, s>>>(h, ln_w, ln_b, eps, out, rows, cols); break;
+    case 16: gelu_ln_kernel<16><<<(unsigned)rows, 256, 0, s>>>(h, ln_w, ln_b, eps, out, rows, cols); break;
+    case 24: gelu_ln_kernel<24><<<(unsigned)rows, 256, 0, s>>>(h, ln_w, ln_b, eps, out, rows, cols); break;
   }
   return gp_check_launch("gp_gelu_layernorm");
 }
@@ -239,9 +294,9 @@ extern "C" int gp_layernorm_f32(const float* x, int64_t row_stride, const float*
   GP_REQUIRE(x && ln_w && ln_b && out, "gp_layernorm_f32: null pointer");
   hipStream_t s = gp_stream(stream);
   switch (cols / 64) {
-    case 12: layernorm_f32_kernel<12><<<row_blocks(rows), 256, 0, s>>>(x, row_stride, ln_w, ln_b, eps, out, rows, cols); break;
-    case 16: layernorm_f32_kernel<16><<<row_blocks(rows), 256, 0, s>>>(x, row_stride, ln_w, ln_b, eps, out, rows, cols); break;
-    case 24: layernorm_f32_kernel<24><<<row_blocks(rows), 256, 0, s>>>(x, row_stride, ln_w, ln_b, eps, out, rows, cols); break;
+    case 12: layernorm_f32_kernel<12><<<row_grid(rows), 256, 0, s>>>(x, row_stride, ln_w, ln_b, eps, out, rows, cols); break;
+    case 16: layernorm_f32_kernel<16><<<row_grid(rows), 256, 0, s>>>(x, row_stride, ln_w, ln_b, eps, out, rows, cols); break;
+    case 24: layernorm_f32_kernel<24><<<row_grid(rows), 256, 0, s>>>(x, row_stride, ln_w, ln_b, eps, out, rows, cols); break;
   }
   return gp_check_launch("gp_layernorm_f32");
 }
