@@ -66,6 +66,21 @@ def cpu_baseline(n_tiles, threads):
                       "extrapolated (%.1f s per forward)" % (n_tiles, t2 - t0, full)}
 
 
+def pmc_traffic(n_tiles, kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary (tools/pmc_bench.sh ->
+    profiles/pmc_traffic.json), or None when it was collected on a different workload."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    k = d.get("kernels", {}).get(kernel)
+    if d.get("tiles") != n_tiles or k is None:
+        return None
+    return round(k["hbm_bytes_per_launch"])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -128,6 +143,11 @@ def main():
     achieved = att_flops_launch / avg_att_s / 1e12 if avg_att_s > 0 else 0.0
     gemm_tf = runtime.gemm_flops(1, args.tiles, 768, 3072, 1536, 12) / 1e12
     total_tf = gemm_tf + 12 * att_flops_launch / 1e12
+    traffic = pmc_traffic(args.tiles, "dilated_attn32_kernel<48, true, 4>")
+    # HBM-bound merge kernel: algorithmic bytes per launch over its live launch time
+    n_mg, ms_mg = kt.get("merge", (0, 0.0))
+    merge_bytes = runtime.merge_bytes(L, segs, ratios, 16, 48)
+    merge_gbs = merge_bytes / (ms_mg / max(n_mg, 1) / 1e3) / 1e9 if ms_mg > 0 else 0.0
     value = world * args.tiles * args.steps / elapsed
     ms_step = elapsed / args.steps * 1e3
     result = {
@@ -140,9 +160,13 @@ def main():
                    "tiles_per_slide": args.tiles, "slides_per_gpu": 1, "parallelism": "replica x%d" % world},
         "roofline": {"bound": "mfma", "kernel": "gp_dilated_attn_fwd", "achieved": round(achieved, 2),
                      "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
-                     "traffic": None, "flops_per_launch": att_flops_launch, "avg_launch_ms": round(avg_att_s * 1e3, 4),
+                     "traffic": traffic, "flops_per_launch": att_flops_launch, "avg_launch_ms": round(avg_att_s * 1e3, 4),
                      "launches": n_att},
         "attn_mfma_util_pct": round(100 * achieved / PEAK_BF16_TFLOPS, 2),
+        "merge_roofline": {"bound": "hbm", "kernel": "gp_branch_merge_ln", "achieved": round(merge_gbs, 1),
+                           "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(merge_gbs / PEAK_HBM_GBS, 4),
+                           "traffic": pmc_traffic(args.tiles, "branch_merge_kernel<12>"),
+                           "bytes_per_launch": merge_bytes},
         "model_tflops": round(total_tf * args.steps * world / elapsed, 2),
         "kernel_ms_per_step": {k: round(v[1] / args.steps, 3) for k, v in sorted(kt.items())},
     }

@@ -282,3 +282,11 @@ class EncoderEngine:
 def gemm_flops(B: int, N: int, E: int, F: int, C: int, depth: int) -> float:
     L = N + 1
     return float(2 * B * L * (4 * E * E + 2 * E * F) * depth + 2 * B * N * C * E)
+
+
+def merge_bytes(L: int, segs: Sequence[int], ratios: Sequence[int], H: int, D: int, B: int = 1) -> float:
+    """Algorithmic HBM bytes of one gp_branch_merge_ln launch (bf16 o, fp32 lse, bf16 out): per token,
+    branch b contributes the E/r_b covered output columns and H/r_b LSE values."""
+    E = H * D
+    per_tok = sum(E / r * 2 + H / r * 4 for r in ratios) + E * 2
+    return float(B * L * per_tok)
