@@ -5,8 +5,11 @@
 
 A step = one gigapath_slide_enc12l768d forward (bf16, inference) over one synthetic slide of
 --tiles tiles (default 70,000 = BASELINE config C3), inputs and weights resident in HBM.
-Multi-GPU: one process per GPU, each rank encodes its own slide (replicas, no data-path
-collective): value = tiles processed by all ranks / max-over-ranks wall time ("weak").
+Multi-GPU (one process per GPU), --mode:
+  sp       (default for N > 1) the SAME slide is sharded across the N ranks by sequence
+           parallelism (seqpar.py: per-layer sparse K/V exchange over RCCL point-to-point);
+           value = slide tiles / max-over-ranks wall time ("strong" scaling, C4's design);
+  replica  every rank encodes its own slide, no collective: value = N x tiles / time ("weak").
 Rank 0 prints ONE JSON line including the attention kernel's roofline (HIP events around
 every gp_dilated_attn_fwd launch in the timed region) and a CPU baseline (the fp32 oracle on
 a bounded sample of the same workload, timed on this host).
@@ -89,21 +92,34 @@ def main():
     ap.add_argument("--tiles", type=int, default=70000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--mode", choices=["sp", "replica"], default="sp")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    sp = world > 1 and args.mode == "sp"
+    # GP_BENCH_BACKEND=gloo: rehearsal of the multi-rank path with several ranks on one GPU
+    backend = os.environ.get("GP_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % torch.cuda.device_count()
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
 
+    import contextlib
     from gigapath import runtime, slide_encoder
-    model = slide_encoder.create_model("", ARCH, 1536).to(dev).eval()
+    with contextlib.redirect_stdout(sys.stderr):       # keep stdout to the one JSON line
+        model = slide_encoder.create_model("", ARCH, 1536).to(dev).eval()
     model.validate_positions = True
-    x, coords = make_slide(args.tiles, seed=1 + rank)
+    if sp:
+        model.enable_sequence_parallel()
+    x, coords = make_slide(args.tiles, seed=1 if sp else 1 + rank)
     xt = torch.from_numpy(x).to(dev)
     ct = torch.from_numpy(coords).to(dev)
 
@@ -128,7 +144,7 @@ def main():
         runtime.TIMER.enabled = False
     elapsed = t1 - t0
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     assert all(torch.isfinite(o).all() for o in out)
@@ -139,6 +155,13 @@ def main():
     L = args.tiles + 1
     att_flops_launch = runtime.attention_valid_flops(L, segs, ratios, 16, 48)
     n_att, ms_att = kt.get("attn", (0, 0.0))
+    if sp:
+        # this rank's attention launches cover its query window: price them with its share of the
+        # valid FLOPs (two launches per layer: local branches, then exchanged ones)
+        plan = model._sp.plan
+        a_w, b_w = plan.bounds[rank]
+        att_flops_launch = runtime.attention_valid_flops_window(L, segs, ratios, 16, 48, a_w, b_w)
+        n_att = args.steps * len(model.encoder.layers)      # per layer: both launches together
     avg_att_s = ms_att / max(n_att, 1) / 1e3
     achieved = att_flops_launch / avg_att_s / 1e12 if avg_att_s > 0 else 0.0
     gemm_tf = runtime.gemm_flops(1, args.tiles, 768, 3072, 1536, 12) / 1e12
@@ -148,16 +171,18 @@ def main():
     n_mg, ms_mg = kt.get("merge", (0, 0.0))
     merge_bytes = runtime.merge_bytes(L, segs, ratios, 16, 48)
     merge_gbs = merge_bytes / (ms_mg / max(n_mg, 1) / 1e3) / 1e9 if ms_mg > 0 else 0.0
-    value = world * args.tiles * args.steps / elapsed
+    value = (1 if sp else world) * args.tiles * args.steps / elapsed
     ms_step = elapsed / args.steps * 1e3
     result = {
         "metric": METRIC, "value": round(value, 2), "unit": "tiles/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
+        "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "strong" if sp else "weak",
         "vs_baseline": None, "dtype": "bf16",
         "data": "synthetic (PCG64 N(0,1) 1536-d tile embeddings, distinct grid coords; random-init weights)",
-        "config": {"workload": "C3: %s forward, one %d-tile slide per GPU, all_layer_embed=True"
-                               % (ARCH, args.tiles),
-                   "tiles_per_slide": args.tiles, "slides_per_gpu": 1, "parallelism": "replica x%d" % world},
+        "config": {"workload": ("%s forward, one %d-tile slide sharded over %d GPUs (sequence parallel), "
+                                "all_layer_embed=True" % (ARCH, args.tiles, world)) if sp else
+                               ("C3: %s forward, one %d-tile slide per GPU, all_layer_embed=True" % (ARCH, args.tiles)),
+                   "tiles_per_slide": args.tiles, "slides_per_gpu": (1.0 / world) if sp else 1,
+                   "parallelism": ("sp%d" % world) if sp else ("replica x%d" % world)},
         "roofline": {"bound": "mfma", "kernel": "gp_dilated_attn_fwd", "achieved": round(achieved, 2),
                      "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
                      "traffic": traffic, "flops_per_launch": att_flops_launch, "avg_launch_ms": round(avg_att_s * 1e3, 4),
@@ -170,6 +195,8 @@ def main():
         "model_tflops": round(total_tf * args.steps * world / elapsed, 2),
         "kernel_ms_per_step": {k: round(v[1] / args.steps, 3) for k, v in sorted(kt.items())},
     }
+    if sp:
+        result["sp_exchange_mb_per_layer_rank0"] = round(model._sp.plan.exchange_bytes(0) / 1e6, 1)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         result["cpu_baseline"] = cpu_baseline(args.tiles, threads)

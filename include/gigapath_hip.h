@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define GP_ABI_VERSION 1
+#define GP_ABI_VERSION 2
 #define GP_EARG (-1)
 #define GP_MAX_BRANCHES 8
 
@@ -51,6 +51,8 @@ int gp_coords_to_pos(const void* coords, int coords_is_f64, int64_t n_tiles, int
  *   ln_out           = LayerNorm(x_out; ln_w, ln_b, eps)    (skipped if ln_w == NULL)
  * xp: [B, N, E] bf16 (patch projection incl. bias); tab: [G, E/2] fp32 one-axis sin-cos
  * table (fp64-built); cls: [E] fp32; x_out: [B, N+1, E] fp32; ln_out: [B, N+1, E] bf16.
+ * cls == NULL: no CLS row (a sequence-parallel shard that does not hold token 0):
+ *   x_out[b, t, :] = xp[b, t, :] + pos row, t < N  (x_out, ln_out: [B, N, E]).
  * E must be 64 * {12, 16, 24}. */
 int gp_posembed_cls_ln(const uint16_t* xp, const int64_t* pos, const float* tab, const float* cls,
                        int64_t B, int64_t N, int E, int G, const float* ln_w, const float* ln_b,
@@ -85,6 +87,48 @@ int gp_dilated_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v,
                         float* const* lse_out, float softmax_scale, int q_log2_prescaled,
                         void* stream);
 
+/* One branch of gp_dilated_attn_fwd_ex: where its keys/values live and where its outputs go. */
+typedef struct GpAttnBranch {
+  int32_t seg_len;           /* sl (segment length before min(sl, L)) */
+  int32_t ratio;             /* r  (dilation ratio) */
+  const uint16_t* k;         /* key rows: token t of batch b is row (b*L + t - kv_tok_base) */
+  const uint16_t* v;         /* value rows, same indexing */
+  int64_t kv_row_stride;     /* elements between consecutive rows */
+  int64_t kv_tok_base;       /* token index held by row 0 */
+  int32_t kv_sparse_cols;    /* 0: head h at columns h*D (dense projection rows);
+                                1: head h at columns (h % (H/r))*D (token-major sparsified rows
+                                   written by gp_dilated_sparsify, where K is at column 0 and V at
+                                   column (H/r)*D of each row; pass v = k + (H/r)*D) */
+  uint16_t* o;               /* [B*nseg, m, H, D] bf16 */
+  float* lse;                /* [B*nseg, H, m] fp32 */
+} GpAttnBranch;
+
+/* Generalised gp_dilated_attn_fwd: per-branch K/V sources and a query window.  Computes, for
+ * every branch, the sparse rows whose sparse_to_dense slot n*g + i*r + j (g = m*r,
+ * dilated_attention.py:33-53) lies in [win_lo, win_hi) of each batch's sequence -- exactly the
+ * rows gp_branch_merge_ln_window reads for tokens [win_lo, win_hi).  The sequence-parallel
+ * shard of one rank passes its own token range; win = [0, L) is the single-device forward.
+ * q: token t of batch b at row (b*L + t - q_tok_base), row stride q_row_stride, head h at
+ * columns h*D.  Keys of a segment are rows n*s + i*r + j for every valid i (all of the segment),
+ * so each branch's k/v rows must cover the gather range of every segment the window meets. */
+int gp_dilated_attn_fwd_ex(const uint16_t* q, int64_t q_row_stride, int64_t q_tok_base, int64_t B,
+                           int64_t L, int H, int D, int64_t win_lo, int64_t win_hi,
+                           const GpAttnBranch* branches, int nbranch, float softmax_scale,
+                           int q_log2_prescaled, void* stream);
+
+/* Token-major sparsified K/V rows for sequence parallelism (one rank's share of
+ * DilatedAttention.gathering, dilated_attention.py:16-31,76-98).  For tokens
+ * p in [tok_lo, tok_lo + n_tok) (rows of src, first row = tok_lo) and branch b with
+ * s = min(sl, L), j = (p % s) % r, C = (H/r)*D:
+ *   dst[b][p - base_b, 0:C]  = src[p - tok_lo, k_col + j*C : k_col + (j+1)*C]
+ *   dst[b][p - base_b, C:2C] = src[p - tok_lo, v_col + j*C : v_col + (j+1)*C]
+ * dst[b]: [rows, 2C] bf16 whose row 0 holds token base_b = dst_tok_base[b] (NULL: all 0,
+ * i.e. full-length [L, 2C] buffers); base_b <= tok_lo.  B = 1.  H % r == 0 for every branch. */
+int gp_dilated_sparsify(const uint16_t* src, int64_t src_row_stride, int64_t k_col, int64_t v_col,
+                        int64_t tok_lo, int64_t n_tok, int64_t L, int H, int D, const int32_t* seg_len,
+                        const int32_t* ratios, int nbranch, uint16_t* const* dst,
+                        const int64_t* dst_tok_base, void* stream);
+
 /* Drop-in for the operator seam flash_attn_func(q, k, v, 0.0, None, scale, False)
  * (torchscale/component/flash_attention.py:13-16): non-causal, no mask, dropout 0.
  * q/k/v/o: [nbatch, seqlen, H, D] bf16 contiguous; lse: [nbatch, H, seqlen] fp32. */
@@ -102,6 +146,14 @@ int gp_branch_merge_ln(const uint16_t* const* o_in, const float* const* lse_in,
                        const int32_t* seg_len, const int32_t* ratios, int nbranch, int64_t B,
                        int64_t L, int H, int D, const float* ln_w, const float* ln_b, float eps,
                        uint16_t* out, void* stream);
+
+/* gp_branch_merge_ln restricted to tokens [tok_lo, tok_lo + n_tok) of each batch (a
+ * sequence-parallel shard): out row b*n_tok + (p - tok_lo).  Reads only the branch rows
+ * gp_dilated_attn_fwd_ex computed for the same window. */
+int gp_branch_merge_ln_window(const uint16_t* const* o_in, const float* const* lse_in,
+                              const int32_t* seg_len, const int32_t* ratios, int nbranch, int64_t B,
+                              int64_t L, int64_t tok_lo, int64_t n_tok, int H, int D, const float* ln_w,
+                              const float* ln_b, float eps, uint16_t* out, void* stream);
 
 /* Residual add fused with the next pre-LN (encoder.py:141,147 / :159,126):
  *   x += y + bias (fp32 residual stream, in place);  ln_out = LayerNorm(x) (skipped if ln_w == NULL).

@@ -28,23 +28,63 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 struct AttnBranch {
   GpBranch g;
   int32_t nqb;          // q-blocks per (batch-segment, head)
+  int32_t n_lo;         // first segment whose dense slots meet the query window
+  int32_t nseg_w;       // segments meeting the window
+  int32_t kv_sparse;    // 0: head h at columns h*D of a k/v row; 1: at (h % hpg)*D (sparsified rows)
   int64_t item_begin;   // first work item of this branch
+  const uint16_t* k;    // key rows: token t of batch b at row (b*L + t - kv_tok_base)
+  const uint16_t* v;
+  int64_t kv_stride;    // elements between consecutive k / v rows
+  int64_t kv_tok_base;
   uint16_t* o;          // [B*nseg, m, H, D]
   float* lse;           // [B*nseg, H, m]
 };
 
 struct AttnArgs {
-  const uint16_t* q;
-  const uint16_t* k;
-  const uint16_t* v;
-  int64_t row_stride;
+  const uint16_t* q;    // query rows: token t of batch b at row (b*L + t - q_tok_base)
+  int64_t q_stride;
+  int64_t q_tok_base;
   int64_t L;
+  int64_t win_lo, win_hi;   // dense-slot window of every batch: rows the merge reads there
   int32_t H;
   int32_t nbranch;
   float c_log2;         // softmax_scale * log2(e)
   int64_t total_items;
   AttnBranch br[GP_MAX_BRANCHES];   // work order (heaviest first)
 };
+
+// Work item -> (branch, batch, segment, head, query-row range).  Rows [i_lo, i_hi) of
+// (segment n, head group j) are those whose sparse_to_dense slot n*g + i*r + j lies in the
+// window (dilated_attention.py:33-53 places sparse row i of head group j at that slot).
+struct WorkItem {
+  int bi, bn, bidx, n, hh, j, c, i_lo, i_hi, qb;
+};
+
+GP_DEV int ceil_div_pos(int64_t a, int r) { return a > 0 ? (int)((a + r - 1) / r) : 0; }
+
+GP_DEV void decode_item(const AttnArgs& a, int item, WorkItem& w) {
+  int bi = 0;
+#pragma unroll
+  for (int t = 1; t < GP_MAX_BRANCHES; ++t)
+    if (t < a.nbranch && item >= (int)a.br[t].item_begin) bi = t;
+  const AttnBranch& br = a.br[bi];
+  const GpBranch& g = br.g;
+  int local = item - (int)br.item_begin;
+  w.bi = bi;
+  w.qb = local % br.nqb;
+  local /= br.nqb;
+  w.hh = local % a.H;
+  const int bnw = local / a.H;
+  w.bidx = bnw / br.nseg_w;
+  w.n = br.n_lo + (bnw - w.bidx * br.nseg_w);
+  w.bn = w.bidx * g.nseg + w.n;
+  w.j = w.hh / g.hpg;
+  w.c = gp_valid_rows(g, a.L, w.n, w.j);
+  const int64_t base = (int64_t)w.n * g.g + w.j;
+  w.i_lo = ceil_div_pos(a.win_lo - base, g.r);
+  const int hi = ceil_div_pos(a.win_hi - base, g.r);
+  w.i_hi = hi < g.m ? hi : g.m;
+}
 
 constexpr int kWaves = 4;
 constexpr int kQT = 2;                       // 16-row q-tiles per wave
@@ -73,35 +113,28 @@ __global__ __launch_bounds__(256, 2) void dilated_attn_kernel(const AttnArgs a) 
   // [K0 | V0 | K1 | V1] + slack: the zero-weight d>=D lanes of the last K row read into V.
   __shared__ __attribute__((aligned(16))) char smem[4 * TILEB + 64];
 
-  const int64_t item = xcd_group(blockIdx.x, gridDim.x);
-  int bi = 0;
-#pragma unroll
-  for (int t = 1; t < GP_MAX_BRANCHES; ++t)
-    if (t < a.nbranch && item >= a.br[t].item_begin) bi = t;
-  const GpBranch g = a.br[bi].g;
-  int64_t local = item - a.br[bi].item_begin;
-  const int nqb = a.br[bi].nqb;
-  const int qb = (int)(local % nqb);
-  local /= nqb;
-  const int hh = (int)(local % a.H);
-  const int64_t bn = local / a.H;
-  const int64_t bidx = bn / g.nseg;
-  const int n = (int)(bn % g.nseg);
-  const int j = hh / g.hpg;
-  const int c = gp_valid_rows(g, a.L, n, j);
-  // Non-last segments: every sparse row can reach the output (incl. the r-pad row when
-  // s % r != 0, whose dense slot lands inside [0, L)).  Last segment: only valid rows can.
-  const int rows_needed = (n < g.nseg - 1) ? g.m : c;
-  const int q0 = qb * kQB;
+  WorkItem wi;
+  decode_item(a, (int)xcd_group(blockIdx.x, gridDim.x), wi);
+  const GpBranch g = a.br[wi.bi].g;
+  const int hh = wi.hh, j = wi.j, c = wi.c;
+  const int64_t bn = wi.bn;
+  const int q0 = wi.i_lo + wi.qb * kQB;
+  const int rows_needed = wi.i_hi;
   if (q0 >= rows_needed) return;
+  // q rows past the window are neither computed nor (in a shard) resident: load only real rows
+  // of the window (rows >= c are the reference's zero-padded queries)
+  const int qvalid = c < rows_needed ? c : rows_needed;
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int l16 = lane & 15, g4 = lane >> 4;
-  const int64_t tok0 = bidx * a.L + (int64_t)n * g.s + j;     // token of sparse row 0
-  const int64_t rstride = (int64_t)g.r * a.row_stride;        // elements between sparse rows
-  const uint16_t* qbase = a.q + tok0 * a.row_stride + hh * D;
-  const uint16_t* kbase = a.k + tok0 * a.row_stride + hh * D;
-  const uint16_t* vbase = a.v + tok0 * a.row_stride + hh * D;
+  const AttnBranch& brr = a.br[wi.bi];
+  const int64_t tok0 = (int64_t)wi.bidx * a.L + (int64_t)wi.n * g.s + j;     // token of sparse row 0
+  const int64_t qstride = (int64_t)g.r * a.q_stride;                        // elements between sparse rows
+  const int64_t kvstride = (int64_t)g.r * brr.kv_stride;
+  const int kcol = brr.kv_sparse ? (hh % g.hpg) * D : hh * D;
+  const uint16_t* qbase = a.q + (tok0 - a.q_tok_base) * a.q_stride + hh * D;
+  const uint16_t* kbase = brr.k + (tok0 - brr.kv_tok_base) * brr.kv_stride + kcol;
+  const uint16_t* vbase = brr.v + (tok0 - brr.kv_tok_base) * brr.kv_stride + kcol;
 
   // ---- Q fragments (B operand of S^T = K.Q^T): lane holds Q[row l16][d = 32ks + 8g4 .. +7]
   bf16x8 qf[kQT][KS];
@@ -112,7 +145,7 @@ __global__ __launch_bounds__(256, 2) void dilated_attn_kernel(const AttnArgs a) 
     for (int ks = 0; ks < KS; ++ks) {
       const int d0 = ks * 32 + g4 * 8;
       bf16x8 z = {};
-      if (i < c && d0 < D) z = *reinterpret_cast<const bf16x8*>(qbase + (int64_t)i * rstride + d0);
+      if (i < qvalid && d0 < D) z = *reinterpret_cast<const bf16x8*>(qbase + (int64_t)i * qstride + d0);
       qf[qt][ks] = z;
     }
   }
@@ -128,7 +161,7 @@ __global__ __launch_bounds__(256, 2) void dilated_attn_kernel(const AttnArgs a) 
       const int row = rem / CH, ch = rem % CH;
       const int key = kv0 + row;
       uint4 z = make_uint4(0, 0, 0, 0);
-      if (key < c) z = *reinterpret_cast<const uint4*>((tsel ? vbase : kbase) + (int64_t)key * rstride + ch * 8);
+      if (key < c) z = *reinterpret_cast<const uint4*>((tsel ? vbase : kbase) + (int64_t)key * kvstride + ch * 8);
       stage[u] = z;
     }
   };
@@ -249,7 +282,7 @@ __global__ __launch_bounds__(256, 2) void dilated_attn_kernel(const AttnArgs a) 
 
   // ---- epilogue: analytic zero-pad keys, normalise, store O rows and LSE
   const int npad = g.m - c;
-  AttnBranch br = a.br[bi];
+  const AttnBranch& br = a.br[wi.bi];
 #pragma unroll
   for (int qt = 0; qt < kQT; ++qt) {
     float l = l_run[qt];
@@ -316,33 +349,25 @@ __global__ __launch_bounds__(NW * 64, 2) void dilated_attn32_kernel(const AttnAr
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
 
   // ---- work item (32-bit index math: items < 2^31, checked on the host)
-  const int item = (int)xcd_group(blockIdx.x, gridDim.x);
-  int bi = 0;
-#pragma unroll
-  for (int t = 1; t < GP_MAX_BRANCHES; ++t)
-    if (t < a.nbranch && item >= (int)a.br[t].item_begin) bi = t;
-  const GpBranch g = a.br[bi].g;
-  const int nqb = a.br[bi].nqb;
-  int local = item - (int)a.br[bi].item_begin;
-  const int qb = local % nqb;
-  local /= nqb;
-  const int hh = local % a.H;
-  const int bn = local / a.H;
-  const int bidx = bn / g.nseg;
-  const int n = bn - bidx * g.nseg;
-  const int j = hh / g.hpg;
-  const int c = gp_valid_rows(g, a.L, n, j);
-  const int rows_needed = (n < g.nseg - 1) ? g.m : c;
-  const int q0 = qb * QB;
+  WorkItem wi;
+  decode_item(a, (int)xcd_group(blockIdx.x, gridDim.x), wi);
+  const GpBranch g = a.br[wi.bi].g;
+  const int hh = wi.hh, c = wi.c, bn = wi.bn;
+  const int rows_needed = wi.i_hi;
+  const int q0 = wi.i_lo + wi.qb * QB;
   if (q0 >= rows_needed) return;
+  const int qvalid = c < rows_needed ? c : rows_needed;   // see dilated_attn_kernel
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int l32 = lane & 31, h = lane >> 5;
-  const int64_t tok0 = (int64_t)bidx * a.L + (int64_t)n * g.s + j;
-  const int64_t rstride = (int64_t)g.r * a.row_stride;
-  const uint16_t* qbase = a.q + tok0 * a.row_stride + hh * D;
-  const uint16_t* kbase = a.k + tok0 * a.row_stride + hh * D;
-  const uint16_t* vbase = a.v + tok0 * a.row_stride + hh * D;
+  const AttnBranch& brr = a.br[wi.bi];
+  const int64_t tok0 = (int64_t)wi.bidx * a.L + (int64_t)wi.n * g.s + wi.j;
+  const int64_t qstride = (int64_t)g.r * a.q_stride;
+  const int64_t kvstride = (int64_t)g.r * brr.kv_stride;
+  const int kcol = brr.kv_sparse ? (hh % g.hpg) * D : hh * D;
+  const uint16_t* qbase = a.q + (tok0 - a.q_tok_base) * a.q_stride + hh * D;
+  const uint16_t* kbase = brr.k + (tok0 - brr.kv_tok_base) * brr.kv_stride + kcol;
+  const uint16_t* vbase = brr.v + (tok0 - brr.kv_tok_base) * brr.kv_stride + kcol;
 
   // V images: the d-columns >= D of every row (block 3 for D = 48) hold bf16 1.0
   if constexpr (kOnes) {
@@ -360,7 +385,7 @@ __global__ __launch_bounds__(NW * 64, 2) void dilated_attn32_kernel(const AttnAr
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       bf16x8 z = {};
-      if (i < c) z = *reinterpret_cast<const bf16x8*>(qbase + (int64_t)i * rstride + 16 * ks + 8 * h);
+      if (i < qvalid) z = *reinterpret_cast<const bf16x8*>(qbase + (int64_t)i * qstride + 16 * ks + 8 * h);
       qf[ks] = z;
     }
   }
@@ -375,7 +400,7 @@ __global__ __launch_bounds__(NW * 64, 2) void dilated_attn32_kernel(const AttnAr
       const int row = rem / CH, ch = rem % CH;
       const int key = kv0 + row;
       uint4 z = make_uint4(0, 0, 0, 0);
-      if (key < c) z = *reinterpret_cast<const uint4*>((tsel ? vbase : kbase) + (int64_t)key * rstride + ch * 8);
+      if (key < c) z = *reinterpret_cast<const uint4*>((tsel ? vbase : kbase) + (int64_t)key * kvstride + ch * 8);
       stage[u] = z;
     }
   };
@@ -550,7 +575,7 @@ __global__ __launch_bounds__(NW * 64, 2) void dilated_attn32_kernel(const AttnAr
   }
   const float inv = so / l;
   const int i = q0 + w * 32 + l32;
-  AttnBranch br = a.br[bi];
+  const AttnBranch& br = a.br[wi.bi];
   if (i < rows_needed) {
     uint16_t* orow = br.o + (((int64_t)bn * g.m + i) * a.H + hh) * (int64_t)D;
 #pragma unroll
@@ -577,6 +602,7 @@ struct MergeBranch {
 
 struct MergeArgs {
   int64_t B, L;
+  int64_t tok_lo, ntok;   // window of tokens [tok_lo, tok_lo + ntok) of every batch; out row = b*ntok + t
   int32_t H, D, E, nbranch;
   MergeBranch br[GP_MAX_BRANCHES];
   const float* ln_w;
@@ -593,9 +619,9 @@ template <int EPL>
 __global__ __launch_bounds__(256) void branch_merge_kernel(const MergeArgs a) {
   const int lane = threadIdx.x & 63;
   const int row = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + (int)(threadIdx.x >> 6));
-  if (row >= (int)(a.B * a.L)) return;
-  const int L = (int)a.L;
-  const int bidx = row / L, p = row - bidx * L;
+  if (row >= (int)(a.B * a.ntok)) return;
+  const int nt = (int)a.ntok;
+  const int bidx = row / nt, p = (int)a.tok_lo + (row - bidx * nt);
   const int col0 = lane * EPL;
   const int hh = col0 / a.D;
 
@@ -686,52 +712,88 @@ extern "C" int gp_dilated_gather(const uint16_t* src, int64_t row_stride, int64_
   return gp_check_launch("gp_dilated_gather");
 }
 
-extern "C" int gp_dilated_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, int64_t row_stride,
-                                   int64_t B, int64_t L, int H, int D, const int32_t* seg_len, const int32_t* ratios,
-                                   int nbranch, uint16_t* const* o_out, float* const* lse_out, float softmax_scale,
-                                   int q_log2_prescaled, void* stream) {
+extern "C" int gp_dilated_attn_fwd_ex(const uint16_t* q, int64_t q_row_stride, int64_t q_tok_base, int64_t B,
+                                      int64_t L, int H, int D, int64_t win_lo, int64_t win_hi,
+                                      const GpAttnBranch* branches, int nbranch, float softmax_scale,
+                                      int q_log2_prescaled, void* stream) {
   GP_REQUIRE(D == 48 || D == 64 || D == 96, "gp_dilated_attn_fwd: head dim %d unsupported (48, 64, 96)", D);
   GP_REQUIRE(nbranch >= 1 && nbranch <= GP_MAX_BRANCHES, "gp_dilated_attn_fwd: nbranch must be 1..%d", GP_MAX_BRANCHES);
-  GP_REQUIRE(B > 0 && L > 0 && H > 0 && row_stride >= (int64_t)H * D && row_stride % 8 == 0,
+  GP_REQUIRE(B > 0 && L > 0 && H > 0 && q_row_stride >= (int64_t)H * D && q_row_stride % 8 == 0,
              "gp_dilated_attn_fwd: bad sizes");
-  GP_REQUIRE(q && k && v && seg_len && ratios && o_out && lse_out, "gp_dilated_attn_fwd: null pointer");
-  GP_REQUIRE(gp_aligned(q, 16) && gp_aligned(k, 16) && gp_aligned(v, 16), "gp_dilated_attn_fwd: q/k/v must be 16-byte aligned");
+  GP_REQUIRE(B * L < (int64_t)0x7fffffff, "gp_dilated_attn_fwd: B*L too large");
+  GP_REQUIRE(0 <= win_lo && win_lo <= win_hi && win_hi <= L, "gp_dilated_attn_fwd: bad window [%lld, %lld) for L=%lld",
+             (long long)win_lo, (long long)win_hi, (long long)L);
+  GP_REQUIRE(q && branches, "gp_dilated_attn_fwd: null pointer");
+  GP_REQUIRE(gp_aligned(q, 16), "gp_dilated_attn_fwd: q must be 16-byte aligned");
+  if (win_lo == win_hi) return 0;
   AttnArgs a;
-  a.q = q; a.k = k; a.v = v;
-  a.row_stride = row_stride;
+  a.q = q;
+  a.q_stride = q_row_stride;
+  a.q_tok_base = q_tok_base;
   a.L = L;
+  a.win_lo = win_lo;
+  a.win_hi = win_hi;
   a.H = H;
   a.nbranch = nbranch;
   const float scale = softmax_scale > 0.f ? softmax_scale : 1.0f / sqrtf((float)D);
   a.c_log2 = q_log2_prescaled ? 1.0f : scale * 1.44269504088896340736f;
+  const char* impl_env = getenv("GP_ATTN_IMPL");   // A/B switch: 1 = 16x16x32 kernel, 2 = 32x32x16 kernel
+  const int impl = (D == 96) ? 1 : (impl_env ? atoi(impl_env) : 2);
+  GP_REQUIRE(impl == 1 || impl == 2, "gp_dilated_attn_fwd: GP_ATTN_IMPL must be 1 or 2");
+  GP_REQUIRE(!q_log2_prescaled || impl != 1, "gp_dilated_attn_fwd: q_log2_prescaled needs D in {48, 64}");
+  const int qblk = 128;                            // query rows per workgroup (both kernels)
   // order branches by keys per work item (descending) so the longest items start first
   int order[GP_MAX_BRANCHES];
   GpBranch geo[GP_MAX_BRANCHES];
   for (int b = 0; b < nbranch; ++b) {
-    GP_REQUIRE(seg_len[b] > 0 && ratios[b] > 0, "gp_dilated_attn_fwd: branch %d has sl=%d r=%d", b, seg_len[b], ratios[b]);
-    GP_REQUIRE(o_out[b] && lse_out[b] && gp_aligned(o_out[b], 8), "gp_dilated_attn_fwd: branch %d output null/misaligned", b);
-    geo[b] = gp_make_branch(L, seg_len[b], ratios[b], H);
+    const GpAttnBranch& d = branches[b];
+    GP_REQUIRE(d.seg_len > 0 && d.ratio > 0, "gp_dilated_attn_fwd: branch %d has sl=%d r=%d", b, d.seg_len, d.ratio);
+    GP_REQUIRE(d.o && d.lse && gp_aligned(d.o, 8), "gp_dilated_attn_fwd: branch %d output null/misaligned", b);
+    GP_REQUIRE(d.k && d.v && gp_aligned(d.k, 16) && gp_aligned(d.v, 16) && d.kv_row_stride % 8 == 0,
+               "gp_dilated_attn_fwd: branch %d k/v must be 16-byte aligned with a row stride multiple of 8", b);
+    geo[b] = gp_make_branch(L, d.seg_len, d.ratio, H);
+    GP_REQUIRE(!d.kv_sparse_cols || H % d.ratio == 0, "gp_dilated_attn_fwd: sparse k/v columns need H %% r == 0");
+    GP_REQUIRE(d.kv_row_stride >= (int64_t)(d.kv_sparse_cols ? geo[b].hpg : H) * D,
+               "gp_dilated_attn_fwd: branch %d k/v row stride too small", b);
     order[b] = b;
   }
   for (int x = 1; x < nbranch; ++x)
     for (int y = x; y > 0 && geo[order[y]].m > geo[order[y - 1]].m; --y) {
       int tmp = order[y]; order[y] = order[y - 1]; order[y - 1] = tmp;
     }
-  const char* impl_env = getenv("GP_ATTN_IMPL");   // A/B switch for benchmarking
-  const int impl = (D == 96) ? 1 : (impl_env ? atoi(impl_env) : 2);
-  GP_REQUIRE(impl == 1 || impl == 2 || impl == 4, "gp_dilated_attn_fwd: GP_ATTN_IMPL must be 1, 2 or 4");
-  GP_REQUIRE(!q_log2_prescaled || impl != 1, "gp_dilated_attn_fwd: q_log2_prescaled needs D in {48, 64}");
-  const int qblk = (impl == 4) ? 256 : 128;       // query rows per workgroup
   int64_t items = 0;
   for (int x = 0; x < nbranch; ++x) {
     const int b = order[x];
+    const GpBranch& g = geo[b];
+    const GpAttnBranch& d = branches[b];
     AttnBranch& e = a.br[x];
-    e.g = geo[b];
-    e.nqb = (geo[b].m + qblk - 1) / qblk;
+    e.g = g;
+    e.n_lo = (int32_t)(win_lo / g.g);
+    const int32_t n_hi = (int32_t)((win_hi - 1) / g.g);
+    e.nseg_w = n_hi - e.n_lo + 1;
+    // q-blocks per (segment, head): the largest window row count over the segments and phases
+    int most = 0;
+    for (int32_t n = e.n_lo; n <= n_hi; ++n) {
+      for (int j = 0; j < g.r; ++j) {
+        const int64_t base = (int64_t)n * g.g + j;
+        const int64_t lo = win_lo > base ? (win_lo - base + g.r - 1) / g.r : 0;
+        int64_t hi = win_hi > base ? (win_hi - base + g.r - 1) / g.r : 0;
+        if (hi > g.m) hi = g.m;
+        if (hi - lo > most) most = (int)(hi - lo);
+      }
+      if (n > e.n_lo + 1 && n < n_hi - 1) n = n_hi - 2;   // interior segments are all full: skip ahead
+    }
+    e.nqb = (most + qblk - 1) / qblk;
+    if (e.nqb == 0) e.nqb = 1;
     e.item_begin = items;
-    e.o = o_out[b];
-    e.lse = lse_out[b];
-    items += B * (int64_t)geo[b].nseg * H * e.nqb;
+    e.k = d.k;
+    e.v = d.v;
+    e.kv_stride = d.kv_row_stride;
+    e.kv_tok_base = d.kv_tok_base;
+    e.kv_sparse = d.kv_sparse_cols ? 1 : 0;
+    e.o = d.o;
+    e.lse = d.lse;
+    items += B * (int64_t)e.nseg_w * H * e.nqb;
   }
   for (int x = nbranch; x < GP_MAX_BRANCHES; ++x) a.br[x] = a.br[nbranch - 1];
   a.total_items = items;
@@ -743,24 +805,37 @@ extern "C" int gp_dilated_attn_fwd(const uint16_t* q, const uint16_t* k, const u
       case 64: dilated_attn_kernel<64><<<(unsigned)items, 256, 0, s>>>(a); break;
       case 96: dilated_attn_kernel<96><<<(unsigned)items, 256, 0, s>>>(a); break;
     }
-  } else if (impl == 2) {
-    if (q_log2_prescaled) {
-      if (D == 48) dilated_attn32_kernel<48, true, 4><<<(unsigned)items, 256, 0, s>>>(a);
-      else dilated_attn32_kernel<64, true, 4><<<(unsigned)items, 256, 0, s>>>(a);
-    } else {
-      if (D == 48) dilated_attn32_kernel<48, false, 4><<<(unsigned)items, 256, 0, s>>>(a);
-      else dilated_attn32_kernel<64, false, 4><<<(unsigned)items, 256, 0, s>>>(a);
-    }
+  } else if (q_log2_prescaled) {
+    if (D == 48) dilated_attn32_kernel<48, true, 4><<<(unsigned)items, 256, 0, s>>>(a);
+    else dilated_attn32_kernel<64, true, 4><<<(unsigned)items, 256, 0, s>>>(a);
   } else {
-    if (q_log2_prescaled) {
-      if (D == 48) dilated_attn32_kernel<48, true, 8><<<(unsigned)items, 512, 0, s>>>(a);
-      else dilated_attn32_kernel<64, true, 8><<<(unsigned)items, 512, 0, s>>>(a);
-    } else {
-      if (D == 48) dilated_attn32_kernel<48, false, 8><<<(unsigned)items, 512, 0, s>>>(a);
-      else dilated_attn32_kernel<64, false, 8><<<(unsigned)items, 512, 0, s>>>(a);
-    }
+    if (D == 48) dilated_attn32_kernel<48, false, 4><<<(unsigned)items, 256, 0, s>>>(a);
+    else dilated_attn32_kernel<64, false, 4><<<(unsigned)items, 256, 0, s>>>(a);
   }
   return gp_check_launch("gp_dilated_attn_fwd");
+}
+
+extern "C" int gp_dilated_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, int64_t row_stride,
+                                   int64_t B, int64_t L, int H, int D, const int32_t* seg_len, const int32_t* ratios,
+                                   int nbranch, uint16_t* const* o_out, float* const* lse_out, float softmax_scale,
+                                   int q_log2_prescaled, void* stream) {
+  GP_REQUIRE(D == 48 || D == 64 || D == 96, "gp_dilated_attn_fwd: head dim %d unsupported (48, 64, 96)", D);
+  GP_REQUIRE(nbranch >= 1 && nbranch <= GP_MAX_BRANCHES, "gp_dilated_attn_fwd: nbranch must be 1..%d", GP_MAX_BRANCHES);
+  GP_REQUIRE(k && v && seg_len && ratios && o_out && lse_out, "gp_dilated_attn_fwd: null pointer");
+  GpAttnBranch br[GP_MAX_BRANCHES];
+  for (int b = 0; b < nbranch; ++b) {
+    br[b].seg_len = seg_len[b];
+    br[b].ratio = ratios[b];
+    br[b].k = k;
+    br[b].v = v;
+    br[b].kv_row_stride = row_stride;
+    br[b].kv_tok_base = 0;
+    br[b].kv_sparse_cols = 0;
+    br[b].o = o_out[b];
+    br[b].lse = lse_out[b];
+  }
+  return gp_dilated_attn_fwd_ex(q, row_stride, 0, B, L, H, D, 0, L, br, nbranch, softmax_scale, q_log2_prescaled,
+                                stream);
 }
 
 extern "C" int gp_seg_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, int64_t nbatch,
@@ -775,15 +850,25 @@ extern "C" int gp_seg_attn_fwd(const uint16_t* q, const uint16_t* k, const uint1
 extern "C" int gp_branch_merge_ln(const uint16_t* const* o_in, const float* const* lse_in, const int32_t* seg_len,
                                   const int32_t* ratios, int nbranch, int64_t B, int64_t L, int H, int D,
                                   const float* ln_w, const float* ln_b, float eps, uint16_t* out, void* stream) {
+  return gp_branch_merge_ln_window(o_in, lse_in, seg_len, ratios, nbranch, B, L, 0, L, H, D, ln_w, ln_b, eps, out,
+                                   stream);
+}
+
+extern "C" int gp_branch_merge_ln_window(const uint16_t* const* o_in, const float* const* lse_in,
+                                         const int32_t* seg_len, const int32_t* ratios, int nbranch, int64_t B,
+                                         int64_t L, int64_t tok_lo, int64_t n_tok, int H, int D, const float* ln_w,
+                                         const float* ln_b, float eps, uint16_t* out, void* stream) {
   const int E = H * D;
   GP_REQUIRE(nbranch >= 1 && nbranch <= GP_MAX_BRANCHES, "gp_branch_merge_ln: nbranch must be 1..%d", GP_MAX_BRANCHES);
   GP_REQUIRE((E == 768 || E == 1024 || E == 1536) && D % (E / 64) == 0, "gp_branch_merge_ln: H*D=%d unsupported", E);
   GP_REQUIRE(B * L < (int64_t)0x7fffffff, "gp_branch_merge_ln: B*L too large");
-  GP_REQUIRE(B > 0 && L > 0, "gp_branch_merge_ln: bad sizes");
+  GP_REQUIRE(B > 0 && L > 0 && tok_lo >= 0 && n_tok >= 0 && tok_lo + n_tok <= L, "gp_branch_merge_ln: bad sizes");
+  if (n_tok == 0) return 0;
   GP_REQUIRE(o_in && lse_in && seg_len && ratios && out, "gp_branch_merge_ln: null pointer");
   GP_REQUIRE(ln_w == nullptr || ln_b != nullptr, "gp_branch_merge_ln: ln_w without ln_b");
   MergeArgs a;
   a.B = B; a.L = L; a.H = H; a.D = D; a.E = E; a.nbranch = nbranch;
+  a.tok_lo = tok_lo; a.ntok = n_tok;
   for (int b = 0; b < nbranch; ++b) {
     GP_REQUIRE(seg_len[b] > 0 && ratios[b] > 0 && o_in[b] && lse_in[b], "gp_branch_merge_ln: bad branch %d", b);
     a.br[b].g = gp_make_branch(L, seg_len[b], ratios[b], H);
@@ -792,7 +877,7 @@ extern "C" int gp_branch_merge_ln(const uint16_t* const* o_in, const float* cons
   }
   for (int b = nbranch; b < GP_MAX_BRANCHES; ++b) a.br[b] = a.br[nbranch - 1];
   a.ln_w = ln_w; a.ln_b = ln_b; a.eps = eps; a.out = out;
-  const unsigned nb = (unsigned)((B * L + 3) / 4);   // one token per wave
+  const unsigned nb = (unsigned)((B * n_tok + 3) / 4);   // one token per wave
   hipStream_t s = gp_stream(stream);
   switch (E) {
     case 768: branch_merge_kernel<12><<<nb, 256, 0, s>>>(a); break;
@@ -800,4 +885,79 @@ extern "C" int gp_branch_merge_ln(const uint16_t* const* o_in, const float* cons
     case 1536: branch_merge_kernel<24><<<nb, 256, 0, s>>>(a); break;
   }
   return gp_check_launch("gp_branch_merge_ln");
+}
+
+// =========================================================================================
+// Token-major sparsified K/V rows for sequence parallelism (the per-rank half of
+// DilatedAttention.gathering, dilated_attention.py:16-31,76-98): for branch b, token p of
+// segment n = p / s sits at offset t = p % s, in head group j = t % r (sparse row t / r).  Its
+// row of dst[b] keeps only that group's hpg*D = C columns: [K cols j*C .. | V cols j*C ..], so a
+// contiguous token range of dst[b] is exactly what another rank's queries need from it.
+namespace {
+struct SparsifyArgs {
+  const uint16_t* src;
+  int64_t src_stride, k_col, v_col;
+  int64_t tok_lo, ntok, L;
+  int32_t nbranch, per_tok;            // 16-byte chunks per token over all branches
+  int32_t s[GP_MAX_BRANCHES], r[GP_MAX_BRANCHES], C[GP_MAX_BRANCHES], cbeg[GP_MAX_BRANCHES + 1];
+  uint16_t* dst[GP_MAX_BRANCHES];
+  int64_t dst_base[GP_MAX_BRANCHES];   // token held by row 0 of dst[b]
+};
+
+__global__ __launch_bounds__(256) void dilated_sparsify_kernel(const SparsifyArgs a) {
+  const int64_t id = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t t = id / a.per_tok;
+  if (t >= a.ntok) return;
+  int rem = (int)(id - t * a.per_tok);
+  int b = 0;
+#pragma unroll
+  for (int x = 1; x < GP_MAX_BRANCHES; ++x)
+    if (x < a.nbranch && rem >= a.cbeg[x]) b = x;
+  rem -= a.cbeg[b];
+  const int C = a.C[b];
+  const int half = C / 8;                      // chunks per K (or V) part
+  const int kv = rem >= half;
+  const int ch = rem - kv * half;
+  const int64_t p = a.tok_lo + t;
+  const int j = (int)(p % a.s[b]) % a.r[b];
+  const uint4 v = *reinterpret_cast<const uint4*>(a.src + t * a.src_stride + (kv ? a.v_col : a.k_col) + (int64_t)j * C + ch * 8);
+  *reinterpret_cast<uint4*>(a.dst[b] + (p - a.dst_base[b]) * (2 * (int64_t)C) + kv * C + ch * 8) = v;
+}
+}  // namespace
+
+extern "C" int gp_dilated_sparsify(const uint16_t* src, int64_t src_row_stride, int64_t k_col, int64_t v_col,
+                                   int64_t tok_lo, int64_t n_tok, int64_t L, int H, int D, const int32_t* seg_len,
+                                   const int32_t* ratios, int nbranch, uint16_t* const* dst,
+                                   const int64_t* dst_tok_base, void* stream) {
+  GP_REQUIRE(nbranch >= 1 && nbranch <= GP_MAX_BRANCHES, "gp_dilated_sparsify: nbranch must be 1..%d", GP_MAX_BRANCHES);
+  GP_REQUIRE(L > 0 && H > 0 && D > 0 && D % 8 == 0 && tok_lo >= 0 && n_tok >= 0 && tok_lo + n_tok <= L,
+             "gp_dilated_sparsify: bad sizes");
+  GP_REQUIRE(src_row_stride % 8 == 0 && k_col % 8 == 0 && v_col % 8 == 0, "gp_dilated_sparsify: strides must be multiples of 8");
+  if (n_tok == 0) return 0;
+  GP_REQUIRE(src && seg_len && ratios && dst && gp_aligned(src, 16), "gp_dilated_sparsify: null or misaligned pointer");
+  SparsifyArgs a;
+  a.src = src; a.src_stride = src_row_stride; a.k_col = k_col; a.v_col = v_col;
+  a.tok_lo = tok_lo; a.ntok = n_tok; a.L = L; a.nbranch = nbranch;
+  int cb = 0;
+  for (int b = 0; b < nbranch; ++b) {
+    GP_REQUIRE(seg_len[b] > 0 && ratios[b] > 0 && H % ratios[b] == 0, "gp_dilated_sparsify: branch %d needs H %% r == 0", b);
+    GP_REQUIRE(dst[b] && gp_aligned(dst[b], 16), "gp_dilated_sparsify: branch %d dst null/misaligned", b);
+    a.s[b] = (int32_t)(seg_len[b] < L ? seg_len[b] : L);
+    a.r[b] = ratios[b];
+    a.C[b] = (H / ratios[b]) * D;
+    a.dst[b] = dst[b];
+    a.dst_base[b] = dst_tok_base ? dst_tok_base[b] : 0;
+    GP_REQUIRE(a.dst_base[b] <= tok_lo, "gp_dilated_sparsify: branch %d dst_tok_base beyond tok_lo", b);
+    a.cbeg[b] = cb;
+    cb += 2 * a.C[b] / 8;
+  }
+  for (int b = nbranch; b < GP_MAX_BRANCHES; ++b) {
+    a.s[b] = 1; a.r[b] = 1; a.C[b] = 8; a.dst[b] = nullptr; a.dst_base[b] = 0; a.cbeg[b] = cb;
+  }
+  a.cbeg[GP_MAX_BRANCHES] = cb;
+  a.per_tok = cb;
+  const int64_t work = n_tok * cb;
+  GP_REQUIRE(work / 256 < (int64_t)0x7fffffff, "gp_dilated_sparsify: too much work");
+  dilated_sparsify_kernel<<<(unsigned)((work + 255) / 256), 256, 0, gp_stream(stream)>>>(a);
+  return gp_check_launch("gp_dilated_sparsify");
 }

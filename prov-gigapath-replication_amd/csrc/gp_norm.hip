@@ -58,16 +58,18 @@ __global__ __launch_bounds__(256) void posembed_cls_ln_kernel(
     ld_x4_f32<EPL>(ln_w, lane, wv);
     ld_x4_f32<EPL>(ln_b, lane, bv);
   }
-  const int64_t rows = B * (N + 1);
+  const int has_cls = cls != nullptr;        // no CLS row: a sequence-parallel shard
+  const int64_t per = N + has_cls;
+  const int64_t rows = B * per;
   for (int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6); row < rows;
        row += (int64_t)gridDim.x * kRowsPerBlock) {
-    const int64_t b = row / (N + 1), t = row % (N + 1);
+    const int64_t b = row / per, t = row % per - has_cls;   // t = tile index, -1 = CLS
     float v[EPL];
-    if (t == 0) {
+    if (t < 0) {
       ld_x4_f32<EPL>(cls, lane, v);
     } else {
-      ld_x4_bf16<EPL>(xp + (b * N + t - 1) * E, lane, v);
-      int64_t p = pos[b * N + t - 1];
+      ld_x4_bf16<EPL>(xp + (b * N + t) * E, lane, v);
+      int64_t p = pos[b * N + t];
       const int64_t nrows = (int64_t)G * G + 1;
       if (p < 0) p += nrows;
       if (p > 0 && p < nrows) {  // p == 0 is the all-zero CLS row; out of range was reported upstream
@@ -240,9 +242,10 @@ extern "C" int gp_posembed_cls_ln(const uint16_t* xp, const int64_t* pos, const 
                                   float eps, float* x_out, uint16_t* ln_out, void* stream) {
   GP_REQUIRE(epl_ok(E), "gp_posembed_cls_ln: E=%d unsupported (64*{12,16,24})", E);
   GP_REQUIRE(B > 0 && N >= 0 && G > 0, "gp_posembed_cls_ln: bad sizes");
-  GP_REQUIRE(cls && tab && x_out && (N == 0 || (xp && pos)), "gp_posembed_cls_ln: null pointer");
+  GP_REQUIRE(tab && x_out && (N == 0 || (xp && pos)), "gp_posembed_cls_ln: null pointer");
   GP_REQUIRE(ln_w == nullptr || (ln_b && ln_out), "gp_posembed_cls_ln: LN needs ln_b and ln_out");
-  const int64_t rows = B * (N + 1);
+  const int64_t rows = B * (N + (cls != nullptr));
+  if (rows == 0) return 0;
   hipStream_t s = gp_stream(stream);
   switch (E / 64) {
     case 12: posembed_cls_ln_kernel<12><<<row_grid(rows), 256, 0, s>>>(xp, pos, tab, cls, B, N, E, G, ln_w, ln_b, eps, x_out, ln_out); break;

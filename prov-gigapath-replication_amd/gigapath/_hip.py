@@ -15,10 +15,16 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GIGAPATH_HIP_LIB", os.path.join(_HERE, "_lib", "libgigapath_hip.so"))
-ABI_VERSION = 1
+ABI_VERSION = 2
 MAX_BRANCHES = 8
 
 c_i32, c_i64, c_f32, c_f64, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_double, ctypes.c_void_p
+
+
+class GpAttnBranch(ctypes.Structure):
+    """struct GpAttnBranch (include/gigapath_hip.h)."""
+    _fields_ = [("seg_len", c_i32), ("ratio", c_i32), ("k", c_vp), ("v", c_vp), ("kv_row_stride", c_i64),
+                ("kv_tok_base", c_i64), ("kv_sparse_cols", c_i32), ("o", c_vp), ("lse", c_vp)]
 
 # name -> argtypes (mirrors include/gigapath_hip.h)
 SIGNATURES = {
@@ -29,6 +35,12 @@ SIGNATURES = {
     "gp_dilated_gather": [c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp],
     "gp_dilated_attn_fwd": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp,
                             c_f32, c_i32, c_vp],
+    "gp_dilated_attn_fwd_ex": [c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i64, c_i64, c_vp, c_i32, c_f32,
+                               c_i32, c_vp],
+    "gp_dilated_sparsify": [c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp,
+                            c_vp, c_vp],
+    "gp_branch_merge_ln_window": [c_vp, c_vp, c_vp, c_vp, c_i32, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp,
+                                  c_f32, c_vp, c_vp],
     "gp_seg_attn_fwd": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i32, c_f32, c_vp, c_vp, c_vp],
     "gp_branch_merge_ln": [c_vp, c_vp, c_vp, c_vp, c_i32, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_f32, c_vp, c_vp],
     "gp_residual_layernorm": [c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_vp, c_i64, c_i32, c_vp],
@@ -118,7 +130,9 @@ def coords_to_pos(coords: torch.Tensor, grid: int, tile_size: float, pos_out: to
 def posembed_cls_ln(xp, pos, tab, cls, B, N, E, G, ln_w, ln_b, eps, x_out, ln_out):
     lib = load_library()
     _dev(xp, torch.bfloat16, "xp"); _dev(pos, torch.int64, "pos"); _dev(tab, torch.float32, "tab")
-    _dev(cls, torch.float32, "cls"); _dev(x_out, torch.float32, "x_out")
+    if cls is not None:
+        _dev(cls, torch.float32, "cls")
+    _dev(x_out, torch.float32, "x_out")
     _check(lib.gp_posembed_cls_ln(_ptr(xp), _ptr(pos), _ptr(tab), _ptr(cls), B, N, E, G, _ptr(ln_w), _ptr(ln_b),
                                   eps, _ptr(x_out), _ptr(ln_out), _stream()), "gp_posembed_cls_ln")
 
@@ -141,6 +155,45 @@ def dilated_attn_fwd(q, k, v, row_stride, B, L, H, D, segs, ratios, outs, lses, 
                                    _i32_array(ratios), len(segs), oa, la, float(softmax_scale),
                                    int(bool(q_log2_prescaled)), _stream()),
            "gp_dilated_attn_fwd")
+
+
+def attn_branch(sl, r, k, v, kv_row_stride, kv_tok_base, kv_sparse_cols, o, lse) -> GpAttnBranch:
+    """One GpAttnBranch descriptor; k / v are device tensors (views allowed) or raw pointers."""
+    kp = k if isinstance(k, int) else k.data_ptr()
+    vp = v if isinstance(v, int) else v.data_ptr()
+    return GpAttnBranch(int(sl), int(r), kp, vp, int(kv_row_stride), int(kv_tok_base), int(bool(kv_sparse_cols)),
+                        o.data_ptr(), lse.data_ptr())
+
+
+def dilated_attn_fwd_ex(q, q_row_stride, q_tok_base, B, L, H, D, win_lo, win_hi, branches, softmax_scale=0.0,
+                        q_log2_prescaled=False):
+    """branches: sequence of GpAttnBranch (attn_branch)."""
+    lib = load_library()
+    if not q.is_cuda or q.dtype != torch.bfloat16:
+        raise TypeError("q must be a bf16 device tensor")
+    arr = (GpAttnBranch * len(branches))(*branches)
+    _check(lib.gp_dilated_attn_fwd_ex(_ptr(q), q_row_stride, q_tok_base, B, L, H, D, win_lo, win_hi,
+                                      ctypes.cast(arr, c_vp), len(branches), float(softmax_scale),
+                                      int(bool(q_log2_prescaled)), _stream()), "gp_dilated_attn_fwd_ex")
+
+
+def dilated_sparsify(src, src_row_stride, k_col, v_col, tok_lo, n_tok, L, H, D, segs, ratios, dsts, dst_bases=None):
+    lib = load_library()
+    _dev(src, torch.bfloat16, "src")
+    for t in dsts:
+        _dev(t, torch.bfloat16, "dst")
+    bases = None if dst_bases is None else (ctypes.c_int64 * len(dst_bases))(*[int(b) for b in dst_bases])
+    _check(lib.gp_dilated_sparsify(_ptr(src), src_row_stride, k_col, v_col, tok_lo, n_tok, L, H, D, _i32_array(segs),
+                                   _i32_array(ratios), len(segs), _ptr_array(dsts), bases, _stream()),
+           "gp_dilated_sparsify")
+
+
+def branch_merge_ln_window(outs, lses, segs, ratios, B, L, tok_lo, n_tok, H, D, ln_w, ln_b, eps, out):
+    lib = load_library()
+    _dev(out, torch.bfloat16, "out")
+    _check(lib.gp_branch_merge_ln_window(_ptr_array(outs), _ptr_array(lses), _i32_array(segs), _i32_array(ratios),
+                                         len(segs), B, L, tok_lo, n_tok, H, D, _ptr(ln_w), _ptr(ln_b), eps, _ptr(out),
+                                         _stream()), "gp_branch_merge_ln_window")
 
 
 def seg_attn_fwd(q, k, v, o, lse, softmax_scale=0.0):

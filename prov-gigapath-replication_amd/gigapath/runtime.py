@@ -290,3 +290,25 @@ def merge_bytes(L: int, segs: Sequence[int], ratios: Sequence[int], H: int, D: i
     E = H * D
     per_tok = sum(E / r * 2 + H / r * 4 for r in ratios) + E * 2
     return float(B * L * per_tok)
+
+
+def attention_valid_flops_window(L: int, segs: Sequence[int], ratios: Sequence[int], H: int, D: int, lo: int,
+                                 hi: int) -> float:
+    """Valid attention FLOPs of the query rows whose sparse_to_dense slot lies in [lo, hi) (one
+    sequence-parallel shard): each such (row, head) costs 4*D*c, c = real keys of its segment."""
+    tot = 0.0
+    p = np.arange(lo, hi, dtype=np.int64)
+    for sl, r in zip(segs, ratios):
+        s, nseg, m = branch_geometry(L, sl, r)
+        hp = H + ((r - H % r) % r)
+        hpg = hp // r
+        g = m * r
+        n = p // g
+        j = (p % g) % r
+        seg_len = np.minimum(L - n * s, s)                 # real tokens of the row's segment
+        rem = seg_len - j
+        c = np.where(rem > 0, -(-rem // r), 0)
+        heads = np.clip(H - j * hpg, 0, hpg)
+        real_q = (p % g) < seg_len                         # a zero-padded query row is not valid work
+        tot += float((4.0 * D * c * heads * real_q).sum())
+    return tot

@@ -1,0 +1,389 @@
+"""Sequence parallelism: one slide's tokens sharded across the GPUs of a node.
+
+The reference has a dormant, rank-aligned K/V all-gather (``DilatedAttention.gather_kv``,
+torchscale/component/dilated_attention.py:55-74, ``Allgather`` component/utils.py:37-50) that
+requires ``segment_length % local_len == 0`` (:57).  This module is its MI355X-native
+replacement for arbitrary shard boundaries:
+
+* **Shards.**  Tokens [0, L) are split into W contiguous ranges [a_w, b_w) (CLS on rank 0),
+  balanced by a per-token cost model (valid attention FLOPs + per-token GEMM/row-kernel work).
+  Everything per token (LN, projections, merge, FFN, residuals) runs on the owner only.
+* **Exchange (one step per layer).**  After the QKV projection, every rank writes token-major
+  sparsified K/V rows of its own tokens for every branch (``gp_dilated_sparsify``: token p keeps
+  the C = (H/r)·D columns of its head group j = (p mod s) mod r, i.e. 1/r of the row).  Rank v
+  needs, for branch b, the gather range of every segment its queries meet:
+  [n_lo·s, min((n_hi+1)·s, L)) with n_lo, n_hi the dense-slot segments of [a_v, b_v).  Each
+  owner sends the intersection of that range with its own tokens directly to v -- one
+  ``batch_isend_irecv`` group of point-to-point RCCL transfers per layer (xGMI is point to point:
+  every rank uses all its links at once, no ring).  When s is not a multiple of r
+  (g = m·r > s), a segment's dense slots sit g - s tokens right of its gather tokens, so the
+  first queries of a shard can need q rows of the left neighbour: a small "q halo" of whole
+  qkv rows rides in the same group.
+* **Compute.**  ``gp_dilated_attn_fwd_ex`` computes exactly the sparse rows whose dense slot lies
+  in [a_v, b_v) (query window), reading q from the local (halo-extended) qkv buffer and K/V from
+  the sparsified buffers.  Branches that need nothing remote are launched before the exchange
+  is waited on (overlap); the rest after.  ``gp_branch_merge_ln_window`` merges the window.
+
+Per-query math is identical to the single-device kernel, so SP output equals the 1-GPU
+output up to the GEMMs' row-count-dependent kernel choice.  Inference only, B = 1.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import _hip, runtime
+
+# per-token time model (seconds) for balancing: attention at ~0.7 PF/s on valid FLOPs, the
+# per-token GEMMs at ~0.9 PF/s and the row kernels at ~4 TB/s (bench.py measurements)
+ATTN_FLOPS_PER_S = 0.7e15
+GEMM_FLOPS_PER_S = 0.9e15
+ROW_BYTES_PER_S = 4.0e12
+
+
+@dataclass(frozen=True)
+class BranchGeo:
+    sl: int
+    r: int
+    s: int
+    nseg: int
+    m: int
+    g: int       # dense length per segment after sparse_to_dense (m * r)
+    hpg: int     # heads per dilation group
+
+
+def branch_geo(L: int, sl: int, r: int, H: int) -> BranchGeo:
+    s, nseg, m = runtime.branch_geometry(L, sl, r)
+    hp = H + (-H) % r
+    return BranchGeo(sl, r, s, nseg, m, m * r, hp // r)
+
+
+def token_cost(L: int, segs: Sequence[int], ratios: Sequence[int], H: int, D: int, F: int) -> np.ndarray:
+    """Modelled forward time of each token (one layer; the shape is what matters)."""
+    E = H * D
+    p = np.arange(L, dtype=np.int64)
+    attn = np.zeros(L, dtype=np.float64)
+    for sl, r in zip(segs, ratios):
+        geo = branch_geo(L, sl, r, H)
+        n = p // geo.g
+        j = (p % geo.g) % r
+        rem = np.minimum(L - n * geo.s, geo.s) - j                   # keys the row's segment/group has
+        c = np.where(rem > 0, -(-rem // r), 0)
+        attn += geo.hpg * 4.0 * D * c
+    lin = 2.0 * (4 * E * E + 2 * E * F)
+    row_bytes = 2 * (E * 12 + F * 4) + E * 6
+    return attn / ATTN_FLOPS_PER_S + lin / GEMM_FLOPS_PER_S + row_bytes / ROW_BYTES_PER_S
+
+
+def balanced_bounds(cost: np.ndarray, world: int) -> List[Tuple[int, int]]:
+    """Contiguous split of the tokens into `world` ranges of near-equal summed cost."""
+    L = len(cost)
+    if world > L:
+        raise ValueError("sequence parallel: %d ranks for %d tokens" % (world, L))
+    cum = np.cumsum(cost)
+    cuts = [0]
+    for w in range(1, world):
+        c = int(np.searchsorted(cum, cum[-1] * w / world))
+        c = max(c, cuts[-1] + 1)
+        c = min(c, L - (world - w))
+        cuts.append(c)
+    cuts.append(L)
+    return [(cuts[w], cuts[w + 1]) for w in range(world)]
+
+
+def _isect(a: Tuple[int, int], b: Tuple[int, int]) -> Tuple[int, int]:
+    lo, hi = max(a[0], b[0]), min(a[1], b[1])
+    return (lo, hi) if lo < hi else (0, 0)
+
+
+class ShardPlan:
+    """All integer bookkeeping of one sharded forward (pure host logic, identical on every rank)."""
+
+    def __init__(self, L: int, world: int, segs: Sequence[int], ratios: Sequence[int], H: int, D: int, F: int,
+                 bounds: Optional[List[Tuple[int, int]]] = None):
+        self.L, self.world, self.H, self.D, self.E = L, world, H, D, H * D
+        self.segs, self.ratios = list(segs), list(ratios)
+        for r in self.ratios:
+            if H % r:
+                raise ValueError("sequence parallel needs H %% r == 0 (H=%d, r=%d)" % (H, r))
+        self.geo = [branch_geo(L, sl, r, H) for sl, r in zip(segs, ratios)]
+        self.C = [(H // r) * D for r in self.ratios]               # sparsified columns of K (and of V)
+        self.bounds = bounds or balanced_bounds(token_cost(L, segs, ratios, H, D, F), world)
+        assert self.bounds[0][0] == 0 and self.bounds[-1][1] == L
+        nb = len(self.geo)
+        # K/V gather range each rank's queries need, per branch
+        self.need = [[self._kv_need(w, b) for b in range(nb)] for w in range(world)]
+        # rows each rank's sparsified buffer of branch b holds: its needs and its own tokens
+        self.buf = [[(min(self.need[w][b][0], self.bounds[w][0]), max(self.need[w][b][1], self.bounds[w][1]))
+                     for b in range(nb)] for w in range(world)]
+        self.q_halo = [max(0, max(self._q_halo(w, b) for b in range(nb))) for w in range(world)]
+        self.branch_halo = [[self._q_halo(w, b) > 0 for b in range(nb)] for w in range(world)]
+
+    # ---- geometry of one rank
+    def _kv_need(self, w: int, b: int) -> Tuple[int, int]:
+        a, e = self.bounds[w]
+        g = self.geo[b]
+        n_lo, n_hi = a // g.g, (e - 1) // g.g
+        return n_lo * g.s, min((n_hi + 1) * g.s, self.L)
+
+    def _q_halo(self, w: int, b: int) -> int:
+        """Tokens left of a_w whose q rows the window's sparse rows read (0 when g == s)."""
+        a, e = self.bounds[w]
+        g = self.geo[b]
+        n_lo, n_hi = a // g.g, (e - 1) // g.g
+        lowest = a - n_lo * (g.g - g.s)
+        if n_hi > n_lo:
+            lowest = min(lowest, (n_lo + 1) * g.s)
+        return max(0, a - lowest)
+
+    def recvs(self, v: int) -> List[Tuple[int, int, int, int]]:
+        """(branch, src, lo, hi) token ranges rank v receives (canonical order: branch, src)."""
+        out = []
+        for b in range(len(self.geo)):
+            for w in range(self.world):
+                if w == v:
+                    continue
+                lo, hi = _isect(self.need[v][b], self.bounds[w])
+                if hi > lo:
+                    out.append((b, w, lo, hi))
+        return out
+
+    def sends(self, w: int) -> List[Tuple[int, int, int, int]]:
+        """(branch, dst, lo, hi) token ranges rank w sends, in the order receivers post them."""
+        out = []
+        for b in range(len(self.geo)):
+            for v in range(self.world):
+                if v == w:
+                    continue
+                lo, hi = _isect(self.need[v][b], self.bounds[w])
+                if hi > lo:
+                    out.append((b, v, lo, hi))
+        return out
+
+    def halo_recvs(self, v: int) -> List[Tuple[int, int, int]]:
+        a = self.bounds[v][0]
+        rng = (a - self.q_halo[v], a)
+        return [(w, lo, hi) for w in range(self.world) if w != v
+                for lo, hi in [_isect(rng, self.bounds[w])] if hi > lo]
+
+    def halo_sends(self, w: int) -> List[Tuple[int, int, int]]:
+        out = []
+        for v in range(self.world):
+            if v == w:
+                continue
+            a = self.bounds[v][0]
+            lo, hi = _isect((a - self.q_halo[v], a), self.bounds[w])
+            if hi > lo:
+                out.append((v, lo, hi))
+        return out
+
+    def local_branches(self, v: int) -> List[int]:
+        """Branches rank v can compute before its exchange completes."""
+        remote = {b for b, _, _, _ in self.recvs(v)}
+        return [b for b in range(len(self.geo)) if b not in remote and not self.branch_halo[v][b]]
+
+    def exchange_bytes(self, v: int) -> int:
+        """bf16 bytes rank v receives per layer."""
+        tot = sum((hi - lo) * 2 * self.C[b] * 2 for b, _, lo, hi in self.recvs(v))
+        tot += sum((hi - lo) * 3 * self.E * 2 for _, lo, hi in self.halo_recvs(v))
+        return tot
+
+
+# ------------------------------------------------------------------------------------------
+# exchange transport
+# ------------------------------------------------------------------------------------------
+class P2PExchange:
+    """One group of point-to-point transfers.  RCCL ("nccl" backend): device tensors, the group is
+    enqueued behind the current stream and `wait()` makes the current stream wait on it (no host
+    sync).  gloo (CPU tests, one-GPU rehearsals): staged through host memory, synchronous."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        self.dist = dist
+        self.group = group
+        self.backend = dist.get_backend(group)
+        self.device_comm = self.backend == "nccl"
+
+    def peer(self, r: int) -> int:
+        return r if self.group is None else self.dist.get_global_rank(self.group, r)
+
+    def run(self, sends: List[Tuple[int, torch.Tensor]], recvs: List[Tuple[int, torch.Tensor]]):
+        """Post all transfers; returns a handle for wait()."""
+        dist = self.dist
+        if not sends and not recvs:
+            return None
+        if self.device_comm:
+            ops = [dist.P2POp(dist.isend, t, self.peer(p), self.group) for p, t in sends]
+            ops += [dist.P2POp(dist.irecv, t, self.peer(p), self.group) for p, t in recvs]
+            return ("dev", dist.batch_isend_irecv(ops))
+        hs = [(p, t.detach().to("cpu", copy=True)) for p, t in sends]
+        hr = [(p, torch.empty(t.shape, dtype=t.dtype)) for p, t in recvs]
+        ops = [dist.P2POp(dist.isend, t, self.peer(p), self.group) for p, t in hs]
+        ops += [dist.P2POp(dist.irecv, t, self.peer(p), self.group) for p, t in hr]
+        works = dist.batch_isend_irecv(ops)
+        for wk in works:
+            wk.wait()
+        for (_, dst), (_, src) in zip(recvs, hr):
+            dst.copy_(src)
+        return None
+
+    def all_reduce_(self, t: torch.Tensor):
+        """In-place SUM over the group (host-staged under gloo)."""
+        if self.device_comm or not t.is_cuda:
+            self.dist.all_reduce(t, group=self.group)
+            return t
+        h = t.detach().to("cpu", copy=True)
+        self.dist.all_reduce(h, group=self.group)
+        t.copy_(h)
+        return t
+
+    def broadcast_(self, t: torch.Tensor, src_rank: int = 0):
+        """In-place broadcast from group rank `src_rank` (host-staged under gloo)."""
+        src = self.peer(src_rank)
+        if self.device_comm or not t.is_cuda:
+            self.dist.broadcast(t, src=src, group=self.group)
+            return t
+        h = t.detach().to("cpu", copy=True)
+        self.dist.broadcast(h, src=src, group=self.group)
+        t.copy_(h)
+        return t
+
+    @staticmethod
+    def wait(handle):
+        if handle is None:
+            return
+        for wk in handle[1]:
+            wk.wait()
+
+
+# ------------------------------------------------------------------------------------------
+# per-rank engine
+# ------------------------------------------------------------------------------------------
+class ShardWorkspace:
+    def __init__(self, plan: ShardPlan, rank: int, dev, F: int):
+        E, H, D = plan.E, plan.H, plan.D
+        a, e = plan.bounds[rank]
+        self.rank = rank
+        self.n = e - a
+        self.hq = plan.q_halo[rank]
+        self.x = torch.empty(self.n, E, dtype=torch.float32, device=dev)
+        self.a = torch.empty(self.n, E, dtype=torch.bfloat16, device=dev)
+        self.qkv_ext = torch.empty(self.hq + self.n, 3 * E, dtype=torch.bfloat16, device=dev)
+        self.qkv = self.qkv_ext[self.hq:]
+        self.y = torch.empty(self.n, E, dtype=torch.bfloat16, device=dev)
+        self.f = torch.empty(self.n, F, dtype=torch.bfloat16, device=dev)
+        self.kvs, self.kv_base = [], []
+        for b in range(len(plan.geo)):
+            lo, hi = plan.buf[rank][b]
+            self.kvs.append(torch.empty(hi - lo, 2 * plan.C[b], dtype=torch.bfloat16, device=dev))
+            self.kv_base.append(lo)
+        # branch outputs keep the single-device layout; only the window's rows are written/read
+        self.attn = runtime.AttentionScratch(dev, 1, plan.L, H, D, plan.segs, plan.ratios)
+
+
+class SeqParallelEngine:
+    """Runs the encoder layers of one rank's shard.  `layers` are runtime.PackedLayer."""
+
+    def __init__(self, plan: ShardPlan, rank: int, exchange: P2PExchange):
+        self.plan, self.rank, self.xch = plan, rank, exchange
+        self._sends = plan.sends(rank)
+        self._recvs = plan.recvs(rank)
+        self._hsends = plan.halo_sends(rank)
+        self._hrecvs = plan.halo_recvs(rank)
+        self._local = plan.local_branches(rank)
+        self._remote = [b for b in range(len(plan.geo)) if b not in self._local]
+
+    def _kv_view(self, ws: ShardWorkspace, b: int, lo: int, hi: int) -> torch.Tensor:
+        base = ws.kv_base[b]
+        return ws.kvs[b][lo - base:hi - base]
+
+    def exchange(self, ws: ShardWorkspace):
+        a = self.plan.bounds[self.rank][0]
+        sends = [(dst, self._kv_view(ws, b, lo, hi)) for b, dst, lo, hi in self._sends]
+        recvs = [(src, self._kv_view(ws, b, lo, hi)) for b, src, lo, hi in self._recvs]
+        sends += [(dst, ws.qkv[lo - a:hi - a]) for dst, lo, hi in self._hsends]
+        recvs += [(src, ws.qkv_ext[lo - (a - ws.hq):hi - (a - ws.hq)]) for src, lo, hi in self._hrecvs]
+        return self.xch.run(sends, recvs)
+
+    def attention(self, pa: runtime.PackedAttention, ws: ShardWorkspace, branches: List[int]):
+        if not branches:
+            return
+        plan = self.plan
+        a, e = plan.bounds[self.rank]
+        descs = []
+        for b in branches:
+            C = plan.C[b]
+            kv = ws.kvs[b]
+            descs.append(_hip.attn_branch(plan.segs[b], plan.ratios[b], kv, kv.data_ptr() + 2 * C, 2 * C,
+                                          ws.kv_base[b], True, ws.attn.outs[b], ws.attn.lses[b]))
+        with runtime.TIMER.span("attn"):
+            _hip.dilated_attn_fwd_ex(ws.qkv_ext, 3 * plan.E, a - ws.hq, 1, plan.L, plan.H, plan.D, a, e, descs, 0.0,
+                                     pa.prescaled)
+
+    def run_layers(self, layers, ws: ShardWorkspace, layer_hook=None):
+        """ws.x holds this shard's fp32 embedding and ws.a = LN1_0(ws.x).  Runs every layer in place."""
+        plan = self.plan
+        E, H, D = plan.E, plan.H, plan.D
+        a, e = plan.bounds[self.rank]
+        M = ws.n
+        F = ws.f.shape[1]
+        nl = len(layers)
+        for li, pl in enumerate(layers):
+            pa = pl.attn
+            with runtime.TIMER.span("gemm_qkv"):
+                torch.addmm(pa.b_qkv, ws.a, pa.w_qkv.t(), out=ws.qkv)
+            with runtime.TIMER.span("sparsify"):
+                _hip.dilated_sparsify(ws.qkv, 3 * E, E, 2 * E, a, M, plan.L, H, D, plan.segs, plan.ratios, ws.kvs,
+                                      ws.kv_base)
+            handle = self.exchange(ws)
+            self.attention(pa, ws, self._local)
+            P2PExchange.wait(handle)
+            self.attention(pa, ws, self._remote)
+            with runtime.TIMER.span("merge"):
+                _hip.branch_merge_ln_window(ws.attn.outs, ws.attn.lses, plan.segs, plan.ratios, 1, plan.L, a, M, H, D,
+                                            pa.ln_w, pa.ln_b, pa.ln_eps, ws.a)
+            with runtime.TIMER.span("gemm_out"):
+                torch.mm(ws.a, pa.w_o.t(), out=ws.y)
+            with runtime.TIMER.span("resid_ln"):
+                _hip.residual_layernorm(ws.x, ws.y, pa.b_o, pl.ln2_w, pl.ln2_b, pl.ln2_eps, ws.a, M, E)
+            with runtime.TIMER.span("gemm_fc1"):
+                torch.addmm(pl.b1, ws.a, pl.w1.t(), out=ws.f)
+            with runtime.TIMER.span("gelu_ln"):
+                _hip.gelu_layernorm(ws.f, pl.fln_w, pl.fln_b, pl.fln_eps, ws.f, M, F)
+            with runtime.TIMER.span("gemm_fc2"):
+                torch.mm(ws.f, pl.w2.t(), out=ws.y)
+            nxt = layers[li + 1] if li + 1 < nl else None
+            with runtime.TIMER.span("resid_ln"):
+                _hip.residual_layernorm(ws.x, ws.y, pl.b2, nxt.ln1_w if nxt else None, nxt.ln1_b if nxt else None,
+                                        nxt.ln1_eps if nxt else 1e-5, ws.a, M, E)
+            if layer_hook is not None:
+                layer_hook(li + 1)
+
+
+class SeqParallelContext:
+    """Attached to a LongNetViT by ``enable_sequence_parallel``; caches plans and workspaces."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        if not dist.is_initialized():
+            raise RuntimeError("sequence parallel needs torch.distributed to be initialised")
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.exchange = P2PExchange(group)
+        self._key = None
+        self.plan: Optional[ShardPlan] = None
+        self.ws: Optional[ShardWorkspace] = None
+        self.engine: Optional[SeqParallelEngine] = None
+
+    def prepare(self, dev, L: int, segs, ratios, H: int, D: int, F: int):
+        key = (str(dev), L, tuple(segs), tuple(ratios), H, D, F)
+        if key != self._key:
+            self.plan = ShardPlan(L, self.world, segs, ratios, H, D, F)
+            self.ws = ShardWorkspace(self.plan, self.rank, dev, F)
+            self.engine = SeqParallelEngine(self.plan, self.rank, self.exchange)
+            self._key = key
+        return self.plan, self.ws, self.engine

@@ -84,7 +84,21 @@ class LongNetViT(nn.Module):
         self._top_sig = None
         self._top = None
         self._pos_full = None
+        self._sp = None
         self.initialize_vit_weights()
+
+    # ---------------------------------------------------------------- sequence parallel
+    def enable_sequence_parallel(self, group=None):
+        """Shard every forward's tokens across the ranks of `group` (one process per GPU,
+        torch.distributed initialised; RCCL for device transfers).  Every rank calls forward with
+        the same full slide and gets the same outputs (seqpar.py)."""
+        from . import seqpar
+        self._sp = seqpar.SeqParallelContext(group)
+        return self
+
+    def disable_sequence_parallel(self):
+        self._sp = None
+        return self
 
     # ---------------------------------------------------------------- init / helpers
     def initialize_vit_weights(self):
@@ -161,6 +175,8 @@ class LongNetViT(nn.Module):
         if coords.shape != (B, N, 2):
             raise ValueError("coords must be [B, N, 2], got %s" % (tuple(coords.shape),))
         E, L, M = self.embed_dim, N + 1, B * (N + 1)
+        if self._sp is not None and self._sp.world > 1:
+            return self._forward_sp(x, coords, all_layer_embed)
         top = self._packed_top(dev)
         eng = self.encoder.engine
         layers = eng.pack(self.encoder, dev)
@@ -206,6 +222,83 @@ class LongNetViT(nn.Module):
                 cls_rows = torch.empty(B, E, dtype=torch.float32, device=dev)
                 _hip.layernorm_f32(ws.x, L * E, top["enc_w"], top["enc_b"], top["enc_eps"], cls_rows, B, E)
                 _hip.layernorm_f32(cls_rows, E, top["norm_w"], top["norm_b"], top["norm_eps"], res[0], B, E)
+        out_dtype = self.norm.weight.dtype
+        return [res[i].to(out_dtype) for i in range(n_out)]
+
+
+    def _forward_sp(self, x, coords, all_layer_embed):
+        """Sequence-parallel forward of one slide (B = 1): this rank embeds and encodes tokens
+        [a, b) and exchanges sparsified K/V per layer; rank 0 reads out the CLS row (global pool:
+        all-reduced token sums) and broadcasts the result."""
+        sp = self._sp
+        B, N, C = x.shape
+        if B != 1:
+            raise ValueError("sequence parallel forward takes one slide (B = 1), got B = %d" % B)
+        dev = self.cls_token.device
+        E, L = self.embed_dim, N + 1
+        top = self._packed_top(dev)
+        eng = self.encoder.engine
+        layers = eng.pack(self.encoder, dev)
+        pa = layers[0].attn
+        F = self.encoder.args.encoder_ffn_embed_dim
+        plan, ws, spe = sp.prepare(dev, L, pa.segs, pa.ratios, pa.H, pa.D, F)
+        a, e = plan.bounds[sp.rank]
+        t0, t1 = max(a, 1) - 1, e - 1                      # tiles of this shard (token = tile + 1)
+        nt = t1 - t0
+        if not hasattr(ws, "pos") or ws.pos.numel() != nt:
+            ws.pos = torch.empty(max(nt, 1), dtype=torch.int64, device=dev)
+            ws.err = torch.zeros(1, dtype=torch.int32, device=dev)
+        xp = ws.y[:nt]
+        if nt > 0:
+            with runtime.TIMER.span("gemm_patch"):
+                torch.addmm(top["bp"], x[0, t0:t1].to(torch.bfloat16), top["wp"].t(), out=xp)
+        c = coords if coords.dtype in (torch.float32, torch.float64) else coords.float()
+        ws.err.zero_()
+        if nt > 0:
+            _hip.coords_to_pos(c[0, t0:t1].contiguous(), self.slide_ngrids, self.tile_size, ws.pos[:nt], ws.err)
+        if self.validate_positions:
+            err = sp.exchange.all_reduce_(ws.err.clone())
+            if int(err.item()) > 0:
+                raise IndexError("coords map outside pos_embed (%d rows): %d tiles" %
+                                 (self.slide_ngrids ** 2 + 1, int(err.item())))
+        with runtime.TIMER.span("posembed"):
+            _hip.posembed_cls_ln(xp, ws.pos, top["tab"], top["cls"] if a == 0 else None, 1, nt, E, self.slide_ngrids,
+                                 top["ln1_w"], top["ln1_b"], top["ln1_eps"], ws.x, ws.a)
+        n_out = (1 + len(layers)) if all_layer_embed else 1
+        res = torch.zeros(n_out, 1, E, dtype=torch.float32, device=dev)
+        pool = torch.empty(1, E, dtype=torch.float32, device=dev)
+
+        def pooled(src):
+            """mean over tiles 1..L-1 of src (this shard's [n, E] rows), all-reduced."""
+            start = 1 if a == 0 else 0
+            if ws.n > start:
+                _hip.mean_tokens(src, 1, ws.n, E, start, pool)
+                pool.mul_(float(ws.n - start))
+            else:
+                pool.zero_()
+            sp.exchange.all_reduce_(pool)
+            pool.div_(float(L - 1))
+            return pool
+
+        def readout(slot: int):
+            if self.global_pool:
+                _hip.layernorm_f32(pooled(ws.x), E, top["norm_w"], top["norm_b"], top["norm_eps"], res[slot], 1, E)
+            elif a == 0:
+                _hip.layernorm_f32(ws.x, E, top["norm_w"], top["norm_b"], top["norm_eps"], res[slot], 1, E)
+
+        if all_layer_embed:
+            readout(0)
+        spe.run_layers(layers, ws, readout if all_layer_embed else None)
+        if not all_layer_embed:
+            if self.global_pool:
+                _hip.layernorm_f32(ws.x, E, top["enc_w"], top["enc_b"], top["enc_eps"], ws.x, ws.n, E)
+                readout(0)
+            elif a == 0:
+                cls_rows = torch.empty(1, E, dtype=torch.float32, device=dev)
+                _hip.layernorm_f32(ws.x, E, top["enc_w"], top["enc_b"], top["enc_eps"], cls_rows, 1, E)
+                _hip.layernorm_f32(cls_rows, E, top["norm_w"], top["norm_b"], top["norm_eps"], res[0], 1, E)
+        if not self.global_pool:
+            sp.exchange.broadcast_(res, 0)
         out_dtype = self.norm.weight.dtype
         return [res[i].to(out_dtype) for i in range(n_out)]
 

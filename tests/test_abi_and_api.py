@@ -68,6 +68,14 @@ def test_argument_errors_are_reported_without_gpu():
     assert b"head dim 40" in lib.gp_last_error_string()
     rc = lib.gp_residual_layernorm(None, None, None, None, None, 1e-5, None, 4, 100, None)
     assert rc == -1 and b"cols=100" in lib.gp_last_error_string()
+    br = (_hip.GpAttnBranch * 1)(_hip.GpAttnBranch(1024, 1, 16, 16, 2304, 0, 0, 16, 16))
+    rc = lib.gp_dilated_attn_fwd_ex(16, 2304, 0, 1, 100, 16, 48, 50, 101, br, 1, 0.0, 0, None)
+    assert rc == -1 and b"bad window" in lib.gp_last_error_string()
+    rc = lib.gp_dilated_sparsify(16, 2304, 768, 1536, 0, 10, 100, 16, 48, (ctypes.c_int32 * 1)(1024),
+                                 (ctypes.c_int32 * 1)(3), 1, (ctypes.c_void_p * 1)(16), None, None)
+    assert rc == -1 and b"H % r == 0" in lib.gp_last_error_string()
+    rc = lib.gp_branch_merge_ln_window(None, None, None, None, 1, 1, 100, 90, 20, 16, 48, None, None, 1e-5, None, None)
+    assert rc == -1
 
 
 # ------------------------------------------------------------------ Python drop-in surface

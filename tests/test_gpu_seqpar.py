@@ -1,0 +1,88 @@
+"""Sequence-parallel forward on a real GPU (run with -m gpu).
+
+W ranks run as separate processes on cuda:0 with the gloo backend (host-staged exchange; the
+pool's boxes have one GPU, and RCCL needs one GPU per rank): every HIP kernel of the sharded
+path runs for real, only the transport differs from the 8-GPU RCCL run.  The result must match
+the single-device forward of the same model (same kernels per query; only the GEMMs' row
+count differs between shard and whole slide).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _model(max_wsi_size):
+    import oracle as orc
+    from gigapath import slide_encoder
+    cfg = orc.arch_config("gigapath_slide_enc12l768d", max_wsi_size=max_wsi_size)
+    m = slide_encoder.create_model("", "gigapath_slide_enc12l768d", 1536, max_wsi_size=max_wsi_size)
+    W = orc.make_weights(cfg, seed=0)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()}, strict=True)
+    return m.cuda().eval()
+
+
+def _worker(rank, world, port, N, max_wsi_size, global_pool, q):
+    try:
+        import torch.distributed as dist
+        import oracle as orc
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        model = _model(max_wsi_size)
+        model.global_pool = global_pool
+        x, coords = orc.synthetic_slide(N)
+        xt, ct = torch.from_numpy(x).cuda(), torch.from_numpy(coords).cuda()
+        model.enable_sequence_parallel()
+        with torch.no_grad():
+            out = torch.stack(model(xt, ct, all_layer_embed=True)).cpu().numpy()
+            last = model(xt, ct)[0].cpu().numpy()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, (out, last)))
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("world,N,max_wsi,gp", [(2, 5000, 262144, False), (3, 30000, 250000, False),
+                                                 (4, 3000, 262144, True)])
+def test_sequence_parallel_matches_single_device(world, N, max_wsi, gp):
+    import oracle as orc
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, N, max_wsi, gp, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    for r, v in res.items():
+        assert not isinstance(v, str), v
+    model = _model(max_wsi)
+    model.global_pool = gp
+    x, coords = orc.synthetic_slide(N)
+    with torch.no_grad():
+        ref = torch.stack(model(torch.from_numpy(x).cuda(), torch.from_numpy(coords).cuda(),
+                                all_layer_embed=True)).cpu().numpy()
+        ref_last = model(torch.from_numpy(x).cuda(), torch.from_numpy(coords).cuda())[0].cpu().numpy()
+    for r in range(world):
+        out, last = res[r]
+        for got, want in ((out, ref), (last, ref_last)):
+            d = np.abs(got - want).max() / np.abs(want).max()
+            cos = (got * want).sum() / np.sqrt((got * got).sum() * (want * want).sum())
+            # the per-query attention math is identical; GEMMs over fewer rows may pick other
+            # hipBLASLt kernels -> bf16-level noise only
+            assert d <= 1e-2 and cos >= 0.99995, (r, d, cos)

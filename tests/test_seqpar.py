@@ -1,0 +1,235 @@
+"""Sequence-parallel bookkeeping and exchange (CPU: planner logic + gloo world_size 2..4).
+
+The GPU half (the sharded forward against the single-device forward) is in test_gpu_seqpar.py.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle as orc
+from gigapath import seqpar
+
+H, D = 16, 48
+E, F = H * D, 4 * H * D
+DEFAULT = ([1024, 5792, 32768, 185363, 1048576], [1, 2, 4, 8, 16])
+WSI250K = ([1024, 4870, 23170, 110217, 524288], [1, 2, 4, 8, 16])
+SMALL_MISALIGNED = ([32, 60, 90, 123, 1000], [1, 2, 4, 8, 16])
+
+
+def sparsify_ref(qkv, L, segs, ratios):
+    """numpy restatement of gp_dilated_sparsify over all tokens: [L, 2C] per branch."""
+    out = []
+    p = np.arange(L)
+    for sl, r in zip(segs, ratios):
+        s = min(sl, L)
+        C = (H // r) * D
+        j = (p % s) % r
+        cols = j[:, None] * C + np.arange(C)[None, :]
+        k = np.take_along_axis(qkv[:, E:2 * E], cols, 1)
+        v = np.take_along_axis(qkv[:, 2 * E:], cols, 1)
+        out.append(np.concatenate([k, v], 1))
+    return out
+
+
+@pytest.mark.parametrize("L,world,sched", [
+    (1025, 2, DEFAULT), (16385, 3, DEFAULT), (70001, 8, DEFAULT), (256001, 8, DEFAULT),
+    (250001, 8, WSI250K), (1001, 5, SMALL_MISALIGNED), (3000, 7, SMALL_MISALIGNED), (37, 4, SMALL_MISALIGNED),
+])
+def test_plan_covers_every_row_the_merge_reads(L, world, sched):
+    segs, ratios = sched
+    plan = seqpar.ShardPlan(L, world, segs, ratios, H, D, F)
+    # shards tile [0, L) contiguously
+    assert [a for a, _ in plan.bounds[1:]] == [e for _, e in plan.bounds[:-1]]
+    assert plan.bounds[0][0] == 0 and plan.bounds[-1][1] == L
+    assert all(e > a for a, e in plan.bounds)
+    for v in range(world):
+        a, e = plan.bounds[v]
+        for b, (sl, r) in enumerate(zip(segs, ratios)):
+            geo = orc.branch_geometry(L, sl, r, H)
+            s, m, nseg = geo["s"], geo["m"], geo["nseg"]
+            g = m * r
+            # every dense slot of the window maps to a sparse row (n, i, j) -- the merge reads it
+            p = np.arange(a, e)
+            n, t = p // g, p % g
+            i, j = t // r, t % r
+            assert (n < nseg).all()
+            gather_tok = n * s + i * r + j
+            valid = (i * r + j < s) & (gather_tok < L)
+            # its query is local or in the q halo
+            assert (gather_tok[valid] >= a - plan.q_halo[v]).all() and (gather_tok[valid] < e).all()
+            # all keys of its segment are in the rank's K/V range and buffer
+            lo, hi = plan.need[v][b]
+            seg_lo, seg_hi = n * s, np.minimum((n + 1) * s, L)
+            assert lo <= seg_lo.min() and hi >= seg_hi.max()
+            blo, bhi = plan.buf[v][b]
+            assert blo <= min(lo, a) and bhi >= max(hi, e)
+        # every received range is owned by its sender and lands inside the buffer
+        for b, w, lo, hi in plan.recvs(v):
+            wa, we = plan.bounds[w]
+            assert wa <= lo < hi <= we and plan.buf[v][b][0] <= lo and hi <= plan.buf[v][b][1]
+    # sends and receives match pairwise, in the same order
+    for w in range(world):
+        for v in range(world):
+            if v == w:
+                continue
+            s_wv = [(b, lo, hi) for b, dst, lo, hi in plan.sends(w) if dst == v]
+            r_vw = [(b, lo, hi) for b, src, lo, hi in plan.recvs(v) if src == w]
+            assert s_wv == r_vw
+            hs = [(lo, hi) for dst, lo, hi in plan.halo_sends(w) if dst == v]
+            hr = [(lo, hi) for src, lo, hi in plan.halo_recvs(v) if src == w]
+            assert hs == hr
+
+
+def test_balanced_bounds_equalise_modelled_cost():
+    L = 256001
+    cost = seqpar.token_cost(L, *DEFAULT, H, D, F)
+    bounds = seqpar.balanced_bounds(cost, 8)
+    per = np.array([cost[a:e].sum() for a, e in bounds])
+    assert per.max() / per.mean() < 1.01
+    # the last b=3 segment (70,638 real tokens) is cheaper per token than the first
+    assert bounds[-1][1] - bounds[-1][0] > bounds[0][1] - bounds[0][0]
+
+
+def test_exchange_volume_is_sparse():
+    """At 256k / 8 ranks each rank receives far less than the dense K/V (786 MB per layer)."""
+    plan = seqpar.ShardPlan(256001, 8, *DEFAULT, H, D, F)
+    dense = 256001 * 2 * E * 2
+    vols = [plan.exchange_bytes(v) for v in range(8)]
+    assert max(vols) < 0.45 * dense, [v / 1e6 for v in vols]
+    assert plan.q_halo[0] == 0
+
+
+def test_misaligned_schedule_has_q_halo():
+    plan = seqpar.ShardPlan(256001, 8, *WSI250K, H, D, F)
+    assert max(plan.q_halo) > 0            # 23170 % 4 != 0, 110217 % 8 != 0: dense slots shift right
+
+
+# ------------------------------------------------------------------ gloo exchange
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _exchange_worker(rank, world, port, L, segs, ratios, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        rng = np.random.default_rng(7)
+        qkv = rng.standard_normal((L, 3 * E)).astype(np.float32)      # same "global" projection on every rank
+        ref = sparsify_ref(qkv, L, segs, ratios)
+        plan = seqpar.ShardPlan(L, world, segs, ratios, H, D, F)
+        ws = seqpar.ShardWorkspace(plan, rank, "cpu", F)
+        a, e = plan.bounds[rank]
+        for t in ws.kvs:
+            t.fill_(float("nan"))
+        ws.qkv_ext.fill_(float("nan"))
+        ws.qkv.copy_(torch.from_numpy(qkv[a:e]).to(ws.qkv.dtype))
+        for b in range(len(segs)):                       # this rank's own sparsified rows
+            lo = ws.kv_base[b]
+            ws.kvs[b][a - lo:e - lo] = torch.from_numpy(ref[b][a:e]).to(ws.kvs[b].dtype)
+        eng = seqpar.SeqParallelEngine(plan, rank, seqpar.P2PExchange())
+        seqpar.P2PExchange.wait(eng.exchange(ws))
+        for b in range(len(segs)):
+            lo, hi = plan.need[rank][b]
+            base = ws.kv_base[b]
+            got = ws.kvs[b][lo - base:hi - base].float().numpy()
+            want = torch.from_numpy(ref[b][lo:hi]).to(ws.kvs[b].dtype).float().numpy()
+            assert np.array_equal(got, want), ("branch", b)
+        if ws.hq:
+            got = ws.qkv_ext[:ws.hq].float().numpy()
+            want = torch.from_numpy(qkv[a - ws.hq:a]).to(ws.qkv.dtype).float().numpy()
+            assert np.array_equal(got, want)
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, "ok"))
+    except Exception as ex:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, traceback.format_exc() + repr(ex)))
+
+
+@pytest.mark.parametrize("world,L,sched", [(2, 3001, DEFAULT), (3, 5000, SMALL_MISALIGNED),
+                                           (4, 2000, WSI250K)])
+def test_gloo_exchange_delivers_every_needed_row(world, L, sched):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, L, sched[0], sched[1], q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert all(v == "ok" for v in res.values()), res
+
+
+# ------------------------------------------------------------------ sharded forward, CPU stand-in kernels
+SP_SCHED = ([64, 130, 250, 333, 1000], [1, 2, 4, 8, 16])      # multi-segment, misaligned (q halos)
+
+
+def _sp_model(segs, ratios):
+    from gigapath import slide_encoder
+    cfg = orc.arch_config("gigapath_slide_enc12l768d")
+    cfg["segment_length"], cfg["dilated_ratio"] = list(segs), list(ratios)
+    m = slide_encoder.create_model("", "gigapath_slide_enc12l768d", 1536)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in orc.make_weights(cfg, seed=0).items()}, strict=True)
+    m.encoder.args.segment_length, m.encoder.args.dilated_ratio = list(segs), list(ratios)
+    return m.eval(), cfg
+
+
+def _sp_forward_worker(rank, world, port, N, gp, q):
+    try:
+        import sp_emulator
+        sp_emulator.install()
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.set_num_threads(2)
+        model, _ = _sp_model(*SP_SCHED)
+        model.global_pool = gp
+        model.enable_sequence_parallel()
+        x, coords = orc.synthetic_slide(N)
+        with torch.no_grad():
+            out = torch.stack(model._forward_sp(torch.from_numpy(x), torch.from_numpy(coords), True)).numpy()
+            last = model._forward_sp(torch.from_numpy(x), torch.from_numpy(coords), False)[0].numpy()
+        dist.destroy_process_group()
+        q.put((rank, (out, last)))
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("world,N,gp", [(2, 600, False), (3, 700, True)])
+def test_sharded_forward_matches_oracle_with_cpu_kernels(world, N, gp):
+    """LongNetViT._forward_sp end to end over gloo with every HIP call replaced by an
+    address-checking CPU stand-in (tests/sp_emulator.py): shard bounds, K/V and q-halo
+    exchange, query windows, window merge, readouts, all-reduce/broadcast."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sp_forward_worker, args=(r, world, port, N, gp, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=600) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    for v in res.values():
+        assert not isinstance(v, str), v
+    _, cfg = _sp_model(*SP_SCHED)
+    W = {k: torch.from_numpy(v) for k, v in orc.make_weights(cfg, seed=0).items()}
+    x, coords = orc.synthetic_slide(N)
+    ref = torch.stack(orc.slide_encoder_forward(W, x, coords, cfg, all_layer_embed=True, global_pool=gp)).numpy()
+    ref_last = orc.slide_encoder_forward(W, x, coords, cfg, global_pool=gp)[0].numpy()
+    for r in range(world):
+        out, last = res[r]
+        for got, want in ((out, ref), (last, ref_last)):
+            for idx in np.ndindex(*got.shape[:-1]):
+                g_, w_ = got[idx].astype(np.float64), want[idx].astype(np.float64)
+                rel = np.abs(g_ - w_).max() / np.abs(w_).max()
+                cos = (g_ * w_).sum() / np.sqrt((g_ * g_).sum() * (w_ * w_).sum())
+                assert rel <= 2e-2 and cos >= 0.9995, (r, idx, rel, cos)
