@@ -28,6 +28,7 @@ extern "C" {
 #define GP_ABI_VERSION 2
 #define GP_EARG (-1)
 #define GP_MAX_BRANCHES 8
+#define GP_MAX_DESTS 8
 
 /* ABI version of the loaded library (== GP_ABI_VERSION). */
 int gp_abi_version(void);
@@ -128,6 +129,23 @@ int gp_dilated_sparsify(const uint16_t* src, int64_t src_row_stride, int64_t k_c
                         int64_t tok_lo, int64_t n_tok, int64_t L, int H, int D, const int32_t* seg_len,
                         const int32_t* ratios, int nbranch, uint16_t* const* dst,
                         const int64_t* dst_tok_base, void* stream);
+
+/* One destination of gp_dilated_sparsify_dests: tokens [tok_lo, tok_hi) of a branch, token p
+ * written at dst + (p - tok_lo) * 2C (a peer's chunk of an all-to-all send buffer). */
+typedef struct GpRowDest {
+  int64_t tok_lo;
+  int64_t tok_hi;
+  uint16_t* dst;
+} GpRowDest;
+
+/* gp_dilated_sparsify writing each token's branch row to every destination whose range holds it
+ * (up to GP_MAX_DESTS per branch): the sequence-parallel send buffers, packed per peer, in one
+ * pass.  dests: [nbranch * GP_MAX_DESTS] (branch b's entries at b*GP_MAX_DESTS ..), ndest:
+ * [nbranch] entries used per branch. */
+int gp_dilated_sparsify_dests(const uint16_t* src, int64_t src_row_stride, int64_t k_col, int64_t v_col,
+                              int64_t tok_lo, int64_t n_tok, int64_t L, int H, int D, const int32_t* seg_len,
+                              const int32_t* ratios, int nbranch, const GpRowDest* dests,
+                              const int32_t* ndest, void* stream);
 
 /* Drop-in for the operator seam flash_attn_func(q, k, v, 0.0, None, scale, False)
  * (torchscale/component/flash_attention.py:13-16): non-causal, no mask, dropout 0.

@@ -900,8 +900,9 @@ struct SparsifyArgs {
   int64_t tok_lo, ntok, L;
   int32_t nbranch, per_tok;            // 16-byte chunks per token over all branches
   int32_t s[GP_MAX_BRANCHES], r[GP_MAX_BRANCHES], C[GP_MAX_BRANCHES], cbeg[GP_MAX_BRANCHES + 1];
-  uint16_t* dst[GP_MAX_BRANCHES];
-  int64_t dst_base[GP_MAX_BRANCHES];   // token held by row 0 of dst[b]
+  int32_t ndest[GP_MAX_BRANCHES];
+  int64_t lo[GP_MAX_BRANCHES][GP_MAX_DESTS], hi[GP_MAX_BRANCHES][GP_MAX_DESTS];
+  uint16_t* dst[GP_MAX_BRANCHES][GP_MAX_DESTS];   // row of token lo
 };
 
 __global__ __launch_bounds__(256) void dilated_sparsify_kernel(const SparsifyArgs a) {
@@ -921,43 +922,76 @@ __global__ __launch_bounds__(256) void dilated_sparsify_kernel(const SparsifyArg
   const int64_t p = a.tok_lo + t;
   const int j = (int)(p % a.s[b]) % a.r[b];
   const uint4 v = *reinterpret_cast<const uint4*>(a.src + t * a.src_stride + (kv ? a.v_col : a.k_col) + (int64_t)j * C + ch * 8);
-  *reinterpret_cast<uint4*>(a.dst[b] + (p - a.dst_base[b]) * (2 * (int64_t)C) + kv * C + ch * 8) = v;
+  for (int d = 0; d < a.ndest[b]; ++d)
+    if (p >= a.lo[b][d] && p < a.hi[b][d])
+      *reinterpret_cast<uint4*>(a.dst[b][d] + (p - a.lo[b][d]) * (2 * (int64_t)C) + kv * C + ch * 8) = v;
 }
 }  // namespace
 
-extern "C" int gp_dilated_sparsify(const uint16_t* src, int64_t src_row_stride, int64_t k_col, int64_t v_col,
-                                   int64_t tok_lo, int64_t n_tok, int64_t L, int H, int D, const int32_t* seg_len,
-                                   const int32_t* ratios, int nbranch, uint16_t* const* dst,
-                                   const int64_t* dst_tok_base, void* stream) {
+extern "C" int gp_dilated_sparsify_dests(const uint16_t* src, int64_t src_row_stride, int64_t k_col, int64_t v_col,
+                                         int64_t tok_lo, int64_t n_tok, int64_t L, int H, int D,
+                                         const int32_t* seg_len, const int32_t* ratios, int nbranch,
+                                         const GpRowDest* dests, const int32_t* ndest, void* stream) {
   GP_REQUIRE(nbranch >= 1 && nbranch <= GP_MAX_BRANCHES, "gp_dilated_sparsify: nbranch must be 1..%d", GP_MAX_BRANCHES);
   GP_REQUIRE(L > 0 && H > 0 && D > 0 && D % 8 == 0 && tok_lo >= 0 && n_tok >= 0 && tok_lo + n_tok <= L,
              "gp_dilated_sparsify: bad sizes");
   GP_REQUIRE(src_row_stride % 8 == 0 && k_col % 8 == 0 && v_col % 8 == 0, "gp_dilated_sparsify: strides must be multiples of 8");
   if (n_tok == 0) return 0;
-  GP_REQUIRE(src && seg_len && ratios && dst && gp_aligned(src, 16), "gp_dilated_sparsify: null or misaligned pointer");
+  GP_REQUIRE(src && seg_len && ratios && dests && ndest && gp_aligned(src, 16), "gp_dilated_sparsify: null or misaligned pointer");
   SparsifyArgs a;
   a.src = src; a.src_stride = src_row_stride; a.k_col = k_col; a.v_col = v_col;
   a.tok_lo = tok_lo; a.ntok = n_tok; a.L = L; a.nbranch = nbranch;
   int cb = 0;
+  for (int b = 0; b < GP_MAX_BRANCHES; ++b) {
+    a.ndest[b] = 0;
+    for (int d = 0; d < GP_MAX_DESTS; ++d) { a.lo[b][d] = 0; a.hi[b][d] = 0; a.dst[b][d] = nullptr; }
+  }
   for (int b = 0; b < nbranch; ++b) {
     GP_REQUIRE(seg_len[b] > 0 && ratios[b] > 0 && H % ratios[b] == 0, "gp_dilated_sparsify: branch %d needs H %% r == 0", b);
-    GP_REQUIRE(dst[b] && gp_aligned(dst[b], 16), "gp_dilated_sparsify: branch %d dst null/misaligned", b);
+    GP_REQUIRE(ndest[b] >= 0 && ndest[b] <= GP_MAX_DESTS, "gp_dilated_sparsify: branch %d has %d destinations (max %d)",
+               b, ndest[b], GP_MAX_DESTS);
     a.s[b] = (int32_t)(seg_len[b] < L ? seg_len[b] : L);
     a.r[b] = ratios[b];
     a.C[b] = (H / ratios[b]) * D;
-    a.dst[b] = dst[b];
-    a.dst_base[b] = dst_tok_base ? dst_tok_base[b] : 0;
-    GP_REQUIRE(a.dst_base[b] <= tok_lo, "gp_dilated_sparsify: branch %d dst_tok_base beyond tok_lo", b);
+    a.ndest[b] = ndest[b];
+    for (int d = 0; d < ndest[b]; ++d) {
+      const GpRowDest& e = dests[b * GP_MAX_DESTS + d];
+      GP_REQUIRE(e.tok_lo <= e.tok_hi && (e.tok_lo == e.tok_hi || (e.dst && gp_aligned(e.dst, 16))),
+                 "gp_dilated_sparsify: branch %d destination %d null/misaligned or empty range", b, d);
+      a.lo[b][d] = e.tok_lo;
+      a.hi[b][d] = e.tok_hi;
+      a.dst[b][d] = e.dst;
+    }
     a.cbeg[b] = cb;
     cb += 2 * a.C[b] / 8;
   }
-  for (int b = nbranch; b < GP_MAX_BRANCHES; ++b) {
-    a.s[b] = 1; a.r[b] = 1; a.C[b] = 8; a.dst[b] = nullptr; a.dst_base[b] = 0; a.cbeg[b] = cb;
-  }
+  for (int b = nbranch; b < GP_MAX_BRANCHES; ++b) { a.s[b] = 1; a.r[b] = 1; a.C[b] = 8; a.cbeg[b] = cb; }
   a.cbeg[GP_MAX_BRANCHES] = cb;
   a.per_tok = cb;
   const int64_t work = n_tok * cb;
   GP_REQUIRE(work / 256 < (int64_t)0x7fffffff, "gp_dilated_sparsify: too much work");
   dilated_sparsify_kernel<<<(unsigned)((work + 255) / 256), 256, 0, gp_stream(stream)>>>(a);
   return gp_check_launch("gp_dilated_sparsify");
+}
+
+extern "C" int gp_dilated_sparsify(const uint16_t* src, int64_t src_row_stride, int64_t k_col, int64_t v_col,
+                                   int64_t tok_lo, int64_t n_tok, int64_t L, int H, int D, const int32_t* seg_len,
+                                   const int32_t* ratios, int nbranch, uint16_t* const* dst,
+                                   const int64_t* dst_tok_base, void* stream) {
+  GP_REQUIRE(nbranch >= 1 && nbranch <= GP_MAX_BRANCHES, "gp_dilated_sparsify: nbranch must be 1..%d", GP_MAX_BRANCHES);
+  GP_REQUIRE(dst && seg_len && ratios, "gp_dilated_sparsify: null pointer");
+  GpRowDest dests[GP_MAX_BRANCHES * GP_MAX_DESTS];
+  int32_t nd[GP_MAX_BRANCHES];
+  for (int b = 0; b < nbranch; ++b) {
+    GP_REQUIRE(ratios[b] > 0 && H > 0 && H % ratios[b] == 0, "gp_dilated_sparsify: branch %d needs H %% r == 0", b);
+    const int64_t base = dst_tok_base ? dst_tok_base[b] : 0;
+    GP_REQUIRE(base <= tok_lo, "gp_dilated_sparsify: branch %d dst_tok_base beyond tok_lo", b);
+    const int64_t C = (int64_t)(H / ratios[b]) * D;
+    dests[b * GP_MAX_DESTS].tok_lo = tok_lo;
+    dests[b * GP_MAX_DESTS].tok_hi = tok_lo + n_tok;
+    dests[b * GP_MAX_DESTS].dst = dst[b] ? dst[b] + (tok_lo - base) * 2 * C : nullptr;
+    nd[b] = 1;
+  }
+  return gp_dilated_sparsify_dests(src, src_row_stride, k_col, v_col, tok_lo, n_tok, L, H, D, seg_len, ratios,
+                                   nbranch, dests, nd, stream);
 }

@@ -17,8 +17,14 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GIGAPATH_HIP_LIB", os.path.join(_HERE, "_lib", "libgigapath_hip.so"))
 ABI_VERSION = 2
 MAX_BRANCHES = 8
+MAX_DESTS = 8
 
 c_i32, c_i64, c_f32, c_f64, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_double, ctypes.c_void_p
+
+
+class GpRowDest(ctypes.Structure):
+    """struct GpRowDest (include/gigapath_hip.h)."""
+    _fields_ = [("tok_lo", c_i64), ("tok_hi", c_i64), ("dst", c_vp)]
 
 
 class GpAttnBranch(ctypes.Structure):
@@ -39,6 +45,8 @@ SIGNATURES = {
                                c_i32, c_vp],
     "gp_dilated_sparsify": [c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp,
                             c_vp, c_vp],
+    "gp_dilated_sparsify_dests": [c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_i32,
+                                  c_vp, c_vp, c_vp],
     "gp_branch_merge_ln_window": [c_vp, c_vp, c_vp, c_vp, c_i32, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp,
                                   c_f32, c_vp, c_vp],
     "gp_seg_attn_fwd": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i32, c_f32, c_vp, c_vp, c_vp],
@@ -186,6 +194,28 @@ def dilated_sparsify(src, src_row_stride, k_col, v_col, tok_lo, n_tok, L, H, D, 
     _check(lib.gp_dilated_sparsify(_ptr(src), src_row_stride, k_col, v_col, tok_lo, n_tok, L, H, D, _i32_array(segs),
                                    _i32_array(ratios), len(segs), _ptr_array(dsts), bases, _stream()),
            "gp_dilated_sparsify")
+
+
+def dilated_sparsify_dests(src, src_row_stride, k_col, v_col, tok_lo, n_tok, L, H, D, segs, ratios, dests):
+    """dests[b] = list of (tok_lo, tok_hi, tensor, row_offset): token p of branch b is written to
+    row row_offset + (p - tok_lo) of that [rows, 2C] bf16 tensor."""
+    lib = load_library()
+    _dev(src, torch.bfloat16, "src")
+    arr = (GpRowDest * (MAX_DESTS * len(segs)))()
+    nd = (ctypes.c_int32 * len(segs))()
+    for b, lst in enumerate(dests):
+        if len(lst) > MAX_DESTS:
+            raise ValueError("at most %d destinations per branch" % MAX_DESTS)
+        nd[b] = len(lst)
+        for d, (lo, hi, t, off) in enumerate(lst):
+            _dev(t, torch.bfloat16, "dst")
+            if off < 0 or off + (hi - lo) > t.shape[0]:
+                raise ValueError("sparsify destination rows [%d, %d) outside a %d-row buffer" % (off, off + hi - lo,
+                                                                                               t.shape[0]))
+            arr[b * MAX_DESTS + d] = GpRowDest(int(lo), int(hi), t.data_ptr() + int(off) * t.stride(0) * 2)
+    _check(lib.gp_dilated_sparsify_dests(_ptr(src), src_row_stride, k_col, v_col, tok_lo, n_tok, L, H, D,
+                                         _i32_array(segs), _i32_array(ratios), len(segs), ctypes.cast(arr, c_vp),
+                                         nd, _stream()), "gp_dilated_sparsify_dests")
 
 
 def branch_merge_ln_window(outs, lses, segs, ratios, B, L, tok_lo, n_tok, H, D, ln_w, ln_b, eps, out):

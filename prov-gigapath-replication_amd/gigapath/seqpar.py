@@ -8,21 +8,23 @@ replacement for arbitrary shard boundaries:
 * **Shards.**  Tokens [0, L) are split into W contiguous ranges [a_w, b_w) (CLS on rank 0),
   balanced by a per-token cost model (valid attention FLOPs + per-token GEMM/row-kernel work).
   Everything per token (LN, projections, merge, FFN, residuals) runs on the owner only.
-* **Exchange (one step per layer).**  After the QKV projection, every rank writes token-major
-  sparsified K/V rows of its own tokens for every branch (``gp_dilated_sparsify``: token p keeps
-  the C = (H/r)·D columns of its head group j = (p mod s) mod r, i.e. 1/r of the row).  Rank v
-  needs, for branch b, the gather range of every segment its queries meet:
-  [n_lo·s, min((n_hi+1)·s, L)) with n_lo, n_hi the dense-slot segments of [a_v, b_v).  Each
-  owner sends the intersection of that range with its own tokens directly to v -- one
-  ``batch_isend_irecv`` group of point-to-point RCCL transfers per layer (xGMI is point to point:
-  every rank uses all its links at once, no ring).  When s is not a multiple of r
-  (g = m·r > s), a segment's dense slots sit g - s tokens right of its gather tokens, so the
-  first queries of a shard can need q rows of the left neighbour: a small "q halo" of whole
-  qkv rows rides in the same group.
+* **Exchange (one step per layer).**  Rank v needs, for branch b, the gather range of every
+  segment its queries meet: [n_lo·s, min((n_hi+1)·s, L)) with n_lo, n_hi the dense-slot segments
+  of [a_v, b_v).  After the QKV projection ONE kernel (``gp_dilated_sparsify_dests``) writes the
+  token-major sparsified K/V rows of the rank's own tokens (token p keeps the C = (H/r)·D columns
+  of its head group j = (p mod s) mod r, i.e. 1/r of the row) straight into a per-branch send
+  buffer packed by destination rank (including itself).  One uneven ``all_to_all_single`` per
+  branch over RCCL then delivers, because shards are contiguous and ordered by rank, exactly the
+  token range [need_lo, need_hi) in token order -- the receive buffer IS the attention kernel's
+  K/V buffer (no unpack).  RCCL runs the all-to-all as concurrent point-to-point transfers, one
+  per xGMI link (no ring).  When s is not a multiple of r (g = m·r > s), a segment's dense slots
+  sit g - s tokens right of its gather tokens, so the first queries of a shard can need q rows
+  of the left neighbour: a small "q halo" of whole qkv rows goes by point-to-point.
 * **Compute.**  ``gp_dilated_attn_fwd_ex`` computes exactly the sparse rows whose dense slot lies
   in [a_v, b_v) (query window), reading q from the local (halo-extended) qkv buffer and K/V from
-  the sparsified buffers.  Branches that need nothing remote are launched before the exchange
-  is waited on (overlap); the rest after.  ``gp_branch_merge_ln_window`` merges the window.
+  the received buffers.  The short-segment branches (segments shorter than a shard: halo-only
+  exchange) are exchanged first and their attention runs while the long-segment branches'
+  all-to-alls are still in flight (overlap).  ``gp_branch_merge_ln_window`` merges the window.
 
 Per-query math is identical to the single-device kernel, so SP output equals the 1-GPU
 output up to the GEMMs' row-count-dependent kernel choice.  Inference only, B = 1.
@@ -102,8 +104,12 @@ def _isect(a: Tuple[int, int], b: Tuple[int, int]) -> Tuple[int, int]:
 class ShardPlan:
     """All integer bookkeeping of one sharded forward (pure host logic, identical on every rank)."""
 
+    MAX_RANKS = 8          # GP_MAX_DESTS: one send chunk per rank (one node)
+
     def __init__(self, L: int, world: int, segs: Sequence[int], ratios: Sequence[int], H: int, D: int, F: int,
                  bounds: Optional[List[Tuple[int, int]]] = None):
+        if world > self.MAX_RANKS:
+            raise ValueError("sequence parallel over at most %d ranks (one node)" % self.MAX_RANKS)
         self.L, self.world, self.H, self.D, self.E = L, world, H, D, H * D
         self.segs, self.ratios = list(segs), list(ratios)
         for r in self.ratios:
@@ -114,13 +120,13 @@ class ShardPlan:
         self.bounds = bounds or balanced_bounds(token_cost(L, segs, ratios, H, D, F), world)
         assert self.bounds[0][0] == 0 and self.bounds[-1][1] == L
         nb = len(self.geo)
-        # K/V gather range each rank's queries need, per branch
+        # K/V gather range each rank's queries need, per branch (= its receive buffer)
         self.need = [[self._kv_need(w, b) for b in range(nb)] for w in range(world)]
-        # rows each rank's sparsified buffer of branch b holds: its needs and its own tokens
-        self.buf = [[(min(self.need[w][b][0], self.bounds[w][0]), max(self.need[w][b][1], self.bounds[w][1]))
-                     for b in range(nb)] for w in range(world)]
         self.q_halo = [max(0, max(self._q_halo(w, b) for b in range(nb))) for w in range(world)]
-        self.branch_halo = [[self._q_halo(w, b) > 0 for b in range(nb)] for w in range(world)]
+        # exchange phases: short segments (halo-only traffic) first, then the long ones
+        shard = L / world
+        self.phase_a = [b for b in range(nb) if self.geo[b].s < shard]
+        self.phase_b = [b for b in range(nb) if b not in self.phase_a]
 
     # ---- geometry of one rank
     def _kv_need(self, w: int, b: int) -> Tuple[int, int]:
@@ -139,29 +145,25 @@ class ShardPlan:
             lowest = min(lowest, (n_lo + 1) * g.s)
         return max(0, a - lowest)
 
+    def chunk(self, src: int, dst: int, b: int) -> Tuple[int, int]:
+        """Tokens of branch b that rank src sends to rank dst (possibly empty, (0, 0))."""
+        return _isect(self.need[dst][b], self.bounds[src])
+
+    def send_splits(self, w: int, b: int) -> List[int]:
+        return [hi - lo for lo, hi in (self.chunk(w, v, b) for v in range(self.world))]
+
+    def recv_splits(self, v: int, b: int) -> List[int]:
+        return [hi - lo for lo, hi in (self.chunk(w, v, b) for w in range(self.world))]
+
     def recvs(self, v: int) -> List[Tuple[int, int, int, int]]:
-        """(branch, src, lo, hi) token ranges rank v receives (canonical order: branch, src)."""
-        out = []
-        for b in range(len(self.geo)):
-            for w in range(self.world):
-                if w == v:
-                    continue
-                lo, hi = _isect(self.need[v][b], self.bounds[w])
-                if hi > lo:
-                    out.append((b, w, lo, hi))
-        return out
+        """(branch, src, lo, hi) token ranges rank v receives from other ranks."""
+        return [(b, w, lo, hi) for b in range(len(self.geo)) for w in range(self.world) if w != v
+                for lo, hi in [self.chunk(w, v, b)] if hi > lo]
 
     def sends(self, w: int) -> List[Tuple[int, int, int, int]]:
-        """(branch, dst, lo, hi) token ranges rank w sends, in the order receivers post them."""
-        out = []
-        for b in range(len(self.geo)):
-            for v in range(self.world):
-                if v == w:
-                    continue
-                lo, hi = _isect(self.need[v][b], self.bounds[w])
-                if hi > lo:
-                    out.append((b, v, lo, hi))
-        return out
+        """(branch, dst, lo, hi) token ranges rank w sends to other ranks."""
+        return [(b, v, lo, hi) for b in range(len(self.geo)) for v in range(self.world) if v != w
+                for lo, hi in [self.chunk(w, v, b)] if hi > lo]
 
     def halo_recvs(self, v: int) -> List[Tuple[int, int, int]]:
         a = self.bounds[v][0]
@@ -180,13 +182,8 @@ class ShardPlan:
                 out.append((v, lo, hi))
         return out
 
-    def local_branches(self, v: int) -> List[int]:
-        """Branches rank v can compute before its exchange completes."""
-        remote = {b for b, _, _, _ in self.recvs(v)}
-        return [b for b in range(len(self.geo)) if b not in remote and not self.branch_halo[v][b]]
-
     def exchange_bytes(self, v: int) -> int:
-        """bf16 bytes rank v receives per layer."""
+        """bf16 bytes rank v receives from other ranks per layer."""
         tot = sum((hi - lo) * 2 * self.C[b] * 2 for b, _, lo, hi in self.recvs(v))
         tot += sum((hi - lo) * 3 * self.E * 2 for _, lo, hi in self.halo_recvs(v))
         return tot
@@ -195,10 +192,10 @@ class ShardPlan:
 # ------------------------------------------------------------------------------------------
 # exchange transport
 # ------------------------------------------------------------------------------------------
-class P2PExchange:
-    """One group of point-to-point transfers.  RCCL ("nccl" backend): device tensors, the group is
-    enqueued behind the current stream and `wait()` makes the current stream wait on it (no host
-    sync).  gloo (CPU tests, one-GPU rehearsals): staged through host memory, synchronous."""
+class Exchange:
+    """Collectives of the sharded forward.  RCCL ("nccl" backend): device tensors, async; a
+    handle's `wait()` makes the current stream wait on the transfer (no host sync).  gloo (CPU
+    tests, one-GPU rehearsals): staged through host memory, synchronous."""
 
     def __init__(self, group=None):
         import torch.distributed as dist
@@ -210,21 +207,32 @@ class P2PExchange:
     def peer(self, r: int) -> int:
         return r if self.group is None else self.dist.get_global_rank(self.group, r)
 
-    def run(self, sends: List[Tuple[int, torch.Tensor]], recvs: List[Tuple[int, torch.Tensor]]):
-        """Post all transfers; returns a handle for wait()."""
+    def all_to_all(self, out: torch.Tensor, inp: torch.Tensor, out_splits: List[int], in_splits: List[int]):
+        """Uneven all-to-all along dim 0 (rows)."""
+        dist = self.dist
+        if self.device_comm or not out.is_cuda:
+            wk = dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group,
+                                        async_op=self.device_comm)
+            return [wk] if self.device_comm else None
+        h_out = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(h_out, inp.detach().to("cpu", copy=True), out_splits, in_splits, group=self.group)
+        out.copy_(h_out)
+        return None
+
+    def p2p(self, sends: List[Tuple[int, torch.Tensor]], recvs: List[Tuple[int, torch.Tensor]]):
+        """Point-to-point group (the q halo)."""
         dist = self.dist
         if not sends and not recvs:
             return None
         if self.device_comm:
             ops = [dist.P2POp(dist.isend, t, self.peer(p), self.group) for p, t in sends]
             ops += [dist.P2POp(dist.irecv, t, self.peer(p), self.group) for p, t in recvs]
-            return ("dev", dist.batch_isend_irecv(ops))
+            return dist.batch_isend_irecv(ops)
         hs = [(p, t.detach().to("cpu", copy=True)) for p, t in sends]
         hr = [(p, torch.empty(t.shape, dtype=t.dtype)) for p, t in recvs]
         ops = [dist.P2POp(dist.isend, t, self.peer(p), self.group) for p, t in hs]
         ops += [dist.P2POp(dist.irecv, t, self.peer(p), self.group) for p, t in hr]
-        works = dist.batch_isend_irecv(ops)
-        for wk in works:
+        for wk in dist.batch_isend_irecv(ops):
             wk.wait()
         for (_, dst), (_, src) in zip(recvs, hr):
             dst.copy_(src)
@@ -252,10 +260,8 @@ class P2PExchange:
         return t
 
     @staticmethod
-    def wait(handle):
-        if handle is None:
-            return
-        for wk in handle[1]:
+    def wait(handles):
+        for wk in handles or ():
             wk.wait()
 
 
@@ -275,11 +281,15 @@ class ShardWorkspace:
         self.qkv = self.qkv_ext[self.hq:]
         self.y = torch.empty(self.n, E, dtype=torch.bfloat16, device=dev)
         self.f = torch.empty(self.n, F, dtype=torch.bfloat16, device=dev)
-        self.kvs, self.kv_base = [], []
+        # per branch: K/V receive buffer = the need range in token order; send buffer packed by peer
+        self.kvs, self.kv_base, self.send, self.send_off = [], [], [], []
         for b in range(len(plan.geo)):
-            lo, hi = plan.buf[rank][b]
+            lo, hi = plan.need[rank][b]
             self.kvs.append(torch.empty(hi - lo, 2 * plan.C[b], dtype=torch.bfloat16, device=dev))
             self.kv_base.append(lo)
+            splits = plan.send_splits(rank, b)
+            self.send.append(torch.empty(sum(splits), 2 * plan.C[b], dtype=torch.bfloat16, device=dev))
+            self.send_off.append(list(np.cumsum([0] + splits[:-1])))
         # branch outputs keep the single-device layout; only the window's rows are written/read
         self.attn = runtime.AttentionScratch(dev, 1, plan.L, H, D, plan.segs, plan.ratios)
 
@@ -287,26 +297,41 @@ class ShardWorkspace:
 class SeqParallelEngine:
     """Runs the encoder layers of one rank's shard.  `layers` are runtime.PackedLayer."""
 
-    def __init__(self, plan: ShardPlan, rank: int, exchange: P2PExchange):
+    def __init__(self, plan: ShardPlan, rank: int, exchange: Exchange):
         self.plan, self.rank, self.xch = plan, rank, exchange
-        self._sends = plan.sends(rank)
-        self._recvs = plan.recvs(rank)
         self._hsends = plan.halo_sends(rank)
         self._hrecvs = plan.halo_recvs(rank)
-        self._local = plan.local_branches(rank)
-        self._remote = [b for b in range(len(plan.geo)) if b not in self._local]
+        self._ssplit = [plan.send_splits(rank, b) for b in range(len(plan.geo))]
+        self._rsplit = [plan.recv_splits(rank, b) for b in range(len(plan.geo))]
 
-    def _kv_view(self, ws: ShardWorkspace, b: int, lo: int, hi: int) -> torch.Tensor:
-        base = ws.kv_base[b]
-        return ws.kvs[b][lo - base:hi - base]
+    def sparsify(self, ws: ShardWorkspace):
+        """This rank's sparsified K/V rows, written into every peer's chunk of the send buffers."""
+        plan = self.plan
+        a, e = plan.bounds[self.rank]
+        E = plan.E
+        dests = []
+        for b in range(len(plan.geo)):
+            lst = []
+            for v in range(plan.world):
+                lo, hi = plan.chunk(self.rank, v, b)
+                if hi > lo:
+                    lst.append((lo, hi, ws.send[b], int(ws.send_off[b][v])))
+            dests.append(lst)
+        with runtime.TIMER.span("sparsify"):
+            _hip.dilated_sparsify_dests(ws.qkv, 3 * E, E, 2 * E, a, e - a, plan.L, plan.H, plan.D, plan.segs,
+                                        plan.ratios, dests)
 
-    def exchange(self, ws: ShardWorkspace):
-        a = self.plan.bounds[self.rank][0]
-        sends = [(dst, self._kv_view(ws, b, lo, hi)) for b, dst, lo, hi in self._sends]
-        recvs = [(src, self._kv_view(ws, b, lo, hi)) for b, src, lo, hi in self._recvs]
-        sends += [(dst, ws.qkv[lo - a:hi - a]) for dst, lo, hi in self._hsends]
-        recvs += [(src, ws.qkv_ext[lo - (a - ws.hq):hi - (a - ws.hq)]) for src, lo, hi in self._hrecvs]
-        return self.xch.run(sends, recvs)
+    def exchange(self, ws: ShardWorkspace, branches: List[int], halo: bool):
+        plan = self.plan
+        handles = []
+        if halo and (self._hsends or self._hrecvs):
+            a = plan.bounds[self.rank][0]
+            sends = [(dst, ws.qkv[lo - a:hi - a]) for dst, lo, hi in self._hsends]
+            recvs = [(src, ws.qkv_ext[lo - (a - ws.hq):hi - (a - ws.hq)]) for src, lo, hi in self._hrecvs]
+            handles += self.xch.p2p(sends, recvs) or []
+        for b in branches:
+            handles += self.xch.all_to_all(ws.kvs[b], ws.send[b], self._rsplit[b], self._ssplit[b]) or []
+        return handles
 
     def attention(self, pa: runtime.PackedAttention, ws: ShardWorkspace, branches: List[int]):
         if not branches:
@@ -335,13 +360,13 @@ class SeqParallelEngine:
             pa = pl.attn
             with runtime.TIMER.span("gemm_qkv"):
                 torch.addmm(pa.b_qkv, ws.a, pa.w_qkv.t(), out=ws.qkv)
-            with runtime.TIMER.span("sparsify"):
-                _hip.dilated_sparsify(ws.qkv, 3 * E, E, 2 * E, a, M, plan.L, H, D, plan.segs, plan.ratios, ws.kvs,
-                                      ws.kv_base)
-            handle = self.exchange(ws)
-            self.attention(pa, ws, self._local)
-            P2PExchange.wait(handle)
-            self.attention(pa, ws, self._remote)
+            self.sparsify(ws)
+            h_a = self.exchange(ws, plan.phase_a, halo=True)
+            h_b = self.exchange(ws, plan.phase_b, halo=False)
+            Exchange.wait(h_a)
+            self.attention(pa, ws, plan.phase_a)
+            Exchange.wait(h_b)
+            self.attention(pa, ws, plan.phase_b)
             with runtime.TIMER.span("merge"):
                 _hip.branch_merge_ln_window(ws.attn.outs, ws.attn.lses, plan.segs, plan.ratios, 1, plan.L, a, M, H, D,
                                             pa.ln_w, pa.ln_b, pa.ln_eps, ws.a)
@@ -373,7 +398,7 @@ class SeqParallelContext:
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
-        self.exchange = P2PExchange(group)
+        self.exchange = Exchange(group)
         self._key = None
         self.plan: Optional[ShardPlan] = None
         self.ws: Optional[ShardWorkspace] = None

@@ -84,6 +84,23 @@ def dilated_sparsify(src, src_row_stride, k_col, v_col, tok_lo, n_tok, L, H, D, 
         dsts[b][rows, C:] = torch.gather(src[:n_tok, v_col:v_col + H * D], 1, cols)
 
 
+def dilated_sparsify_dests(src, src_row_stride, k_col, v_col, tok_lo, n_tok, L, H, D, segs, ratios, dests):
+    assert src.shape[0] >= n_tok and src.shape[1] == src_row_stride
+    p = torch.arange(tok_lo, tok_lo + n_tok)
+    for b, (sl, r) in enumerate(zip(segs, ratios)):
+        s, C = min(sl, L), (H // r) * D
+        j = (p % s) % r
+        cols = j[:, None] * C + torch.arange(C)[None, :]
+        krow = torch.gather(src[:n_tok, k_col:k_col + H * D], 1, cols)
+        vrow = torch.gather(src[:n_tok, v_col:v_col + H * D], 1, cols)
+        for lo, hi, t, off in dests[b]:
+            sel = (p >= lo) & (p < hi)
+            rows = off + (p[sel] - lo)
+            assert t.shape[1] == 2 * C and (len(rows) == 0 or (rows.min() >= 0 and rows.max() < t.shape[0]))
+            t[rows, :C] = krow[sel].to(t.dtype)
+            t[rows, C:] = vrow[sel].to(t.dtype)
+
+
 def attn_branch(sl, r, k, v, kv_row_stride, kv_tok_base, kv_sparse_cols, o, lse):
     return dict(sl=sl, r=r, k=k, v=v, stride=kv_row_stride, base=kv_tok_base, sparse=kv_sparse_cols, o=o, lse=lse)
 
@@ -176,7 +193,7 @@ def install():
     """Replace the _hip entry points in this process (call in a test subprocess only)."""
     from gigapath import _hip
     for name in ("coords_to_pos", "posembed_cls_ln", "layernorm_f32", "mean_tokens", "residual_layernorm",
-                 "gelu_layernorm", "dilated_sparsify", "attn_branch", "dilated_attn_fwd_ex",
+                 "gelu_layernorm", "dilated_sparsify", "dilated_sparsify_dests", "attn_branch", "dilated_attn_fwd_ex",
                  "branch_merge_ln_window"):
         setattr(_hip, name, globals()[name])
     _written.clear()

@@ -62,24 +62,27 @@ def test_plan_covers_every_row_the_merge_reads(L, world, sched):
             valid = (i * r + j < s) & (gather_tok < L)
             # its query is local or in the q halo
             assert (gather_tok[valid] >= a - plan.q_halo[v]).all() and (gather_tok[valid] < e).all()
-            # all keys of its segment are in the rank's K/V range and buffer
+            # all keys of its segment are in the rank's K/V (receive) range
             lo, hi = plan.need[v][b]
             seg_lo, seg_hi = n * s, np.minimum((n + 1) * s, L)
             assert lo <= seg_lo.min() and hi >= seg_hi.max()
-            blo, bhi = plan.buf[v][b]
-            assert blo <= min(lo, a) and bhi >= max(hi, e)
-        # every received range is owned by its sender and lands inside the buffer
+            # the all-to-all chunks from ranks 0..W-1, in rank order, tile [lo, hi) exactly
+            chunks = [plan.chunk(w, v, b) for w in range(world)]
+            got = [c for c in chunks if c[1] > c[0]]
+            assert got[0][0] == lo and got[-1][1] == hi
+            assert all(x[1] == y[0] for x, y in zip(got[:-1], got[1:]))
+            assert sum(plan.recv_splits(v, b)) == hi - lo
+        # every received range is owned by its sender
         for b, w, lo, hi in plan.recvs(v):
             wa, we = plan.bounds[w]
-            assert wa <= lo < hi <= we and plan.buf[v][b][0] <= lo and hi <= plan.buf[v][b][1]
-    # sends and receives match pairwise, in the same order
+            assert wa <= lo < hi <= we
+    # send and receive split tables agree pairwise
     for w in range(world):
         for v in range(world):
+            for b in range(len(segs)):
+                assert plan.send_splits(w, b)[v] == plan.recv_splits(v, b)[w]
             if v == w:
                 continue
-            s_wv = [(b, lo, hi) for b, dst, lo, hi in plan.sends(w) if dst == v]
-            r_vw = [(b, lo, hi) for b, src, lo, hi in plan.recvs(v) if src == w]
-            assert s_wv == r_vw
             hs = [(lo, hi) for dst, lo, hi in plan.halo_sends(w) if dst == v]
             hr = [(lo, hi) for src, lo, hi in plan.halo_recvs(v) if src == w]
             assert hs == hr
@@ -130,11 +133,13 @@ def _exchange_worker(rank, world, port, L, segs, ratios, q):
             t.fill_(float("nan"))
         ws.qkv_ext.fill_(float("nan"))
         ws.qkv.copy_(torch.from_numpy(qkv[a:e]).to(ws.qkv.dtype))
-        for b in range(len(segs)):                       # this rank's own sparsified rows
-            lo = ws.kv_base[b]
-            ws.kvs[b][a - lo:e - lo] = torch.from_numpy(ref[b][a:e]).to(ws.kvs[b].dtype)
-        eng = seqpar.SeqParallelEngine(plan, rank, seqpar.P2PExchange())
-        seqpar.P2PExchange.wait(eng.exchange(ws))
+        for b in range(len(segs)):                       # this rank's sparsified rows, packed per peer
+            for v in range(world):
+                lo, hi = plan.chunk(rank, v, b)
+                off = ws.send_off[b][v]
+                ws.send[b][off:off + hi - lo] = torch.from_numpy(ref[b][lo:hi]).to(ws.send[b].dtype)
+        eng = seqpar.SeqParallelEngine(plan, rank, seqpar.Exchange())
+        seqpar.Exchange.wait(eng.exchange(ws, list(range(len(segs))), halo=True))
         for b in range(len(segs)):
             lo, hi = plan.need[rank][b]
             base = ws.kv_base[b]
