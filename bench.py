@@ -9,7 +9,10 @@ Multi-GPU (one process per GPU), --mode:
   sp       (default for N > 1) the SAME slide is sharded across the N ranks by sequence
            parallelism (seqpar.py: per-layer sparse K/V exchange over RCCL point-to-point);
            value = slide tiles / max-over-ranks wall time ("strong" scaling, C4's design);
-  replica  every rank encodes its own slide, no collective: value = N x tiles / time ("weak").
+  replica  every rank encodes its own slide, no collective: value = N x tiles / time ("weak");
+  mixed    C5: a batch of 32 slides of 2k-100k tiles (log-uniform, seed 3), LPT-assigned to the
+           ranks (batch.py, data parallel, one all-reduce of the outputs at the end); value =
+           batch tiles / time ("strong").
 Rank 0 prints ONE JSON line including the attention kernel's roofline (HIP events around
 every gp_dilated_attn_fwd launch in the timed region) and a CPU baseline (the fp32 oracle on
 a bounded sample of the same workload, timed on this host).
@@ -92,13 +95,14 @@ def main():
     ap.add_argument("--tiles", type=int, default=70000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
-    ap.add_argument("--mode", choices=["sp", "replica"], default="sp")
+    ap.add_argument("--mode", choices=["sp", "replica", "mixed"], default="sp")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     sp = world > 1 and args.mode == "sp"
+    mixed = args.mode == "mixed"
     # GP_BENCH_BACKEND=gloo: rehearsal of the multi-rank path with several ranks on one GPU
     backend = os.environ.get("GP_BENCH_BACKEND", "nccl")
     if backend != "nccl":
@@ -119,12 +123,24 @@ def main():
     model.validate_positions = True
     if sp:
         model.enable_sequence_parallel()
-    x, coords = make_slide(args.tiles, seed=1 if sp else 1 + rank)
-    xt = torch.from_numpy(x).to(dev)
-    ct = torch.from_numpy(coords).to(dev)
+    if mixed:
+        from gigapath import batch
+        sizes = batch.mixed_batch_sizes()
+        slides = []
+        for i, n in enumerate(sizes):
+            x, coords = make_slide(n, seed=100 + 2 * i)
+            slides.append((torch.from_numpy(x[0]).to(dev), torch.from_numpy(coords[0]).to(dev)))
+        args.tiles = sum(sizes)
 
-    def step():
-        return model(xt, ct, all_layer_embed=True)
+        def step():
+            return batch.encode_slides(model, slides, all_layer_embed=True)[0]
+    else:
+        x, coords = make_slide(args.tiles, seed=1 if sp else 1 + rank)
+        xt = torch.from_numpy(x).to(dev)
+        ct = torch.from_numpy(coords).to(dev)
+
+        def step():
+            return model(xt, ct, all_layer_embed=True)
 
     with torch.no_grad():
         for _ in range(args.warmup):
@@ -154,6 +170,11 @@ def main():
     ratios = model.encoder.layers[0].self_attn.args.dilated_ratio
     L = args.tiles + 1
     att_flops_launch = runtime.attention_valid_flops(L, segs, ratios, 16, 48)
+    if mixed:
+        # average launch = (all slides' attention FLOPs this rank ran) / (its launches)
+        from gigapath import batch as _b
+        mine = _b.lpt_assign([_b.slide_cost(n, segs, ratios) for n in sizes], world)[rank]
+        att_flops_launch = sum(runtime.attention_valid_flops(sizes[i] + 1, segs, ratios, 16, 48) for i in mine) / len(mine)
     n_att, ms_att = kt.get("attn", (0, 0.0))
     if sp:
         # this rank's attention launches cover its query window: price them with its share of the
@@ -164,25 +185,39 @@ def main():
         n_att = args.steps * len(model.encoder.layers)      # per layer: both launches together
     avg_att_s = ms_att / max(n_att, 1) / 1e3
     achieved = att_flops_launch / avg_att_s / 1e12 if avg_att_s > 0 else 0.0
-    gemm_tf = runtime.gemm_flops(1, args.tiles, 768, 3072, 1536, 12) / 1e12
-    total_tf = gemm_tf + 12 * att_flops_launch / 1e12
-    traffic = pmc_traffic(args.tiles, "dilated_attn32_kernel<48, true, 4>")
+    if mixed:   # whole batch (all ranks)
+        total_tf = sum(runtime.gemm_flops(1, n, 768, 3072, 1536, 12)
+                       + 12 * runtime.attention_valid_flops(n + 1, segs, ratios, 16, 48) for n in sizes) / 1e12
+    else:       # one slide (SP: shared by the ranks; replicas: one per rank)
+        total_tf = (runtime.gemm_flops(1, args.tiles, 768, 3072, 1536, 12)
+                    + 12 * runtime.attention_valid_flops(L, segs, ratios, 16, 48)) / 1e12
+    plain = not (sp or mixed)          # the PMC summary was collected on the plain C3 run
+    traffic = pmc_traffic(args.tiles, "dilated_attn32_kernel<48, true, 4>") if plain else None
     # HBM-bound merge kernel: algorithmic bytes per launch over its live launch time
     n_mg, ms_mg = kt.get("merge", (0, 0.0))
-    merge_bytes = runtime.merge_bytes(L, segs, ratios, 16, 48)
+    if sp:
+        merge_tok = b_w - a_w
+    elif mixed:
+        merge_tok = sum(sizes[i] + 1 for i in mine) / len(mine)
+    else:
+        merge_tok = L
+    merge_bytes = runtime.merge_bytes(L, segs, ratios, 16, 48) * merge_tok / L
     merge_gbs = merge_bytes / (ms_mg / max(n_mg, 1) / 1e3) / 1e9 if ms_mg > 0 else 0.0
-    value = (1 if sp else world) * args.tiles * args.steps / elapsed
+    value = (1 if (sp or mixed) else world) * args.tiles * args.steps / elapsed
     ms_step = elapsed / args.steps * 1e3
     result = {
         "metric": METRIC, "value": round(value, 2), "unit": "tiles/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "strong" if sp else "weak",
+        "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "strong" if (sp or mixed) else "weak",
         "vs_baseline": None, "dtype": "bf16",
         "data": "synthetic (PCG64 N(0,1) 1536-d tile embeddings, distinct grid coords; random-init weights)",
-        "config": {"workload": ("%s forward, one %d-tile slide sharded over %d GPUs (sequence parallel), "
+        "config": {"workload": ("C5: %s forward of a 32-slide mixed batch (%d tiles, 2k-100k per slide), "
+                                "LPT data parallel over %d GPUs, all_layer_embed=True" % (ARCH, args.tiles, world))
+                               if mixed else
+                               ("%s forward, one %d-tile slide sharded over %d GPUs (sequence parallel), "
                                 "all_layer_embed=True" % (ARCH, args.tiles, world)) if sp else
                                ("C3: %s forward, one %d-tile slide per GPU, all_layer_embed=True" % (ARCH, args.tiles)),
                    "tiles_per_slide": args.tiles, "slides_per_gpu": (1.0 / world) if sp else 1,
-                   "parallelism": ("sp%d" % world) if sp else ("replica x%d" % world)},
+                   "parallelism": ("dp%d-lpt" % world) if mixed else ("sp%d" % world) if sp else ("replica x%d" % world)},
         "roofline": {"bound": "mfma", "kernel": "gp_dilated_attn_fwd", "achieved": round(achieved, 2),
                      "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
                      "traffic": traffic, "flops_per_launch": att_flops_launch, "avg_launch_ms": round(avg_att_s * 1e3, 4),
@@ -190,14 +225,14 @@ def main():
         "attn_mfma_util_pct": round(100 * achieved / PEAK_BF16_TFLOPS, 2),
         "merge_roofline": {"bound": "hbm", "kernel": "gp_branch_merge_ln", "achieved": round(merge_gbs, 1),
                            "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(merge_gbs / PEAK_HBM_GBS, 4),
-                           "traffic": pmc_traffic(args.tiles, "branch_merge_kernel<12>"),
+                           "traffic": pmc_traffic(args.tiles, "branch_merge_kernel<12>") if plain else None,
                            "bytes_per_launch": merge_bytes},
-        "model_tflops": round(total_tf * args.steps * world / elapsed, 2),
+        "model_tflops": round(total_tf * args.steps * (1 if (sp or mixed) else world) / elapsed, 2),
         "kernel_ms_per_step": {k: round(v[1] / args.steps, 3) for k, v in sorted(kt.items())},
     }
     if sp:
         result["sp_exchange_mb_per_layer_rank0"] = round(model._sp.plan.exchange_bytes(0) / 1e6, 1)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not mixed:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         result["cpu_baseline"] = cpu_baseline(args.tiles, threads)
     if rank == 0:

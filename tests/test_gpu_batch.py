@@ -1,0 +1,27 @@
+"""Mixed-length batch (C5) on the GPU: every slide's output equals its own B = 1 forward."""
+import pytest
+import torch
+
+import oracle as orc
+from gigapath import batch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_mixed_batch_equals_individual_forwards():
+    from gigapath import slide_encoder
+    cfg = orc.arch_config("gigapath_slide_enc12l768d")
+    model = slide_encoder.create_model("", "gigapath_slide_enc12l768d", 1536)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in orc.make_weights(cfg, seed=0).items()}, strict=True)
+    model = model.cuda().eval()
+    slides = []
+    for i, n in enumerate([300, 2500, 1200, 5000]):
+        x, c = orc.synthetic_slide(n, seed_x=10 + i, seed_c=20 + i)
+        slides.append((torch.from_numpy(x[0]).cuda(), torch.from_numpy(c[0]).cuda()))
+    out = batch.encode_slides(model, slides, all_layer_embed=True)
+    with torch.no_grad():
+        for (x, c), got in zip(slides, out):
+            ref = model(x[None], c[None], all_layer_embed=True)
+            assert len(got) == len(ref) == 13
+            for g, r in zip(got, ref):
+                assert torch.equal(g, r)
