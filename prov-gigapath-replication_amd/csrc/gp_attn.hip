@@ -328,8 +328,12 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 GP_DEV float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
-template <int D, bool kPre, int NW>
-__global__ __launch_bounds__(NW * 64, 2) void dilated_attn32_kernel(const AttnArgs a) {
+// VAR bits (A/B variants, all numerically identical): 1 = S's first k-step takes its C operand
+// from a persistent -m_run block (no per-tile accumulator init), 2 = staging addresses computed
+// once (no per-tile 64-bit index math, no bound checks on full tiles), 4 = all K fragments read
+// before the S MFMAs.  OCC = waves per SIMD the register budget must allow.
+template <int D, bool kPre, int NW, int VAR = 0, int OCC = 2>
+__global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const AttnArgs a) {
   static_assert(D == 48 || D == 64, "v2 kernel covers D = 48 and 64");
   static_assert(NW == 4 || NW == 8, "");
   constexpr int NT = NW * 64;                // threads
@@ -391,34 +395,71 @@ __global__ __launch_bounds__(NW * 64, 2) void dilated_attn32_kernel(const AttnAr
   }
 
   uint4 stage[LPT];
-  auto load_tile = [&](int kv0) {
+  // VAR & 2: per-thread staging chunks (source of key 0, row, LDS offset) computed once
+  const uint16_t* lsrc[LPT];
+  int lrow[LPT], loff[LPT];
+  if constexpr ((VAR & 2) != 0) {
 #pragma unroll
     for (int u = 0; u < LPT; ++u) {
       const int idx = threadIdx.x + NT * u;
       const int tsel = idx / (KT * CH);
       const int rem = idx % (KT * CH);
       const int row = rem / CH, ch = rem % CH;
-      const int key = kv0 + row;
-      uint4 z = make_uint4(0, 0, 0, 0);
-      if (key < c) z = *reinterpret_cast<const uint4*>((tsel ? vbase : kbase) + (int64_t)key * kvstride + ch * 8);
-      stage[u] = z;
+      lsrc[u] = (tsel ? vbase : kbase) + (int64_t)row * kvstride + ch * 8;
+      lrow[u] = row;
+      loff[u] = tsel ? KTILE + row * VROWB + 32 * ((ch >> 1) ^ (row & 3)) + 16 * (ch & 1) : row * KROWB + ch * 16;
+    }
+  }
+  auto load_tile = [&](int kv0) {
+    if constexpr ((VAR & 2) != 0) {
+      const int64_t toff = (int64_t)kv0 * kvstride;      // wave-uniform
+      if (kv0 + KT <= c) {                                // full tile: no per-key bound checks
+#pragma unroll
+        for (int u = 0; u < LPT; ++u) stage[u] = *reinterpret_cast<const uint4*>(lsrc[u] + toff);
+      } else {
+#pragma unroll
+        for (int u = 0; u < LPT; ++u) {
+          uint4 z = make_uint4(0, 0, 0, 0);
+          if (kv0 + lrow[u] < c) z = *reinterpret_cast<const uint4*>(lsrc[u] + toff);
+          stage[u] = z;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < LPT; ++u) {
+        const int idx = threadIdx.x + NT * u;
+        const int tsel = idx / (KT * CH);
+        const int rem = idx % (KT * CH);
+        const int row = rem / CH, ch = rem % CH;
+        const int key = kv0 + row;
+        uint4 z = make_uint4(0, 0, 0, 0);
+        if (key < c) z = *reinterpret_cast<const uint4*>((tsel ? vbase : kbase) + (int64_t)key * kvstride + ch * 8);
+        stage[u] = z;
+      }
     }
   };
   auto store_tile = [&](int buf) {
 #pragma unroll
     for (int u = 0; u < LPT; ++u) {
-      const int idx = threadIdx.x + NT * u;
-      const int tsel = idx / (KT * CH);
-      const int rem = idx % (KT * CH);
-      const int row = rem / CH, ch = rem % CH;
-      const int off = tsel ? KTILE + row * VROWB + 32 * ((ch >> 1) ^ (row & 3)) + 16 * (ch & 1)
-                           : row * KROWB + ch * 16;
+      int off;
+      if constexpr ((VAR & 2) != 0) {
+        off = loff[u];
+      } else {
+        const int idx = threadIdx.x + NT * u;
+        const int tsel = idx / (KT * CH);
+        const int rem = idx % (KT * CH);
+        const int row = rem / CH, ch = rem % CH;
+        off = tsel ? KTILE + row * VROWB + 32 * ((ch >> 1) ^ (row & 3)) + 16 * (ch & 1) : row * KROWB + ch * 16;
+      }
       *reinterpret_cast<uint4*>(smem + buf * BUF + off) = stage[u];
     }
   };
 
   float m_run = -INFINITY;   // running max, log2 domain, of query l32
   float lsum = 0.f;          // row sum (VALU path, D % 32 == 0 only)
+  f32x16 minit;              // kPre: -m_run (0 before the first tile); else 0
+#pragma unroll
+  for (int r = 0; r < 16; ++r) minit[r] = 0.f;
   f32x16 oacc[2];
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt)
@@ -444,16 +485,33 @@ __global__ __launch_bounds__(NW * 64, 2) void dilated_attn32_kernel(const AttnAr
       // ---- S^T for two 32-key sub-tiles.  kPre (q pre-multiplied by scale*log2 e): the
       // accumulator starts at -m_run, so it already holds log2-domain scores minus the max.
       f32x16 sacc[2];
+      // VAR & 1: the first k-step takes its C operand from minit (= -m_run in every element, kept
+      // in its own registers, rewritten only on a rescale) instead of initialising per tile
       const float init = (kPre && sub > 0) ? -m_run : 0.f;
+      bf16x8 kf[2][KS];
+      if constexpr ((VAR & 4) != 0) {      // all K fragments first: one LDS wait, not one per MFMA
+  #pragma unroll
+        for (int u = 0; u < 2; ++u)
+  #pragma unroll
+          for (int ks = 0; ks < KS; ++ks)
+            kf[u][ks] = *reinterpret_cast<const bf16x8*>(Kb + (32 * u + l32) * KROWB + 32 * ks + 16 * h);
+      }
   #pragma unroll
       for (int u = 0; u < 2; ++u) {
         f32x16 acc;
+        if constexpr ((VAR & 1) == 0) {
   #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[r] = init;
+          for (int r = 0; r < 16; ++r) acc[r] = init;
+        }
   #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
-          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Kb + (32 * u + l32) * KROWB + 32 * ks + 16 * h);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], acc, 0, 0, 0);
+          bf16x8 kk;
+          if constexpr ((VAR & 4) != 0) kk = kf[u][ks];
+          else kk = *reinterpret_cast<const bf16x8*>(Kb + (32 * u + l32) * KROWB + 32 * ks + 16 * h);
+          if constexpr ((VAR & 1) != 0)
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kk, qf[ks], ks == 0 ? minit : acc, 0, 0, 0);
+          else
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kk, qf[ks], acc, 0, 0, 0);
         }
         sacc[u] = acc;
       }
@@ -498,6 +556,8 @@ __global__ __launch_bounds__(NW * 64, 2) void dilated_attn32_kernel(const AttnAr
           for (int u = 0; u < 2; ++u)
   #pragma unroll
             for (int r = 0; r < 16; ++r) sacc[u][r] -= delta;
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) minit[r] = -m_run;
         }
   #pragma unroll
         for (int u = 0; u < 2; ++u)
@@ -561,6 +621,286 @@ __global__ __launch_bounds__(NW * 64, 2) void dilated_attn32_kernel(const AttnAr
   float l;
   if constexpr (kOnes) {
     l = oacc[1][8];                       // d-row 48 (+4h): the ones row = sum_k P
+  } else {
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(lsum), __float_as_uint(lsum), false, false);
+    l = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+  }
+  const int npad = g.m - c;
+  float mr = m_run, so = 1.f;
+  if (npad > 0) {
+    const float mf = fmaxf(mr, 0.f);
+    so = fast_exp2(mr - mf);
+    l = l * so + (float)npad * fast_exp2(-mf);
+    mr = mf;
+  }
+  const float inv = so / l;
+  const int i = q0 + w * 32 + l32;
+  const AttnBranch& br = a.br[wi.bi];
+  if (i < rows_needed) {
+    uint16_t* orow = br.o + (((int64_t)bn * g.m + i) * a.H + hh) * (int64_t)D;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        const int d0 = 32 * mt + 8 * rg + 4 * h;
+        if (d0 < D) {
+          float vv[4] = {oacc[mt][4 * rg] * inv, oacc[mt][4 * rg + 1] * inv, oacc[mt][4 * rg + 2] * inv,
+                         oacc[mt][4 * rg + 3] * inv};
+          store_bf16<4>(orow + d0, vv);
+        }
+      }
+    if (h == 0) br.lse[((int64_t)bn * a.H + hh) * g.m + i] = (mr + __builtin_amdgcn_logf(l)) * 0.69314718055994530942f;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// v3: the v2 formulation (q pre-scaled into the log2 domain) software-pipelined across 64-key
+// tiles so every MFMA has independent VALU work beside it in the same wave:
+//   phase A: S(t+1) = K(t+1).Q^T MFMAs      | exp2/cvt of S(t), keys 0..31
+//   phase B: O += V(t)^T.P(t)^T, keys 0..31 | exp2/cvt of S(t), keys 32..63
+//   phase C: O += V(t)^T.P(t)^T, keys 32..63| row max of S(t+1), deferred-rescale decision
+// LDS holds K one tile ahead of V: iteration t reads K(t+1) and V(t) and stages K(t+2), V(t+1)
+// (both double buffered; one barrier per tile).
+template <int D>
+__global__ __launch_bounds__(256, 2) void dilated_attn_pp_kernel(const AttnArgs a) {
+  static_assert(D == 48 || D == 64, "v3 kernel covers D = 48 and 64");
+  constexpr int NT = 256;
+  constexpr int QB = 128;
+  constexpr int KT = 64;                     // keys per tile
+  constexpr int KS = D / 16;
+  constexpr bool kOnes = (D % 32) != 0;
+  constexpr int KROWB = D * 2 + 16;
+  constexpr int VROWB = 128;
+  constexpr int KTILE = KT * KROWB;
+  constexpr int VTILE = KT * VROWB;
+  constexpr int VOFF = 2 * KTILE;            // [K0 | K1 | V0 | V1]
+  constexpr int CH = D / 8;
+  constexpr int KCH = KT * CH;               // 16-byte chunks of one K (or V) tile
+  constexpr int LPT = 2 * KCH / NT;          // chunks per thread for one K tile + one V tile
+  static_assert((2 * KCH) % NT == 0, "");
+  constexpr float kThr = 8.0f;
+  __shared__ __attribute__((aligned(16))) char smem[2 * KTILE + 2 * VTILE];
+
+  WorkItem wi;
+  decode_item(a, (int)xcd_group(blockIdx.x, gridDim.x), wi);
+  const GpBranch g = a.br[wi.bi].g;
+  const int hh = wi.hh, c = wi.c, bn = wi.bn;
+  const int rows_needed = wi.i_hi;
+  const int q0 = wi.i_lo + wi.qb * QB;
+  if (q0 >= rows_needed) return;
+  const int qvalid = c < rows_needed ? c : rows_needed;
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int l32 = lane & 31, h = lane >> 5;
+  const AttnBranch& brr = a.br[wi.bi];
+  const int64_t tok0 = (int64_t)wi.bidx * a.L + (int64_t)wi.n * g.s + wi.j;
+  const int64_t qstride = (int64_t)g.r * a.q_stride;
+  const int64_t kvstride = (int64_t)g.r * brr.kv_stride;
+  const int kcol = brr.kv_sparse ? (hh % g.hpg) * D : hh * D;
+  const uint16_t* qbase = a.q + (tok0 - a.q_tok_base) * a.q_stride + hh * D;
+  const uint16_t* kbase = brr.k + (tok0 - brr.kv_tok_base) * brr.kv_stride + kcol;
+  const uint16_t* vbase = brr.v + (tok0 - brr.kv_tok_base) * brr.kv_stride + kcol;
+
+  if constexpr (kOnes) {
+    for (int idx = threadIdx.x; idx < 2 * KT * 2; idx += NT) {
+      const int buf = idx / (2 * KT), rem = idx % (2 * KT), row = rem >> 1, half = rem & 1;
+      const uint4 ones = make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
+      *reinterpret_cast<uint4*>(smem + VOFF + buf * VTILE + row * VROWB + 32 * (3 ^ (row & 3)) + 16 * half) = ones;
+    }
+  }
+
+  bf16x8 qf[KS];
+  {
+    const int i = q0 + w * 32 + l32;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      bf16x8 z = {};
+      if (i < qvalid) z = *reinterpret_cast<const bf16x8*>(qbase + (int64_t)i * qstride + 16 * ks + 8 * h);
+      qf[ks] = z;
+    }
+  }
+
+  const int ntiles = (c + KT - 1) / KT;
+  // staging: chunk idx < KCH is K of tile tk, else V of tile tv
+  uint4 stage[LPT];
+  auto load_stage = [&](int tk, int tv) {
+#pragma unroll
+    for (int u = 0; u < LPT; ++u) {
+      const int idx = threadIdx.x + NT * u;
+      const int tsel = idx / KCH;
+      const int rem = idx % KCH;
+      const int row = rem / CH, ch = rem % CH;
+      const int key = (tsel ? tv : tk) * KT + row;
+      uint4 z = make_uint4(0, 0, 0, 0);
+      if (key < c) z = *reinterpret_cast<const uint4*>((tsel ? vbase : kbase) + (int64_t)key * kvstride + ch * 8);
+      stage[u] = z;
+    }
+  };
+  auto store_stage = [&](int bk, int bv) {
+#pragma unroll
+    for (int u = 0; u < LPT; ++u) {
+      const int idx = threadIdx.x + NT * u;
+      const int tsel = idx / KCH;
+      const int rem = idx % KCH;
+      const int row = rem / CH, ch = rem % CH;
+      const int off = tsel ? VOFF + bv * VTILE + row * VROWB + 32 * ((ch >> 1) ^ (row & 3)) + 16 * (ch & 1)
+                           : bk * KTILE + row * KROWB + ch * 16;
+      *reinterpret_cast<uint4*>(smem + off) = stage[u];
+    }
+  };
+  auto compute_s = [&](int bk, const f32x16& init, f32x16 (&acc)[2]) {
+    const char* Kb = smem + bk * KTILE;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Kb + (32 * u + l32) * KROWB + 32 * ks + 16 * h);
+        acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], ks == 0 ? init : acc[u], 0, 0, 0);
+      }
+    }
+  };
+  auto mask_tail = [&](int t, f32x16 (&acc)[2]) {
+    const int kv0 = t * KT;
+    if (kv0 + KT > c) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (kv0 + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * h >= c) acc[u][r] = -INFINITY;
+    }
+  };
+  auto row_max = [&](const f32x16 (&acc)[2]) {
+    float mxa = acc[0][0], mxb = acc[1][0];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) {
+      mxa = fmaxf(mxa, acc[0][r]);
+      mxb = fmaxf(mxb, acc[1][r]);
+    }
+    float mx = fmaxf(mxa, mxb);
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+    return fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+  };
+
+  float m_run = 0.f;
+  float lsum = 0.f;
+  f32x16 oacc[2];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) oacc[mt][r] = 0.f;
+
+  f32x16 scur[2], snext[2];
+  f32x16 minit;                             // -m_run in every element (C operand of S's first k-step)
+#pragma unroll
+  for (int r = 0; r < 16; ++r) minit[r] = 0.f;
+  if (ntiles > 0) {
+    // prologue: K(0), V(0) -> LDS; S(0) with its exact max; K(1) -> LDS
+    load_stage(0, 0);
+    store_stage(0, 0);
+    __syncthreads();
+    load_stage(1, ntiles);                  // K(1); the V half loads nothing (tile past the end)
+    compute_s(0, minit, scur);
+    mask_tail(0, scur);
+    m_run = row_max(scur);
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) scur[u][r] -= m_run;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) minit[r] = -m_run;
+#pragma unroll
+    for (int u = 0; u < LPT; ++u) {         // store only the K half (the V half is tile 'ntiles')
+      const int idx = threadIdx.x + NT * u;
+      if (idx < KCH) {
+        const int row = idx / CH, ch = idx % CH;
+        *reinterpret_cast<uint4*>(smem + KTILE + row * KROWB + ch * 16) = stage[u];
+      }
+    }
+    __syncthreads();
+  }
+
+  for (int t = 0; t < ntiles; ++t) {
+    load_stage(t + 2, t + 1);
+    // phase A: S(t+1) | P(t) keys 0..31.  Branch-free: after the last tile S(t+1) reads a zeroed
+    // K buffer and is fully masked (row max -inf: no rescale), so nothing of it is used.
+    compute_s((t + 1) & 1, minit, snext);
+    bf16x8 pf[2][2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float p = fast_exp2(scur[0][8 * s2 + e]);
+        if constexpr (!kOnes) lsum += p;
+        pf[0][s2][e] = (__bf16)p;
+      }
+    const char* Vb = smem + VOFF + (t & 1) * VTILE;
+    // phase B: O += V(t)^T P(t)^T keys 0..31 | P(t) keys 32..63
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int row = 16 * s2 + 4 * (lane >> 5) + ((lane >> 2) & 3);
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const int blk = 2 * mt + ((lane >> 4) & 1);
+        const char* p0 = Vb + row * VROWB + 32 * (blk ^ (row & 3)) + 8 * (lane & 3);
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0 + 8 * VROWB));
+        const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        oacc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[0][s2], oacc[mt], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float p = fast_exp2(scur[1][8 * s2 + e]);
+        if constexpr (!kOnes) lsum += p;
+        pf[1][s2][e] = (__bf16)p;
+      }
+    // phase C: O += V(t)^T P(t)^T keys 32..63 | row max of S(t+1)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int row = 32 + 16 * s2 + 4 * (lane >> 5) + ((lane >> 2) & 3);
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const int blk = 2 * mt + ((lane >> 4) & 1);
+        const char* p0 = Vb + row * VROWB + 32 * (blk ^ (row & 3)) + 8 * (lane & 3);
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0 + 8 * VROWB));
+        const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        oacc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[1][s2], oacc[mt], 0, 0, 0);
+      }
+    }
+    {
+      mask_tail(t + 1, snext);
+      const float mx = row_max(snext);       // scores of tile t+1 minus m_run
+      const bool need = mx > kThr;
+      if (__builtin_amdgcn_ballot_w64(need)) {
+        const float delta = need ? mx : 0.f;
+        const float alpha = fast_exp2(-delta);
+        m_run += delta;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) minit[r] = -m_run;
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) snext[u][r] -= delta;
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) oacc[mt][r] *= alpha;
+        lsum *= alpha;
+      }
+    }
+    store_stage(t & 1, (t + 1) & 1);
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 2; ++u) scur[u] = snext[u];
+  }
+
+  // ---- epilogue (as v2)
+  float l;
+  if constexpr (kOnes) {
+    l = oacc[1][8];
   } else {
     const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(lsum), __float_as_uint(lsum), false, false);
     l = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
@@ -739,9 +1079,12 @@ extern "C" int gp_dilated_attn_fwd_ex(const uint16_t* q, int64_t q_row_stride, i
   a.c_log2 = q_log2_prescaled ? 1.0f : scale * 1.44269504088896340736f;
   const char* impl_env = getenv("GP_ATTN_IMPL");   // A/B switch: 1 = 16x16x32 kernel, 2 = 32x32x16 kernel
   const int impl = (D == 96) ? 1 : (impl_env ? atoi(impl_env) : 2);
-  GP_REQUIRE(impl == 1 || impl == 2, "gp_dilated_attn_fwd: GP_ATTN_IMPL must be 1 or 2");
+  GP_REQUIRE(impl == 1 || impl == 2 || impl == 3, "gp_dilated_attn_fwd: GP_ATTN_IMPL must be 1, 2 or 3");
+  GP_REQUIRE(impl != 3 || q_log2_prescaled, "gp_dilated_attn_fwd: GP_ATTN_IMPL=3 needs q_log2_prescaled");
   GP_REQUIRE(!q_log2_prescaled || impl != 1, "gp_dilated_attn_fwd: q_log2_prescaled needs D in {48, 64}");
   const int qblk = 128;                            // query rows per workgroup (both kernels)
+  const char* var_env = getenv("GP_ATTN_VAR");
+  const int var = var_env ? atoi(var_env) : 0;
   // order branches by keys per work item (descending) so the longest items start first
   int order[GP_MAX_BRANCHES];
   GpBranch geo[GP_MAX_BRANCHES];
@@ -805,8 +1148,24 @@ extern "C" int gp_dilated_attn_fwd_ex(const uint16_t* q, int64_t q_row_stride, i
       case 64: dilated_attn_kernel<64><<<(unsigned)items, 256, 0, s>>>(a); break;
       case 96: dilated_attn_kernel<96><<<(unsigned)items, 256, 0, s>>>(a); break;
     }
-  } else if (q_log2_prescaled) {
-    if (D == 48) dilated_attn32_kernel<48, true, 4><<<(unsigned)items, 256, 0, s>>>(a);
+  } else if (impl == 3) {
+    if (D == 48) dilated_attn_pp_kernel<48><<<(unsigned)items, 256, 0, s>>>(a);
+    else dilated_attn_pp_kernel<64><<<(unsigned)items, 256, 0, s>>>(a);
+  } else if (q_log2_prescaled && D == 48 && var != 0) {
+    switch (var) {   // A/B variants of the v2 kernel (GP_ATTN_VAR; 100 = VAR 0)
+      case 100: dilated_attn32_kernel<48, true, 4, 0><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 1: dilated_attn32_kernel<48, true, 4, 1><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 2: dilated_attn32_kernel<48, true, 4, 2><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 3: dilated_attn32_kernel<48, true, 4, 3><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 4: dilated_attn32_kernel<48, true, 4, 4><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 7: dilated_attn32_kernel<48, true, 4, 7><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 11: dilated_attn32_kernel<48, true, 4, 3, 4><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 12: dilated_attn32_kernel<48, true, 4, 2, 4><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 15: dilated_attn32_kernel<48, true, 4, 7, 4><<<(unsigned)items, 256, 0, s>>>(a); break;
+      default: return gp_set_error("gp_dilated_attn_fwd: GP_ATTN_VAR=%d unknown", var), GP_EARG;
+    }
+  } else if (q_log2_prescaled) {   // default: VAR 2 (staging addresses hoisted), +2% over VAR 0
+    if (D == 48) dilated_attn32_kernel<48, true, 4, 2><<<(unsigned)items, 256, 0, s>>>(a);
     else dilated_attn32_kernel<64, true, 4><<<(unsigned)items, 256, 0, s>>>(a);
   } else {
     if (D == 48) dilated_attn32_kernel<48, false, 4><<<(unsigned)items, 256, 0, s>>>(a);

@@ -22,6 +22,7 @@ across calls of the same shape.  No CPU fallback exists: every non-GEMM op is a 
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -29,6 +30,23 @@ import numpy as np
 import torch
 
 from . import _hip
+
+_TUNED = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned", "tunableop_results.csv")
+_tuned_loaded = False
+
+
+def use_tuned_gemms():
+    """Load the hipBLASLt solutions tools/tune_gemms.py selected for the slide encoder's GEMM
+    shapes (PyTorch TunableOp, tuning itself off).  Shapes not in the file keep hipBLASLt's
+    default heuristic.  GIGAPATH_NO_TUNED_GEMMS=1 disables it."""
+    global _tuned_loaded
+    if _tuned_loaded or os.environ.get("GIGAPATH_NO_TUNED_GEMMS") == "1" or not os.path.exists(_TUNED):
+        return
+    _tuned_loaded = True
+    torch.cuda.tunable.enable(True)
+    torch.cuda.tunable.tuning_enable(False)
+    torch.cuda.tunable.record_untuned_enable(False)
+    torch.cuda.tunable.read_file(_TUNED)
 
 
 # ------------------------------------------------------------------------------------------
@@ -236,6 +254,7 @@ class EncoderEngine:
         self.ws: Optional[Workspace] = None
 
     def pack(self, encoder, dev):
+        use_tuned_gemms()
         sig = (str(dev), param_signature(encoder))
         if sig != self._sig:
             self.layers = [PackedLayer.from_module(l, dev) for l in encoder.layers]

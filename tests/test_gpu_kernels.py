@@ -183,7 +183,7 @@ def test_dilated_attention_vs_oracle(name, B, L, segs, ratios, attn_impl):
 LSE_ATOL = 2.5e-3
 
 
-@pytest.mark.parametrize("impl", ["2"])
+@pytest.mark.parametrize("impl", ["2", "3"])
 @pytest.mark.parametrize("name,B,L,segs,ratios", ATTN_CASES)
 def test_dilated_attention_prescaled_q(name, B, L, segs, ratios, impl, monkeypatch):
     monkeypatch.setenv("GP_ATTN_IMPL", impl)

@@ -16,7 +16,7 @@ from gigapath import _hip, runtime  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--L", type=int, default=70001)
 ap.add_argument("--iters", type=int, default=10)
-ap.add_argument("--impls", default="2p,4p")
+ap.add_argument("--impls", default="2p,3p")
 ap.add_argument("--D", type=int, default=48)
 args = ap.parse_args()
 H, D = 16, args.D
@@ -32,11 +32,13 @@ flops = runtime.attention_valid_flops(L, segs, ratios, H, D)
 res = {}
 for rnd in range(args.iters):
     for impl in args.impls.split(","):
-        os.environ["GP_ATTN_IMPL"] = impl.rstrip("p")
+        base, _, var = impl.partition("@")            # "2p@4": impl 2, prescaled q, GP_ATTN_VAR=4
+        os.environ["GP_ATTN_IMPL"] = base.rstrip("p")
+        os.environ["GP_ATTN_VAR"] = var or "0"
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         _hip.dilated_attn_fwd(qkv, qkv[:, E:], qkv[:, 2 * E:], 3 * E, 1, L, H, D, segs, ratios, sc.outs, sc.lses,
-                              0.0, impl.endswith("p"))
+                              0.0, base.endswith("p"))
         e1.record()
         torch.cuda.synchronize()
         if rnd > 0:

@@ -2,12 +2,12 @@
 # PMC passes over the attention kernel (tools/attn_bench.py, impl 2 only). One pass per counter group.
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-OUT=gpurun_out/pmc_attn
+OUT=gpurun_out/pmc_attn_${IMPL:-2p}
 mkdir -p $OUT
 rocprofv3 -L > $OUT/counters.txt 2>&1 || true
 pass() {
   name=$1; shift
-  timeout -s KILL 90 rocprofv3 --pmc "$@" --output-format csv -d $OUT/$name -o run -- python tools/attn_bench.py --impls 2 --iters 3 > $OUT/$name.log 2>&1
+  timeout -s KILL 90 rocprofv3 --pmc "$@" --output-format csv -d $OUT/$name -o run -- python tools/attn_bench.py --impls ${IMPL:-2p} --iters 3 > $OUT/$name.log 2>&1
   echo "pass $name rc=$?"
 }
 pass a SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MFMA
