@@ -331,7 +331,10 @@ GP_DEV float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 // VAR bits (A/B variants, all numerically identical): 1 = S's first k-step takes its C operand
 // from a persistent -m_run block (no per-tile accumulator init), 2 = staging addresses computed
 // once (no per-tile 64-bit index math, no bound checks on full tiles), 4 = all K fragments read
-// before the S MFMAs.  OCC = waves per SIMD the register budget must allow.
+// before the S MFMAs, 8 = the running max rides in a 4th k-step of S (D = 48, kPre): K image
+// column 48 holds 1.0, Q column 48 holds -m (m kept bf16-exact), so S arrives already shifted
+// with no per-tile accumulator initialisation and no extra registers (2 more MFMAs per tile,
+// ~17 fewer VALU).  OCC = waves per SIMD the register budget must allow.
 template <int D, bool kPre, int NW, int VAR = 0, int OCC = 2>
 __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const AttnArgs a) {
   static_assert(D == 48 || D == 64, "v2 kernel covers D = 48 and 64");
@@ -341,7 +344,10 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
   constexpr int KT = 16 * NW;                // keys per staged tile (64 or 128): 3 chunks / thread
   constexpr int KS = D / 16;                 // k-steps of Q.K^T
   constexpr bool kOnes = (D % 32) != 0;      // spare d rows carry the row-sum ones
-  constexpr int KROWB = D * 2 + 16;          // K image row bytes (padded)
+  constexpr bool kMK = (VAR & 8) != 0;       // running max in an extra k-step
+  static_assert(!kMK || (D == 48 && kPre), "VAR 8 needs D = 48 and a pre-scaled q");
+  constexpr int KSS = kMK ? KS + 1 : KS;     // k-steps of S
+  constexpr int KROWB = (kMK ? 64 : D) * 2 + 16;   // K image row bytes (padded)
   constexpr int VROWB = 128;                 // V image row bytes (64 bf16, swizzled 32-B blocks)
   constexpr int KTILE = KT * KROWB;
   constexpr int VTILE = KT * VROWB;
@@ -373,6 +379,13 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
   const uint16_t* kbase = brr.k + (tok0 - brr.kv_tok_base) * brr.kv_stride + kcol;
   const uint16_t* vbase = brr.v + (tok0 - brr.kv_tok_base) * brr.kv_stride + kcol;
 
+  if constexpr (kMK) {   // K image columns 48..63: [1, 0 x 15] (never overwritten by staging)
+    for (int idx = threadIdx.x; idx < 2 * KT * 2; idx += NT) {   // 2 bufs x KT rows x 2 chunks
+      const int buf = idx / (2 * KT), rem = idx % (2 * KT), row = rem >> 1, half = rem & 1;
+      const uint4 col = half ? make_uint4(0, 0, 0, 0) : make_uint4(0x3F80u, 0, 0, 0);
+      *reinterpret_cast<uint4*>(smem + buf * BUF + row * KROWB + 96 + 16 * half) = col;
+    }
+  }
   // V images: the d-columns >= D of every row (block 3 for D = 48) hold bf16 1.0
   if constexpr (kOnes) {
     for (int idx = threadIdx.x; idx < 2 * KT * 2; idx += NT) {   // 2 bufs x KT rows x 2 chunks
@@ -382,8 +395,10 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
     }
   }
 
-  // Q fragments (B operand): lane holds Q[q = l32][d = 16ks + 8h .. +7]
-  bf16x8 qf[KS];
+  // Q fragments (B operand): lane holds Q[q = l32][d = 16ks + 8h .. +7]; with kMK, qf[KS] is
+  // [-m, 0 x 7] on h = 0 lanes and zeros on h = 1 lanes
+  bf16x8 qf[KSS];
+  if constexpr (kMK) qf[KS] = bf16x8{};
   {
     const int i = q0 + w * 32 + l32;
 #pragma unroll
@@ -488,33 +503,38 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
       // VAR & 1: the first k-step takes its C operand from minit (= -m_run in every element, kept
       // in its own registers, rewritten only on a rescale) instead of initialising per tile
       const float init = (kPre && sub > 0) ? -m_run : 0.f;
-      bf16x8 kf[2][KS];
+      bf16x8 kf[2][KSS];
       if constexpr ((VAR & 4) != 0) {      // all K fragments first: one LDS wait, not one per MFMA
   #pragma unroll
         for (int u = 0; u < 2; ++u)
   #pragma unroll
-          for (int ks = 0; ks < KS; ++ks)
+          for (int ks = 0; ks < KSS; ++ks)
             kf[u][ks] = *reinterpret_cast<const bf16x8*>(Kb + (32 * u + l32) * KROWB + 32 * ks + 16 * h);
       }
+      if constexpr ((VAR & 32) != 0) __builtin_amdgcn_s_setprio(1);
   #pragma unroll
       for (int u = 0; u < 2; ++u) {
         f32x16 acc;
-        if constexpr ((VAR & 1) == 0) {
+        if constexpr (kMK) {
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+        } else if constexpr ((VAR & 1) == 0) {
   #pragma unroll
           for (int r = 0; r < 16; ++r) acc[r] = init;
         }
   #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
+        for (int ks = 0; ks < KSS; ++ks) {
           bf16x8 kk;
           if constexpr ((VAR & 4) != 0) kk = kf[u][ks];
           else kk = *reinterpret_cast<const bf16x8*>(Kb + (32 * u + l32) * KROWB + 32 * ks + 16 * h);
-          if constexpr ((VAR & 1) != 0)
+          if constexpr ((VAR & 1) != 0 && !kMK)
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kk, qf[ks], ks == 0 ? minit : acc, 0, 0, 0);
           else
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kk, qf[ks], acc, 0, 0, 0);
         }
         sacc[u] = acc;
       }
+      if constexpr ((VAR & 32) != 0) __builtin_amdgcn_s_setprio(0);
       if (kv0 + 64 > c) {      // keys >= c are zero pads (added analytically at the end)
         // (the -inf below also holds for the kPre accumulator offset)
   #pragma unroll
@@ -542,22 +562,44 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
         // (tile 0: always, which sets m_run to that tile's exact max)
         const bool need = (sub == 0) || (mx > kThr);
         if (__builtin_amdgcn_ballot_w64(need)) {
-          const float delta = need ? mx : 0.f;
-          const float alpha = fast_exp2(-delta);
-          if (sub > 0) {
+          if constexpr (kMK) {
+            // m stays exactly representable in bf16 (it enters the MFMA through q); the shift
+            // applied is the rounded one, so numerator and denominator stay consistent
+            const float m_old = (sub == 0) ? 0.f : m_run;
+            const float m_new = need ? (float)(__bf16)(m_old + mx) : m_old;
+            const float d = m_new - m_old;
+            if (sub > 0) {
+              const float alpha = fast_exp2(-d);
   #pragma unroll
-            for (int mt = 0; mt < 2; ++mt)
+              for (int mt = 0; mt < 2; ++mt)
   #pragma unroll
-              for (int r = 0; r < 16; ++r) oacc[mt][r] *= alpha;
-            lsum *= alpha;
+                for (int r = 0; r < 16; ++r) oacc[mt][r] *= alpha;
+              lsum *= alpha;
+            }
+            m_run = m_new;
+  #pragma unroll
+            for (int u = 0; u < 2; ++u)
+  #pragma unroll
+              for (int r = 0; r < 16; ++r) sacc[u][r] -= d;
+            if (h == 0) qf[KS][0] = (__bf16)(-m_run);
+          } else {
+            const float delta = need ? mx : 0.f;
+            const float alpha = fast_exp2(-delta);
+            if (sub > 0) {
+  #pragma unroll
+              for (int mt = 0; mt < 2; ++mt)
+  #pragma unroll
+                for (int r = 0; r < 16; ++r) oacc[mt][r] *= alpha;
+              lsum *= alpha;
+            }
+            m_run = (sub == 0) ? delta : m_run + delta;
+  #pragma unroll
+            for (int u = 0; u < 2; ++u)
+  #pragma unroll
+              for (int r = 0; r < 16; ++r) sacc[u][r] -= delta;
+  #pragma unroll
+            for (int r = 0; r < 16; ++r) minit[r] = -m_run;
           }
-          m_run = (sub == 0) ? delta : m_run + delta;
-  #pragma unroll
-          for (int u = 0; u < 2; ++u)
-  #pragma unroll
-            for (int r = 0; r < 16; ++r) sacc[u][r] -= delta;
-  #pragma unroll
-          for (int r = 0; r < 16; ++r) minit[r] = -m_run;
         }
   #pragma unroll
         for (int u = 0; u < 2; ++u)
@@ -595,6 +637,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
       }
 
       // ---- O^T += V^T . P^T  (2 sub-tiles x 2 k-steps x 2 d-tiles)
+      if constexpr ((VAR & 32) != 0) __builtin_amdgcn_s_setprio(1);   // MFMA-issuing wave first
   #pragma unroll
       for (int u = 0; u < 2; ++u)
   #pragma unroll
@@ -611,6 +654,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
             oacc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[u][s], oacc[mt], 0, 0, 0);
           }
         }
+      if constexpr ((VAR & 32) != 0) __builtin_amdgcn_s_setprio(0);
     }
 
     if (t + 1 < ntiles) store_tile((t + 1) & 1);
@@ -1162,6 +1206,11 @@ extern "C" int gp_dilated_attn_fwd_ex(const uint16_t* q, int64_t q_row_stride, i
       case 11: dilated_attn32_kernel<48, true, 4, 3, 4><<<(unsigned)items, 256, 0, s>>>(a); break;
       case 12: dilated_attn32_kernel<48, true, 4, 2, 4><<<(unsigned)items, 256, 0, s>>>(a); break;
       case 15: dilated_attn32_kernel<48, true, 4, 7, 4><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 10: dilated_attn32_kernel<48, true, 4, 10><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 14: dilated_attn32_kernel<48, true, 4, 14><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 34: dilated_attn32_kernel<48, true, 4, 34><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 26: dilated_attn32_kernel<48, true, 4, 10, 4><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 30: dilated_attn32_kernel<48, true, 4, 14, 4><<<(unsigned)items, 256, 0, s>>>(a); break;
       default: return gp_set_error("gp_dilated_attn_fwd: GP_ATTN_VAR=%d unknown", var), GP_EARG;
     }
   } else if (q_log2_prescaled) {   // default: VAR 2 (staging addresses hoisted), +2% over VAR 0
