@@ -995,64 +995,108 @@ struct MergeArgs {
   uint16_t* out;
 };
 
-// One wave per token; lane l owns the EPL = E/64 contiguous elements [l*EPL, (l+1)*EPL) of
-// head l*EPL/D (EPL divides D).  Everything that depends only on the token (segment n, sparse
-// row i, dilation phase of each branch) is wave-uniform 32-bit scalar math; only the
-// coverage test "head/hpg == phase" is per lane.
-template <int EPL>
+// One wave per run of kTPW consecutive tokens; lane l owns the EPL = E/64 contiguous elements
+// [l*EPL, (l+1)*EPL) of head l*EPL/D (EPL divides D).  The sparse_to_dense position of the
+// token in every branch -- segment n, dense slot t = p mod g, sparse row i = t / r, phase
+// jj = t mod r -- is wave-uniform: divided out once per run, then stepped token by token.  The
+// lanes a branch covers for phase jj are the contiguous range [jj*LPH, (jj+1)*LPH), LPH = lanes
+// per head group.  Math per token is that of dilated_attention.py:100-131 (fp32 weights,
+// branch-order accumulation) followed by inner_attn_ln.
+constexpr int kTPW = 1;
+
+template <int EPL, int D>
 __global__ __launch_bounds__(256) void branch_merge_kernel(const MergeArgs a) {
   const int lane = threadIdx.x & 63;
-  const int row = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + (int)(threadIdx.x >> 6));
-  if (row >= (int)(a.B * a.ntok)) return;
+  const int run = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + (int)(threadIdx.x >> 6));
+  const int total = (int)(a.B * a.ntok);
+  const int r0 = run * kTPW;
+  if (r0 >= total) return;
   const int nt = (int)a.ntok;
-  const int bidx = row / nt, p = (int)a.tok_lo + (row - bidx * nt);
+  const int E = 64 * EPL;
   const int col0 = lane * EPL;
-  const int hh = col0 / a.D;
-
-  float lse[GP_MAX_BRANCHES];
-  float mx = -INFINITY;
+  const int hh = col0 / D;                       // compile-time divisor
+  int pn[GP_MAX_BRANCHES], pt[GP_MAX_BRANCHES], pi[GP_MAX_BRANCHES], pj[GP_MAX_BRANCHES];
+  int bidx = 0, p = 0;
+  for (int k = 0; k < kTPW; ++k) {
+    const int row = r0 + k;
+    if (row >= total) break;
+    if (k == 0 || p + 1 >= (int)a.tok_lo + nt) {   // (re)derive positions: run start / next batch
+      bidx = row / nt;
+      p = (int)a.tok_lo + (row - bidx * nt);
 #pragma unroll
-  for (int b = 0; b < GP_MAX_BRANCHES; ++b) {
-    lse[b] = -1e8f;
-    if (b < a.nbranch) {
-      const GpBranch g = a.br[b].g;
-      const int n = p / g.g, t = p - n * g.g;       // sparse_to_dense slot of token p
-      const int i = t / g.r, jj = t - i * g.r;
-      if (hh / g.hpg == jj) {
-        const float v = a.br[b].lse[((int64_t)(bidx * g.nseg + n) * a.H + hh) * g.m + i];
-        lse[b] = (v == 0.f) ? -1e8f : v;             // dilated_attention.py:46
+      for (int b = 0; b < GP_MAX_BRANCHES; ++b)
+        if (b < a.nbranch) {
+          const GpBranch& g = a.br[b].g;
+          pn[b] = p / g.g;
+          pt[b] = p - pn[b] * g.g;
+          pi[b] = pt[b] / g.r;
+          pj[b] = pt[b] - pi[b] * g.r;
+        }
+    } else {
+      ++p;
+#pragma unroll
+      for (int b = 0; b < GP_MAX_BRANCHES; ++b)
+        if (b < a.nbranch) {
+          const GpBranch& g = a.br[b].g;
+          if (++pt[b] == g.g) { pt[b] = 0; ++pn[b]; pi[b] = 0; pj[b] = 0; }
+          else if (++pj[b] == g.r) { pj[b] = 0; ++pi[b]; }
+        }
+    }
+    // issue every load first (the o rows do not depend on the weights), then the math
+    float lse[GP_MAX_BRANCHES];
+    bool cov[GP_MAX_BRANCHES];
+    uint2 ob[GP_MAX_BRANCHES][EPL / 4];
+#pragma unroll
+    for (int b = 0; b < GP_MAX_BRANCHES; ++b) {
+      lse[b] = -1e8f;
+      cov[b] = false;
+      if (b < a.nbranch) {
+        const GpBranch& g = a.br[b].g;
+        const int lph = g.hpg * (D / EPL);        // lanes per head group
+        cov[b] = lane >= pj[b] * lph && lane < (pj[b] + 1) * lph;
+        if (cov[b]) {
+          lse[b] = a.br[b].lse[((int64_t)(bidx * g.nseg + pn[b]) * a.H + hh) * g.m + pi[b]];
+          const uint2* src = reinterpret_cast<const uint2*>(
+              a.br[b].o + ((int64_t)(bidx * g.nseg + pn[b]) * g.m + pi[b]) * E + col0);
+#pragma unroll
+          for (int q = 0; q < EPL / 4; ++q) ob[b][q] = src[q];
+        }
       }
-      mx = fmaxf(mx, lse[b]);
     }
-  }
-  float wsum = 0.f;
+    float mx = -INFINITY;
 #pragma unroll
-  for (int b = 0; b < GP_MAX_BRANCHES; ++b)
-    if (b < a.nbranch) {
-      lse[b] = expf(lse[b] - mx);
-      wsum += lse[b];
-    }
-  const float inv = 1.0f / wsum;
-  float acc[EPL];
+    for (int b = 0; b < GP_MAX_BRANCHES; ++b)
+      if (b < a.nbranch) {
+        if (cov[b] && lse[b] == 0.f) lse[b] = -1e8f;   // dilated_attention.py:46
+        mx = fmaxf(mx, lse[b]);
+      }
+    float wsum = 0.f;
 #pragma unroll
-  for (int e = 0; e < EPL; ++e) acc[e] = 0.f;
+    for (int b = 0; b < GP_MAX_BRANCHES; ++b)
+      if (b < a.nbranch) {
+        lse[b] = expf(lse[b] - mx);
+        wsum += lse[b];
+      }
+    const float inv = 1.0f / wsum;
+    float acc[EPL];
 #pragma unroll
-  for (int b = 0; b < GP_MAX_BRANCHES; ++b) {
-    if (b < a.nbranch) {
-      const GpBranch g = a.br[b].g;
-      const int n = p / g.g, t = p - n * g.g;
-      const int i = t / g.r, jj = t - i * g.r;
-      if (hh / g.hpg == jj) {
+    for (int e = 0; e < EPL; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int b = 0; b < GP_MAX_BRANCHES; ++b) {
+      if (b < a.nbranch && cov[b]) {
         const float wb = lse[b] * inv;
-        float ov[EPL];
-        load_bf16<EPL>(a.br[b].o + ((int64_t)(bidx * g.nseg + n) * g.m + i) * (a.H * a.D) + col0, ov);
 #pragma unroll
-        for (int e = 0; e < EPL; ++e) acc[e] += ov[e] * wb;
+        for (int q = 0; q < EPL / 4; ++q) {
+          acc[4 * q + 0] += __uint_as_float(ob[b][q].x << 16) * wb;
+          acc[4 * q + 1] += __uint_as_float(ob[b][q].x & 0xffff0000u) * wb;
+          acc[4 * q + 2] += __uint_as_float(ob[b][q].y << 16) * wb;
+          acc[4 * q + 3] += __uint_as_float(ob[b][q].y & 0xffff0000u) * wb;
+        }
       }
     }
+    if (a.ln_w != nullptr) wave_layernorm<EPL>(acc, E, a.ln_w, a.ln_b, a.eps, col0);   // weights via L1
+    store_bf16<EPL>(a.out + (int64_t)row * E + col0, acc);
   }
-  if (a.ln_w != nullptr) wave_layernorm<EPL>(acc, a.E, a.ln_w, a.ln_b, a.eps, col0);
-  store_bf16<EPL>(a.out + (int64_t)row * a.E + col0, acc);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1268,7 +1312,9 @@ extern "C" int gp_branch_merge_ln_window(const uint16_t* const* o_in, const floa
                                          const float* ln_b, float eps, uint16_t* out, void* stream) {
   const int E = H * D;
   GP_REQUIRE(nbranch >= 1 && nbranch <= GP_MAX_BRANCHES, "gp_branch_merge_ln: nbranch must be 1..%d", GP_MAX_BRANCHES);
-  GP_REQUIRE((E == 768 || E == 1024 || E == 1536) && D % (E / 64) == 0, "gp_branch_merge_ln: H*D=%d unsupported", E);
+  GP_REQUIRE((E == 768 && (D == 48 || D == 96 || D == 12)) || (E == 1024 && (D == 64 || D == 16)) ||
+                 (E == 1536 && (D == 96 || D == 48 || D == 24)),
+             "gp_branch_merge_ln: H*D=%d with D=%d unsupported", E, D);
   GP_REQUIRE(B * L < (int64_t)0x7fffffff, "gp_branch_merge_ln: B*L too large");
   GP_REQUIRE(B > 0 && L > 0 && tok_lo >= 0 && n_tok >= 0 && tok_lo + n_tok <= L, "gp_branch_merge_ln: bad sizes");
   if (n_tok == 0) return 0;
@@ -1285,12 +1331,23 @@ extern "C" int gp_branch_merge_ln_window(const uint16_t* const* o_in, const floa
   }
   for (int b = nbranch; b < GP_MAX_BRANCHES; ++b) a.br[b] = a.br[nbranch - 1];
   a.ln_w = ln_w; a.ln_b = ln_b; a.eps = eps; a.out = out;
-  const unsigned nb = (unsigned)((B * n_tok + 3) / 4);   // one token per wave
+  const unsigned nb = (unsigned)((B * n_tok + 4 * kTPW - 1) / (4 * kTPW));   // kTPW tokens per wave
   hipStream_t s = gp_stream(stream);
   switch (E) {
-    case 768: branch_merge_kernel<12><<<nb, 256, 0, s>>>(a); break;
-    case 1024: branch_merge_kernel<16><<<nb, 256, 0, s>>>(a); break;
-    case 1536: branch_merge_kernel<24><<<nb, 256, 0, s>>>(a); break;
+    case 768:
+      if (D == 48) branch_merge_kernel<12, 48><<<nb, 256, 0, s>>>(a);
+      else if (D == 96) branch_merge_kernel<12, 96><<<nb, 256, 0, s>>>(a);
+      else branch_merge_kernel<12, 12><<<nb, 256, 0, s>>>(a);
+      break;
+    case 1024:
+      if (D == 64) branch_merge_kernel<16, 64><<<nb, 256, 0, s>>>(a);
+      else branch_merge_kernel<16, 16><<<nb, 256, 0, s>>>(a);
+      break;
+    case 1536:
+      if (D == 96) branch_merge_kernel<24, 96><<<nb, 256, 0, s>>>(a);
+      else if (D == 48) branch_merge_kernel<24, 48><<<nb, 256, 0, s>>>(a);
+      else branch_merge_kernel<24, 24><<<nb, 256, 0, s>>>(a);
+      break;
   }
   return gp_check_launch("gp_branch_merge_ln");
 }

@@ -3,6 +3,8 @@
 // lane owning EPL = cols/64 contiguous values (16-byte fp32 / 8-byte bf16 accesses).
 #include <math.h>
 
+#include <stdlib.h>
+
 #include "gp_api.h"
 #include "gp_common.h"
 
@@ -126,6 +128,25 @@ __global__ __launch_bounds__(256) void residual_ln_kernel(float* __restrict__ x,
 }
 
 // ---------------------------------------------------------------------------------------
+// Exact-erf GELU, x * Phi(x) = 0.5 x (1 + erf(x / sqrt 2)) (feedforward_network.py:135, torch's
+// F.gelu default), with erf from Abramowitz & Stegun 7.1.26: |erf error| <= 1.5e-7, i.e. GELU
+// within 0.75e-7 |x| of the libm value -- far below the bf16 rounding of the output, at a
+// fraction of erff's instruction count (one v_rcp, one v_exp, ~10 FMA-class ops).
+GP_DEV float gelu_erf(float x) {
+  const float z = fabsf(x) * 0.70710678118654752440f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  float poly = fmaf(1.061405429f, t, -1.453152027f);
+  poly = fmaf(poly, t, 1.421413741f);
+  poly = fmaf(poly, t, -0.284496736f);
+  poly = fmaf(poly, t, 0.254829592f);
+  poly *= t;
+  const float e = __builtin_amdgcn_exp2f(-z * z * 1.44269504088896340736f);
+  const float erf_x = copysignf(fmaf(-poly, e, 1.0f), x);
+  const float hx = 0.5f * x;
+  return fmaf(hx, erf_x, hx);
+}
+
+// ---------------------------------------------------------------------------------------
 // GELU + LN over a 3072/4096/6144-wide bf16 row: one 256-thread block per row, thread t owns
 // elements k*1024 + 4t + {0..3} (k < EPT/4: each wave-instruction covers 512 contiguous bytes);
 // mean and variance through a 4-wave LDS reduction.  Small register footprint keeps many rows
@@ -144,7 +165,7 @@ __global__ __launch_bounds__(256) void gelu_ln_kernel(const uint16_t* h, const f
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < EPT; ++i) {
-    v[i] = 0.5f * v[i] * (1.0f + erff(v[i] * 0.70710678118654752440f));
+    v[i] = gelu_erf(v[i]);
     s += v[i];
   }
   s = wave_sum(s);
@@ -172,6 +193,44 @@ __global__ __launch_bounds__(256) void gelu_ln_kernel(const uint16_t* h, const f
   uint16_t* dst = out + row * cols;
 #pragma unroll
   for (int k = 0; k < EPT / 4; ++k) store_bf16<4>(dst + k * 1024 + 4 * t, v + 4 * k);
+}
+
+// GELU + LN, one 64-lane wave per row (no LDS, no barrier): lane owns elements
+// k*512 + 8*lane + {0..7}, k < EPL/8 (16-byte accesses, each wave-instruction one contiguous
+// 1 KiB span); LN weights are read per 8-element chunk in the epilogue (L1/L2 resident).
+template <int EPL>
+__global__ __launch_bounds__(256) void gelu_ln_wave_kernel(const uint16_t* h, const float* __restrict__ ln_w,
+                                                           const float* __restrict__ ln_b, float eps,
+                                                           uint16_t* out, int64_t rows) {
+  constexpr int C = 64 * EPL;
+  const int lane = threadIdx.x & 63;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += (int64_t)gridDim.x * 4) {
+    float v[EPL];
+    ld_x8_bf16<EPL>(h + row * C, lane, v);
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < EPL; ++i) {
+      v[i] = gelu_erf(v[i]);
+      s += v[i];
+    }
+    const float mean = wave_sum(s) / (float)C;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < EPL; ++i) {
+      const float d = v[i] - mean;
+      q += d * d;
+    }
+    const float rstd = rsqrtf(wave_sum(q) / (float)C + eps);
+#pragma unroll
+    for (int k = 0; k < EPL / 8; ++k) {
+      float wv[8], bv[8];
+      load_f32<8>(ln_w + k * 512 + 8 * lane, wv);
+      load_f32<8>(ln_b + k * 512 + 8 * lane, bv);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[8 * k + i] = (v[8 * k + i] - mean) * rstd * wv[i] + bv[i];
+    }
+    st_x8_bf16<EPL>(out + row * C, lane, v);
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -281,10 +340,20 @@ extern "C" int gp_gelu_layernorm(const uint16_t* h, const float* ln_w, const flo
   GP_REQUIRE(h && ln_w && ln_b && out, "gp_gelu_layernorm: null pointer");
   hipStream_t s = gp_stream(stream);
   GP_REQUIRE(rows < (int64_t)0x7fffffff, "gp_gelu_layernorm: too many rows");
-  switch (cols / 256) {
-    case 12: gelu_ln_kernel<12><<<(unsigned)rows, 256, 0, s>>>(h, ln_w, ln_b, eps, out, rows, cols); break;
-    case 16: gelu_ln_kernel<16><<<(unsigned)rows, 256, 0, s>>>(h, ln_w, ln_b, eps, out, rows, cols); break;
-    case 24: gelu_ln_kernel<24><<<(unsigned)rows, 256, 0, s>>>(h, ln_w, ln_b, eps, out, rows, cols); break;
+  const char* impl = getenv("GP_GELU_IMPL");    // A/B: 1 = block-per-row kernel
+  if (impl && atoi(impl) == 1) {
+    switch (cols / 256) {
+      case 12: gelu_ln_kernel<12><<<(unsigned)rows, 256, 0, s>>>(h, ln_w, ln_b, eps, out, rows, cols); break;
+      case 16: gelu_ln_kernel<16><<<(unsigned)rows, 256, 0, s>>>(h, ln_w, ln_b, eps, out, rows, cols); break;
+      case 24: gelu_ln_kernel<24><<<(unsigned)rows, 256, 0, s>>>(h, ln_w, ln_b, eps, out, rows, cols); break;
+    }
+  } else {
+    const unsigned nb = (unsigned)((rows + 3) / 4 < (1 << 20) ? (rows + 3) / 4 : (1 << 20));
+    switch (cols / 64) {
+      case 48: gelu_ln_wave_kernel<48><<<nb, 256, 0, s>>>(h, ln_w, ln_b, eps, out, rows); break;
+      case 64: gelu_ln_wave_kernel<64><<<nb, 256, 0, s>>>(h, ln_w, ln_b, eps, out, rows); break;
+      case 96: gelu_ln_wave_kernel<96><<<nb, 256, 0, s>>>(h, ln_w, ln_b, eps, out, rows); break;
+    }
   }
   return gp_check_launch("gp_gelu_layernorm");
 }
