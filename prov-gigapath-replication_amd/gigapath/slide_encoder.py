@@ -85,6 +85,11 @@ class LongNetViT(nn.Module):
         self._top = None
         self._pos_full = None
         self._sp = None
+        # HIP graphs: the whole single-device forward as one replay per input shape
+        self.use_hip_graphs = False
+        self.max_hip_graphs = 64
+        self._graphs = {}
+        self._graph_ws = {}
         self.initialize_vit_weights()
 
     # ---------------------------------------------------------------- sequence parallel
@@ -174,9 +179,66 @@ class LongNetViT(nn.Module):
         B, N, C = x.shape
         if coords.shape != (B, N, 2):
             raise ValueError("coords must be [B, N, 2], got %s" % (tuple(coords.shape),))
-        E, L, M = self.embed_dim, N + 1, B * (N + 1)
         if self._sp is not None and self._sp.world > 1:
             return self._forward_sp(x, coords, all_layer_embed)
+        if self.use_hip_graphs and not runtime.TIMER.enabled:
+            return self._forward_graphed(x, coords, all_layer_embed)
+        return self._forward_device(x, coords, all_layer_embed, self.validate_positions)
+
+    def _forward_graphed(self, x, coords, all_layer_embed):
+        """Replay of a HIP graph holding the whole forward (~170 launches) for this input shape:
+        captured on first use per (shape, dtypes, options, weights version), inputs copied into the
+        graph's static buffers, outputs cloned out.  Coordinates are validated eagerly first (one
+        small kernel + one sync, as in the eager path)."""
+        dev = self.cls_token.device
+        B, N, C = x.shape
+        c = coords if coords.dtype in (torch.float32, torch.float64) else coords.float()
+        if self.validate_positions:
+            pos = torch.empty(B * N, dtype=torch.int64, device=dev)
+            err = torch.zeros(1, dtype=torch.int32, device=dev)
+            _hip.coords_to_pos(c.contiguous(), self.slide_ngrids, self.tile_size, pos, err)
+            if int(err.item()) > 0:
+                raise IndexError("coords map outside pos_embed (%d rows): %d tiles" %
+                                 (self.slide_ngrids ** 2 + 1, int(err.item())))
+        self._packed_top(dev)
+        self.encoder.engine.pack(self.encoder, dev)
+        key = (str(dev), tuple(x.shape), x.dtype, c.dtype, bool(all_layer_embed), bool(self.global_pool),
+               self._top_sig, self.encoder.engine._sig)
+        ent = self._graphs.get(key)
+        if ent is None:
+            ent = self._capture(key, x, c, all_layer_embed)
+        graph, sx, sc, outs = ent
+        sx.copy_(x)
+        sc.copy_(c)
+        graph.replay()
+        return [o.clone() for o in outs]
+
+    def _capture(self, key, x, c, all_layer_embed):
+        while len(self._graphs) >= self.max_hip_graphs:          # oldest first (insertion order)
+            old = next(iter(self._graphs))
+            self._graphs.pop(old)
+            self._graph_ws.pop(old, None)
+        sx, sc = x.detach().clone(), c.detach().clone().contiguous()
+        cur = torch.cuda.current_stream()
+        side = torch.cuda.Stream(device=sx.device)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):                             # warm-up: allocations, TunableOp lookups
+            self._forward_device(sx, sc, all_layer_embed, False)
+        cur.wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            outs = self._forward_device(sx, sc, all_layer_embed, False)
+        # the graph bakes this shape's workspace: keep it alive with the graph
+        ent = (graph, sx, sc, outs)
+        self._graphs[key] = ent
+        self._graph_ws[key] = self.encoder.engine.ws
+        return ent
+
+    def _forward_device(self, x, coords, all_layer_embed, validate):
+        """The eager forward: every launch on the current stream (captured as is by _capture)."""
+        dev = self.cls_token.device
+        B, N, C = x.shape
+        E, L, M = self.embed_dim, N + 1, B * (N + 1)
         top = self._packed_top(dev)
         eng = self.encoder.engine
         layers = eng.pack(self.encoder, dev)
@@ -193,7 +255,7 @@ class LongNetViT(nn.Module):
         c = coords if coords.dtype in (torch.float32, torch.float64) else coords.float()
         ws.err.zero_()
         _hip.coords_to_pos(c.contiguous(), self.slide_ngrids, self.tile_size, ws.pos, ws.err)
-        if self.validate_positions and int(ws.err.item()) > 0:
+        if validate and int(ws.err.item()) > 0:
             raise IndexError("coords map outside pos_embed (%d rows): %d tiles" %
                              (self.slide_ngrids ** 2 + 1, int(ws.err.item())))
         with runtime.TIMER.span("posembed"):

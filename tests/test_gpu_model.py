@@ -163,3 +163,40 @@ def test_full_size_70k_one_layer_vs_oracle(model):
     for t in [0, 1, 1023, 1024, 5791, 5792, 32767, 32768, 69999, 70000]:
         r2, c2, ok2 = close_enough(got[t], ref[t])
         assert c2 >= 0.999, (t, r2, c2)
+
+
+def test_hip_graph_replay_matches_eager(model):
+    """use_hip_graphs: one graph replay per input shape, bit-identical to the eager launches,
+    across shape changes (each graph keeps its own workspace) and weight updates (re-capture)."""
+    shapes = [1500, 700, 1500]
+    x = {n: orc.synthetic_slide(n, seed_x=n) for n in set(shapes)}
+    with torch.no_grad():
+        eager = {n: torch.stack(model(torch.from_numpy(x[n][0]).to(DEV), torch.from_numpy(x[n][1]).to(DEV),
+                                      all_layer_embed=True)) for n in set(shapes)}
+        model.use_hip_graphs = True
+        try:
+            for n in shapes:
+                xt, ct = torch.from_numpy(x[n][0]).to(DEV), torch.from_numpy(x[n][1]).to(DEV)
+                got = torch.stack(model(xt, ct, all_layer_embed=True))
+                assert torch.equal(got, eager[n]), n
+            assert len(model._graphs) == 2
+            # a weight update changes the packed-weight signature -> new capture, new result
+            w = model.encoder.layers[3].ffn.fc2.weight
+            saved = w.detach().clone()
+            w.mul_(0.5)                  # in-place on the parameter: bumps its version
+            n = shapes[0]
+            got = torch.stack(model(torch.from_numpy(x[n][0]).to(DEV), torch.from_numpy(x[n][1]).to(DEV),
+                                    all_layer_embed=True))
+            assert not torch.equal(got, eager[n])
+            w.copy_(saved)
+            got = torch.stack(model(torch.from_numpy(x[n][0]).to(DEV), torch.from_numpy(x[n][1]).to(DEV),
+                                    all_layer_embed=True))
+            assert torch.equal(got, eager[n])
+            with pytest.raises(IndexError):
+                bad = torch.from_numpy(x[n][1]).to(DEV).clone()
+                bad[0, 0, 0] = 256.0 * 1000
+                model(torch.from_numpy(x[n][0]).to(DEV), bad)
+        finally:
+            model.use_hip_graphs = False
+            model._graphs.clear()
+            model._graph_ws.clear()
