@@ -125,7 +125,9 @@ def main():
     model.validate_positions = True
     if sp:
         model.enable_sequence_parallel()
-    model.use_hip_graphs = not args.no_graphs and not sp   # SP runs eager (RCCL calls between kernels)
+    # graphs: the whole forward (1 GPU, C5) or, under SP, the per-layer compute segments between
+    # the RCCL exchanges (collectives stay eager)
+    model.use_hip_graphs = not args.no_graphs
     if mixed:
         from gigapath import batch
         sizes = batch.mixed_batch_sizes()

@@ -35,12 +35,14 @@ _TUNED = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned", "tuna
 _tuned_loaded = False
 
 
-def use_tuned_gemms():
+def use_tuned_gemms(dev=None):
     """Load the hipBLASLt solutions tools/tune_gemms.py selected for the slide encoder's GEMM
     shapes (PyTorch TunableOp, tuning itself off).  Shapes not in the file keep hipBLASLt's
     default heuristic.  GIGAPATH_NO_TUNED_GEMMS=1 disables it."""
     global _tuned_loaded
     if _tuned_loaded or os.environ.get("GIGAPATH_NO_TUNED_GEMMS") == "1" or not os.path.exists(_TUNED):
+        return
+    if dev is None or torch.device(dev).type != "cuda":
         return
     _tuned_loaded = True
     torch.cuda.tunable.enable(True)
@@ -254,7 +256,7 @@ class EncoderEngine:
         self.ws: Optional[Workspace] = None
 
     def pack(self, encoder, dev):
-        use_tuned_gemms()
+        use_tuned_gemms(dev)
         sig = (str(dev), param_signature(encoder))
         if sig != self._sig:
             self.layers = [PackedLayer.from_module(l, dev) for l in encoder.layers]

@@ -303,6 +303,9 @@ class SeqParallelEngine:
         self._hrecvs = plan.halo_recvs(rank)
         self._ssplit = [plan.send_splits(rank, b) for b in range(len(plan.geo))]
         self._rsplit = [plan.recv_splits(rank, b) for b in range(len(plan.geo))]
+        self.use_graphs = False
+        self.graphs = {}                    # (segment, layer, weights signature) -> CUDAGraph
+        self._graph_sig = None
 
     def sparsify(self, ws: ShardWorkspace):
         """This rank's sparsified K/V rows, written into every peer's chunk of the send buffers."""
@@ -348,42 +351,72 @@ class SeqParallelEngine:
             _hip.dilated_attn_fwd_ex(ws.qkv_ext, 3 * plan.E, a - ws.hq, 1, plan.L, plan.H, plan.D, a, e, descs, 0.0,
                                      pa.prescaled)
 
-    def run_layers(self, layers, ws: ShardWorkspace, layer_hook=None):
-        """ws.x holds this shard's fp32 embedding and ws.a = LN1_0(ws.x).  Runs every layer in place."""
+    def _segment(self, key, fn):
+        """Run fn (launches on the current stream only, no collectives, no host syncs); with
+        use_graphs, the first call runs it eagerly and captures it, later calls replay."""
+        if not self.use_graphs or runtime.TIMER.enabled:
+            fn()
+            return
+        g = self.graphs.get(key)
+        if g is None:
+            fn()                                    # this call's work (and allocator warm-up)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                fn()                                # captured, not executed
+            self.graphs[key] = g
+            return
+        g.replay()
+
+    def run_layers(self, layers, ws: ShardWorkspace, layer_hook=None, weights_sig=None):
+        """ws.x holds this shard's fp32 embedding and ws.a = LN1_0(ws.x).  Runs every layer in place.
+        Per layer: [QKV GEMM + sparsify] -> all-to-alls (phase A, phase B) -> wait A -> attention A
+        -> wait B -> [attention B + merge + out-proj + residual/LN + FFN + residual/LN]; with
+        use_graphs the two bracketed segments are HIP-graph replays (collectives stay eager)."""
         plan = self.plan
         E, H, D = plan.E, plan.H, plan.D
         a, e = plan.bounds[self.rank]
         M = ws.n
         F = ws.f.shape[1]
         nl = len(layers)
+        wsig = weights_sig if weights_sig is not None else id(layers)
+        if wsig != self._graph_sig:          # new weights: captures of the old ones never replay
+            self.graphs.clear()
+            self._graph_sig = wsig
         for li, pl in enumerate(layers):
             pa = pl.attn
-            with runtime.TIMER.span("gemm_qkv"):
-                torch.addmm(pa.b_qkv, ws.a, pa.w_qkv.t(), out=ws.qkv)
-            self.sparsify(ws)
+            nxt = layers[li + 1] if li + 1 < nl else None
+
+            def head(pa=pa):
+                with runtime.TIMER.span("gemm_qkv"):
+                    torch.addmm(pa.b_qkv, ws.a, pa.w_qkv.t(), out=ws.qkv)
+                self.sparsify(ws)
+
+            def tail(pa=pa, pl=pl, nxt=nxt):
+                self.attention(pa, ws, plan.phase_b)
+                with runtime.TIMER.span("merge"):
+                    _hip.branch_merge_ln_window(ws.attn.outs, ws.attn.lses, plan.segs, plan.ratios, 1, plan.L, a, M,
+                                                H, D, pa.ln_w, pa.ln_b, pa.ln_eps, ws.a)
+                with runtime.TIMER.span("gemm_out"):
+                    torch.mm(ws.a, pa.w_o.t(), out=ws.y)
+                with runtime.TIMER.span("resid_ln"):
+                    _hip.residual_layernorm(ws.x, ws.y, pa.b_o, pl.ln2_w, pl.ln2_b, pl.ln2_eps, ws.a, M, E)
+                with runtime.TIMER.span("gemm_fc1"):
+                    torch.addmm(pl.b1, ws.a, pl.w1.t(), out=ws.f)
+                with runtime.TIMER.span("gelu_ln"):
+                    _hip.gelu_layernorm(ws.f, pl.fln_w, pl.fln_b, pl.fln_eps, ws.f, M, F)
+                with runtime.TIMER.span("gemm_fc2"):
+                    torch.mm(ws.f, pl.w2.t(), out=ws.y)
+                with runtime.TIMER.span("resid_ln"):
+                    _hip.residual_layernorm(ws.x, ws.y, pl.b2, nxt.ln1_w if nxt else None,
+                                            nxt.ln1_b if nxt else None, nxt.ln1_eps if nxt else 1e-5, ws.a, M, E)
+
+            self._segment(("head", li, wsig), head)
             h_a = self.exchange(ws, plan.phase_a, halo=True)
             h_b = self.exchange(ws, plan.phase_b, halo=False)
             Exchange.wait(h_a)
             self.attention(pa, ws, plan.phase_a)
             Exchange.wait(h_b)
-            self.attention(pa, ws, plan.phase_b)
-            with runtime.TIMER.span("merge"):
-                _hip.branch_merge_ln_window(ws.attn.outs, ws.attn.lses, plan.segs, plan.ratios, 1, plan.L, a, M, H, D,
-                                            pa.ln_w, pa.ln_b, pa.ln_eps, ws.a)
-            with runtime.TIMER.span("gemm_out"):
-                torch.mm(ws.a, pa.w_o.t(), out=ws.y)
-            with runtime.TIMER.span("resid_ln"):
-                _hip.residual_layernorm(ws.x, ws.y, pa.b_o, pl.ln2_w, pl.ln2_b, pl.ln2_eps, ws.a, M, E)
-            with runtime.TIMER.span("gemm_fc1"):
-                torch.addmm(pl.b1, ws.a, pl.w1.t(), out=ws.f)
-            with runtime.TIMER.span("gelu_ln"):
-                _hip.gelu_layernorm(ws.f, pl.fln_w, pl.fln_b, pl.fln_eps, ws.f, M, F)
-            with runtime.TIMER.span("gemm_fc2"):
-                torch.mm(ws.f, pl.w2.t(), out=ws.y)
-            nxt = layers[li + 1] if li + 1 < nl else None
-            with runtime.TIMER.span("resid_ln"):
-                _hip.residual_layernorm(ws.x, ws.y, pl.b2, nxt.ln1_w if nxt else None, nxt.ln1_b if nxt else None,
-                                        nxt.ln1_eps if nxt else 1e-5, ws.a, M, E)
+            self._segment(("tail", li, wsig), tail)
             if layer_hook is not None:
                 layer_hook(li + 1)
 

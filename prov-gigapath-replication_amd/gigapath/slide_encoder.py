@@ -304,6 +304,7 @@ class LongNetViT(nn.Module):
         pa = layers[0].attn
         F = self.encoder.args.encoder_ffn_embed_dim
         plan, ws, spe = sp.prepare(dev, L, pa.segs, pa.ratios, pa.H, pa.D, F)
+        spe.use_graphs = self.use_hip_graphs
         a, e = plan.bounds[sp.rank]
         t0, t1 = max(a, 1) - 1, e - 1                      # tiles of this shard (token = tile + 1)
         nt = t1 - t0
@@ -350,7 +351,7 @@ class LongNetViT(nn.Module):
 
         if all_layer_embed:
             readout(0)
-        spe.run_layers(layers, ws, readout if all_layer_embed else None)
+        spe.run_layers(layers, ws, readout if all_layer_embed else None, weights_sig=eng._sig)
         if not all_layer_embed:
             if self.global_pool:
                 _hip.layernorm_f32(ws.x, E, top["enc_w"], top["enc_b"], top["enc_eps"], ws.x, ws.n, E)

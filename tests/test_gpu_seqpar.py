@@ -48,6 +48,12 @@ def _worker(rank, world, port, N, max_wsi_size, global_pool, q):
         with torch.no_grad():
             out = torch.stack(model(xt, ct, all_layer_embed=True)).cpu().numpy()
             last = model(xt, ct)[0].cpu().numpy()
+            # per-layer compute segments as HIP-graph replays: bit-identical to the eager shard
+            model.use_hip_graphs = True
+            for _ in range(2):                       # capture, then replay
+                g_out = torch.stack(model(xt, ct, all_layer_embed=True)).cpu().numpy()
+                assert np.array_equal(g_out, out), "graph replay differs from eager"
+            model.use_hip_graphs = False
         dist.barrier()
         dist.destroy_process_group()
         q.put((rank, (out, last)))
