@@ -361,7 +361,7 @@ class SeqParallelEngine:
         if g is None:
             fn()                                    # this call's work (and allocator warm-up)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 fn()                                # captured, not executed
             self.graphs[key] = g
             return

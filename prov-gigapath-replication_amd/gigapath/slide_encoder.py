@@ -226,7 +226,7 @@ class LongNetViT(nn.Module):
             self._forward_device(sx, sc, all_layer_embed, False)
         cur.wait_stream(side)
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
             outs = self._forward_device(sx, sc, all_layer_embed, False)
         # the graph bakes this shape's workspace: keep it alive with the graph
         ent = (graph, sx, sc, outs)
