@@ -81,9 +81,10 @@ def pmc_traffic(n_tiles, kernel):
             d = json.load(f)
     except (OSError, ValueError):
         return None
-    k = d.get("kernels", {}).get(kernel)
-    if d.get("tiles") != n_tiles or k is None:
+    ks = [v for name, v in sorted(d.get("kernels", {}).items()) if name.startswith(kernel)]
+    if d.get("tiles") != n_tiles or not ks:
         return None
+    k = ks[0]
     return round(k["hbm_bytes_per_launch"])
 
 
@@ -203,7 +204,7 @@ def main():
         total_tf = (runtime.gemm_flops(1, args.tiles, 768, 3072, 1536, 12)
                     + 12 * runtime.attention_valid_flops(L, segs, ratios, 16, 48)) / 1e12
     plain = not (sp or mixed)          # the PMC summary was collected on the plain C3 run
-    traffic = pmc_traffic(args.tiles, "dilated_attn32_kernel<48, true, 4>") if plain else None
+    traffic = pmc_traffic(args.tiles, "dilated_attn32_kernel<48, true, 4") if plain else None
     # HBM-bound merge kernel: algorithmic bytes per launch over its live launch time
     n_mg, ms_mg = kt.get("merge", (0, 0.0))
     if sp:
@@ -236,7 +237,7 @@ def main():
         "attn_mfma_util_pct": round(100 * achieved / PEAK_BF16_TFLOPS, 2),
         "merge_roofline": {"bound": "hbm", "kernel": "gp_branch_merge_ln", "achieved": round(merge_gbs, 1),
                            "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(merge_gbs / PEAK_HBM_GBS, 4),
-                           "traffic": pmc_traffic(args.tiles, "branch_merge_kernel<12>") if plain else None,
+                           "traffic": pmc_traffic(args.tiles, "branch_merge_kernel<12") if plain else None,
                            "bytes_per_launch": merge_bytes},
         "model_tflops": round(total_tf * args.steps * (1 if (sp or mixed) else world) / elapsed, 2),
         "kernel_ms_per_step": {k: round(v[1] / args.timing_steps, 3) for k, v in sorted(kt.items())},
