@@ -158,3 +158,17 @@ def test_flops_model_matches_survey():
     gemm = runtime.gemm_flops(1, 70000, 768, 3072, 1536, 12)
     assert abs(att / 1e12 - 14.868) < 0.01
     assert abs((att + gemm) / 1e12 - 26.924) < 0.01
+
+
+def test_classification_head_surface():
+    """The reference's slide-level caller (classification_head.py): same constructor, encoder
+    frozen (inference-only engine), classifier over the selected layer embeddings."""
+    from gigapath import classification_head
+    head = classification_head.get_model(input_dim=1536, latent_dim=768, feat_layer="5-11", n_classes=3,
+                                         model_arch="gigapath_slide_enc12l768d", pretrained="")
+    assert head.feat_layer == [5, 11] and head.feat_dim == 1536
+    assert head.classifier[0].weight.shape == (3, 1536)
+    assert not any(p.requires_grad for p in head.slide_encoder.parameters())
+    head.train()
+    assert head.training and not head.slide_encoder.training
+    assert sum(p.requires_grad for p in head.parameters()) == 2      # classifier weight + bias

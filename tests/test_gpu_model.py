@@ -200,3 +200,40 @@ def test_hip_graph_replay_matches_eager(model):
             model.use_hip_graphs = False
             model._graphs.clear()
             model._graph_ws.clear()
+
+
+@pytest.mark.parametrize("arch", ["gigapath_slide_enc24l1024d", "gigapath_slide_enc12l1536d"])
+def test_other_registered_archs_vs_oracle(arch):
+    """24L1024d (D = 64) and 12L1536d (D = 96) end to end against the fp32 oracle."""
+    from gigapath import slide_encoder
+    cfg = orc.arch_config(arch)
+    m = slide_encoder.create_model("", arch, 1536)
+    W = orc.make_weights(cfg, seed=0)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()}, strict=True)
+    m = m.to(DEV).eval()
+    x, coords = orc.synthetic_slide(700)
+    with torch.no_grad():
+        got = torch.stack(m(torch.from_numpy(x).to(DEV), torch.from_numpy(coords).to(DEV),
+                            all_layer_embed=True)).cpu().numpy()
+    Wt = {k: torch.from_numpy(v) for k, v in W.items()}
+    ref = torch.stack(orc.slide_encoder_forward(Wt, x, coords, cfg, all_layer_embed=True)).numpy()
+    for idx in np.ndindex(*got.shape[:-1]):
+        rel, cos, ok = close_enough(got[idx], ref[idx])
+        assert ok, (arch, idx, rel, cos)
+
+
+def test_classification_head_logits(model):
+    from gigapath import classification_head
+    head = classification_head.ClassificationHead(1536, 768, "0-6-12", n_classes=4, pretrained="")
+    head.slide_encoder.load_state_dict(model.state_dict())
+    head = head.to(DEV)
+    x, coords = orc.synthetic_slide(900)
+    xt, ct = torch.from_numpy(x).to(DEV), torch.from_numpy(coords).to(DEV)
+    logits = head(xt, ct)
+    assert logits.shape == (1, 4) and logits.requires_grad
+    with torch.no_grad():
+        emb = model(xt, ct, all_layer_embed=True)
+        want = head.classifier(torch.cat([emb[0], emb[6], emb[12]], -1))
+    assert torch.allclose(logits.detach(), want, atol=1e-5)
+    logits.sum().backward()                          # the classifier trains on frozen features
+    assert head.classifier[0].weight.grad is not None
