@@ -16,6 +16,7 @@
 //   * the reference's zero-padded keys (dilated_attention.py:85-91, unmasked in flash-attn)
 //     are added analytically at the end: n_pad * exp(0 - max) in the denominator.
 #include <math.h>
+#include <type_traits>
 #include <stdlib.h>
 
 #include "gp_api.h"
@@ -341,7 +342,9 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
   static_assert(NW == 4 || NW == 8, "");
   constexpr int NT = NW * 64;                // threads
   constexpr int QB = NW * 32;                // query rows per workgroup
-  constexpr int KT = 16 * NW;                // keys per staged tile (64 or 128): 3 chunks / thread
+  // keys per staged tile: 16*NW (3 chunks / thread), or 64 with VAR & 512 (8 waves sharing one
+  // 64-key tile: 256 queries per K/V load)
+  constexpr int KT = ((VAR & 512) != 0) ? 64 : 16 * NW;
   constexpr int KS = D / 16;                 // k-steps of Q.K^T
   constexpr bool kOnes = (D % 32) != 0;      // spare d rows carry the row-sum ones
   constexpr bool kMK = (VAR & 8) != 0;       // running max in an extra k-step
@@ -353,8 +356,9 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
   constexpr int VTILE = KT * VROWB;
   constexpr int BUF = KTILE + VTILE;
   constexpr int CH = D / 8;                  // 16-byte chunks per K/V row in HBM
-  constexpr int LPT = 2 * KT * CH / NT;
-  static_assert((2 * KT * CH) % NT == 0, "");
+  constexpr int TOT = 2 * KT * CH;           // 16-byte chunks of one K tile + one V tile
+  constexpr int LPT = (TOT + NT - 1) / NT;
+  static_assert(TOT % NT == 0 || (VAR & 2) != 0, "uneven chunk split needs VAR & 2");
   constexpr float kThr = 8.0f;               // lazy-rescale threshold (log2 units)
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
 
@@ -416,7 +420,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
   if constexpr ((VAR & 2) != 0) {
 #pragma unroll
     for (int u = 0; u < LPT; ++u) {
-      const int idx = threadIdx.x + NT * u;
+      const int idx = (threadIdx.x + NT * u) % TOT;   // (an out-of-range chunk repeats a valid one)
       const int tsel = idx / (KT * CH);
       const int rem = idx % (KT * CH);
       const int row = rem / CH, ch = rem % CH;
@@ -430,12 +434,14 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
       const int64_t toff = (int64_t)kv0 * kvstride;      // wave-uniform
       if (kv0 + KT <= c) {                                // full tile: no per-key bound checks
 #pragma unroll
-        for (int u = 0; u < LPT; ++u) stage[u] = *reinterpret_cast<const uint4*>(lsrc[u] + toff);
+        for (int u = 0; u < LPT; ++u)
+          if (TOT % NT == 0 || threadIdx.x + NT * u < TOT) stage[u] = *reinterpret_cast<const uint4*>(lsrc[u] + toff);
       } else {
 #pragma unroll
         for (int u = 0; u < LPT; ++u) {
           uint4 z = make_uint4(0, 0, 0, 0);
-          if (kv0 + lrow[u] < c) z = *reinterpret_cast<const uint4*>(lsrc[u] + toff);
+          if (kv0 + lrow[u] < c && (TOT % NT == 0 || threadIdx.x + NT * u < TOT))
+            z = *reinterpret_cast<const uint4*>(lsrc[u] + toff);
           stage[u] = z;
         }
       }
@@ -458,6 +464,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
     for (int u = 0; u < LPT; ++u) {
       int off;
       if constexpr ((VAR & 2) != 0) {
+        if (TOT % NT != 0 && threadIdx.x + NT * u >= TOT) continue;
         off = loff[u];
       } else {
         const int idx = threadIdx.x + NT * u;
@@ -482,21 +489,57 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
     for (int r = 0; r < 16; ++r) oacc[mt][r] = 0.f;
 
   const int ntiles = (c + KT - 1) / KT;
+  // VAR & 1024: prefetch distance 2 -- two register stage sets (tile t+2 loads while tile t+1
+  // waits in the other set), the loop unrolled by 2 so each set is a compile-time choice
+  constexpr bool kPF2 = (VAR & 1024) != 0;
+  static_assert(!kPF2 || (VAR & 2) != 0, "VAR 1024 builds on VAR 2");
+  uint4 stage2[kPF2 ? 2 : 1][LPT];
+  auto load_into = [&](uint4 (&st)[LPT], int kv0) {
+    const int64_t toff = (int64_t)kv0 * kvstride;
+#pragma unroll
+    for (int u = 0; u < LPT; ++u) {
+      uint4 z = make_uint4(0, 0, 0, 0);
+      if (kv0 + lrow[u] < c && (TOT % NT == 0 || threadIdx.x + NT * u < TOT))
+        z = *reinterpret_cast<const uint4*>(lsrc[u] + toff);
+      st[u] = z;
+    }
+  };
+  auto store_from = [&](const uint4 (&st)[LPT], int buf) {
+#pragma unroll
+    for (int u = 0; u < LPT; ++u) {
+      if (TOT % NT != 0 && threadIdx.x + NT * u >= TOT) continue;
+      *reinterpret_cast<uint4*>(smem + buf * BUF + loff[u]) = st[u];
+    }
+  };
   if (ntiles > 0) {
-    load_tile(0);
-    store_tile(0);
+    if constexpr (kPF2) {
+      load_into(stage2[0], 0);
+      store_from(stage2[0], 0);
+      if (ntiles > 1) load_into(stage2[1], KT);
+    } else {
+      load_tile(0);
+      store_tile(0);
+    }
   }
   __syncthreads();
 
-  for (int t = 0; t < ntiles; ++t) {
-    if (t + 1 < ntiles) load_tile((t + 1) * KT);
+  auto tile_step = [&](int t, auto setc) {
+    constexpr int SET = decltype(setc)::value;
+    (void)SET;
+    // VAR 128/256/64: timing-only ablations (wrong results): no K/V streaming after tile 0 /
+    // no barrier / no exp
+    if constexpr (kPF2) {
+      if (t + 2 < ntiles) load_into(stage2[SET], (t + 2) * KT);
+    } else {
+      if (t + 1 < ntiles && (VAR & 128) == 0) load_tile((t + 1) * KT);
+    }
 #pragma unroll
     for (int hf = 0; hf < KT / 64; ++hf) {
       // 64-key sub-tile; a sub-tile past c (only in the last tile) is fully masked: p = 0
       const int sub = t * (KT / 64) + hf;
       const int kv0 = sub * 64;
-      const char* Kb = smem + (t & 1) * BUF + hf * 64 * KROWB;
-      const char* Vb = smem + (t & 1) * BUF + KTILE + hf * 64 * VROWB;
+      const char* Kb = smem + (((VAR & 128) != 0) ? 0 : (t & 1)) * BUF + hf * 64 * KROWB;
+      const char* Vb = smem + (((VAR & 128) != 0) ? 0 : (t & 1)) * BUF + KTILE + hf * 64 * VROWB;
       // ---- S^T for two 32-key sub-tiles.  kPre (q pre-multiplied by scale*log2 e): the
       // accumulator starts at -m_run, so it already holds log2-domain scores minus the max.
       f32x16 sacc[2];
@@ -607,7 +650,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
           for (int s = 0; s < 2; ++s)
   #pragma unroll
             for (int e = 0; e < 8; ++e) {
-              const float p = fast_exp2(sacc[u][8 * s + e]);
+              const float p = (VAR & 64) ? sacc[u][8 * s + e] : fast_exp2(sacc[u][8 * s + e]);
               if constexpr (!kOnes) lsum += p;
               pf[u][s][e] = (__bf16)p;
             }
@@ -657,8 +700,20 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
       if constexpr ((VAR & 32) != 0) __builtin_amdgcn_s_setprio(0);
     }
 
-    if (t + 1 < ntiles) store_tile((t + 1) & 1);
-    __syncthreads();
+    if constexpr (kPF2) {
+      if (t + 1 < ntiles) store_from(stage2[1 - SET], (t + 1) & 1);
+    } else {
+      if (t + 1 < ntiles && (VAR & 128) == 0) store_tile((t + 1) & 1);
+    }
+    if constexpr ((VAR & 256) == 0) __syncthreads();
+    };
+  if constexpr (kPF2) {
+    for (int t = 0; t < ntiles; t += 2) {
+      tile_step(t, std::integral_constant<int, 0>());
+      if (t + 1 < ntiles) tile_step(t + 1, std::integral_constant<int, 1>());
+    }
+  } else {
+    for (int t = 0; t < ntiles; ++t) tile_step(t, std::integral_constant<int, 0>());
   }
 
   // ---- epilogue
@@ -1170,9 +1225,9 @@ extern "C" int gp_dilated_attn_fwd_ex(const uint16_t* q, int64_t q_row_stride, i
   GP_REQUIRE(impl == 1 || impl == 2 || impl == 3, "gp_dilated_attn_fwd: GP_ATTN_IMPL must be 1, 2 or 3");
   GP_REQUIRE(impl != 3 || q_log2_prescaled, "gp_dilated_attn_fwd: GP_ATTN_IMPL=3 needs q_log2_prescaled");
   GP_REQUIRE(!q_log2_prescaled || impl != 1, "gp_dilated_attn_fwd: q_log2_prescaled needs D in {48, 64}");
-  const int qblk = 128;                            // query rows per workgroup (both kernels)
   const char* var_env = getenv("GP_ATTN_VAR");
   const int var = var_env ? atoi(var_env) : 0;
+  const int qblk = (impl == 2 && var >= 512 && (var & 512)) ? 256 : 128;   // query rows per workgroup
   // order branches by keys per work item (descending) so the longest items start first
   int order[GP_MAX_BRANCHES];
   GpBranch geo[GP_MAX_BRANCHES];
@@ -1252,6 +1307,14 @@ extern "C" int gp_dilated_attn_fwd_ex(const uint16_t* q, int64_t q_row_stride, i
       case 15: dilated_attn32_kernel<48, true, 4, 7, 4><<<(unsigned)items, 256, 0, s>>>(a); break;
       case 10: dilated_attn32_kernel<48, true, 4, 10><<<(unsigned)items, 256, 0, s>>>(a); break;
       case 14: dilated_attn32_kernel<48, true, 4, 14><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 66: dilated_attn32_kernel<48, true, 4, 66><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 130: dilated_attn32_kernel<48, true, 4, 130><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 258: dilated_attn32_kernel<48, true, 4, 258><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 386: dilated_attn32_kernel<48, true, 4, 386><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 450: dilated_attn32_kernel<48, true, 4, 450><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 514: dilated_attn32_kernel<48, true, 8, 514><<<(unsigned)items, 512, 0, s>>>(a); break;
+      case 1538: dilated_attn32_kernel<48, true, 8, 1538><<<(unsigned)items, 512, 0, s>>>(a); break;
+      case 1026: dilated_attn32_kernel<48, true, 4, 1026><<<(unsigned)items, 256, 0, s>>>(a); break;
       case 34: dilated_attn32_kernel<48, true, 4, 34><<<(unsigned)items, 256, 0, s>>>(a); break;
       case 26: dilated_attn32_kernel<48, true, 4, 10, 4><<<(unsigned)items, 256, 0, s>>>(a); break;
       case 30: dilated_attn32_kernel<48, true, 4, 14, 4><<<(unsigned)items, 256, 0, s>>>(a); break;

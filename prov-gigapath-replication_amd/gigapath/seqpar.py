@@ -22,9 +22,9 @@ replacement for arbitrary shard boundaries:
   of the left neighbour: a small "q halo" of whole qkv rows goes by point-to-point.
 * **Compute.**  ``gp_dilated_attn_fwd_ex`` computes exactly the sparse rows whose dense slot lies
   in [a_v, b_v) (query window), reading q from the local (halo-extended) qkv buffer and K/V from
-  the received buffers.  The short-segment branches (segments shorter than a shard: halo-only
-  exchange) are exchanged first and their attention runs while the long-segment branches'
-  all-to-alls are still in flight (overlap).  ``gp_branch_merge_ln_window`` merges the window.
+  the received buffers.  Exchanges run in three phases -- short segments (halo-only), segments
+  spanning several shards, whole-sequence segments -- and each phase's attention runs while the
+  next phase's all-to-alls are in flight.  ``gp_branch_merge_ln_window`` merges the window.
 
 Per-query math is identical to the single-device kernel, so SP output equals the 1-GPU
 output up to the GEMMs' row-count-dependent kernel choice.  Inference only, B = 1.
@@ -123,10 +123,16 @@ class ShardPlan:
         # K/V gather range each rank's queries need, per branch (= its receive buffer)
         self.need = [[self._kv_need(w, b) for b in range(nb)] for w in range(world)]
         self.q_halo = [max(0, max(self._q_halo(w, b) for b in range(nb))) for w in range(world)]
-        # exchange phases: short segments (halo-only traffic) first, then the long ones
+        # exchange phases, each one's attention overlapping the next one's transfer: short segments
+        # (halo-only traffic) first, then segments spanning several shards, then the branches
+        # whose one segment is the whole sequence (every rank needs every token's rows)
         shard = L / world
         self.phase_a = [b for b in range(nb) if self.geo[b].s < shard]
-        self.phase_b = [b for b in range(nb) if b not in self.phase_a]
+        self.phase_b1 = [b for b in range(nb) if b not in self.phase_a and self.geo[b].nseg > 1]
+        self.phase_b2 = [b for b in range(nb) if b not in self.phase_a and self.geo[b].nseg == 1]
+        if not self.phase_b1:                      # nothing in the middle: keep two phases
+            self.phase_b1, self.phase_b2 = self.phase_b2, []
+        self.phase_b = self.phase_b1 + self.phase_b2
 
     # ---- geometry of one rank
     def _kv_need(self, w: int, b: int) -> Tuple[int, int]:
@@ -392,7 +398,7 @@ class SeqParallelEngine:
                 self.sparsify(ws)
 
             def tail(pa=pa, pl=pl, nxt=nxt):
-                self.attention(pa, ws, plan.phase_b)
+                self.attention(pa, ws, plan.phase_b2 if plan.phase_b2 else plan.phase_b1)
                 with runtime.TIMER.span("merge"):
                     _hip.branch_merge_ln_window(ws.attn.outs, ws.attn.lses, plan.segs, plan.ratios, 1, plan.L, a, M,
                                                 H, D, pa.ln_w, pa.ln_b, pa.ln_eps, ws.a)
@@ -412,10 +418,14 @@ class SeqParallelEngine:
 
             self._segment(("head", li, wsig), head)
             h_a = self.exchange(ws, plan.phase_a, halo=True)
-            h_b = self.exchange(ws, plan.phase_b, halo=False)
+            h_b1 = self.exchange(ws, plan.phase_b1, halo=False)
+            h_b2 = self.exchange(ws, plan.phase_b2, halo=False)
             Exchange.wait(h_a)
             self.attention(pa, ws, plan.phase_a)
-            Exchange.wait(h_b)
+            Exchange.wait(h_b1)
+            if plan.phase_b2:                      # the middle phase runs while the last transfers
+                self.attention(pa, ws, plan.phase_b1)
+            Exchange.wait(h_b2)
             self._segment(("tail", li, wsig), tail)
             if layer_hook is not None:
                 layer_hook(li + 1)
