@@ -89,6 +89,9 @@ def pmc_traffic(n_tiles, kernel):
 
 
 def main():
+    if os.environ.get("GP_BENCH_TRACE_AFTER"):           # debugging aid: dump every thread's stack
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["GP_BENCH_TRACE_AFTER"]), exit=True)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -98,6 +101,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--mode", choices=["sp", "replica", "mixed"], default="sp")
     ap.add_argument("--timing-steps", type=int, default=2, help="eager steps with per-kernel HIP events")
+    ap.add_argument("--mixed-slides", type=int, default=32, help="--mode mixed: slides in the batch")
     ap.add_argument("--no-graphs", action="store_true", help="eager launches instead of HIP graph replay")
     args = ap.parse_args()
 
@@ -131,7 +135,7 @@ def main():
     model.use_hip_graphs = not args.no_graphs
     if mixed:
         from gigapath import batch
-        sizes = batch.mixed_batch_sizes()
+        sizes = batch.mixed_batch_sizes(n_slides=args.mixed_slides)
         slides = []
         for i, n in enumerate(sizes):
             x, coords = make_slide(n, seed=100 + 2 * i)

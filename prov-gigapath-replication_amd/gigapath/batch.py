@@ -49,7 +49,12 @@ def encode_slides(model, slides: Sequence[Tuple[torch.Tensor, torch.Tensor]], al
     Single process: sequential B = 1 forwards.  Under torch.distributed (one process per GPU,
     every rank passing the same list): LPT-sharded across the ranks of `group`, results
     all-reduced so every rank returns every slide's outputs.  Returns, per slide, the list the
-    model's forward returns (1 or 1 + depth tensors of [1, E])."""
+    model's forward returns (1 or 1 + depth tensors of [1, E]).
+
+    With ``model.use_hip_graphs`` each slide is a replay of its shape's captured forward.  The
+    replays run one after another on one stream: replaying graphs of different slides concurrently
+    on several streams hung the GPU on MI355X (32 slides over 4 streams; GEMM kernels that assume
+    their workgroups are co-resident are the suspect), so there is no cross-slide concurrency."""
     import torch.distributed as dist
     if getattr(model, "_sp", None) is not None:
         raise ValueError("encode_slides is data parallel: call model.disable_sequence_parallel() first")
@@ -66,11 +71,16 @@ def encode_slides(model, slides: Sequence[Tuple[torch.Tensor, torch.Tensor]], al
     E = model.embed_dim
     dev = model.cls_token.device
     table = torch.zeros(len(slides), n_out, E, dtype=torch.float32, device=dev)
+
+    def shaped(i):
+        x, c = slides[i]
+        x = x if x.dim() == 3 else x.unsqueeze(0)
+        c = c if c.dim() == 3 else c.unsqueeze(0)
+        return x, (c if c.dtype in (torch.float32, torch.float64) else c.float())
+
     with torch.no_grad():
         for i in mine:
-            x, c = slides[i]
-            x = x if x.dim() == 3 else x.unsqueeze(0)
-            c = c if c.dim() == 3 else c.unsqueeze(0)
+            x, c = shaped(i)
             outs = encode_fn(x, c)
             table[i] = torch.stack([o.reshape(E).float() for o in outs])
     if world > 1:
@@ -88,3 +98,4 @@ def mixed_batch_sizes(n_slides: int = 32, lo: int = 2000, hi: int = 100000, seed
     """C5's slide sizes: N_i = round(exp(U(ln lo, ln hi))) from PCG64(seed)."""
     rng = np.random.Generator(np.random.PCG64(seed))
     return [int(round(float(np.exp(u)))) for u in rng.uniform(np.log(lo), np.log(hi), n_slides)]
+

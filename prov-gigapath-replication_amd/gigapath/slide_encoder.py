@@ -90,6 +90,7 @@ class LongNetViT(nn.Module):
         self.max_hip_graphs = 64
         self._graphs = {}
         self._graph_ws = {}
+        self._capture_streams = {}
         self.initialize_vit_weights()
 
     # ---------------------------------------------------------------- sequence parallel
@@ -190,44 +191,61 @@ class LongNetViT(nn.Module):
         captured on first use per (shape, dtypes, options, weights version), inputs copied into the
         graph's static buffers, outputs cloned out.  Coordinates are validated eagerly first (one
         small kernel + one sync, as in the eager path)."""
-        dev = self.cls_token.device
-        B, N, C = x.shape
         c = coords if coords.dtype in (torch.float32, torch.float64) else coords.float()
         if self.validate_positions:
-            pos = torch.empty(B * N, dtype=torch.int64, device=dev)
-            err = torch.zeros(1, dtype=torch.int32, device=dev)
+            self.check_positions([c])
+        graph, sx, sc, outs = self.graph_entry(x, c, all_layer_embed)
+        sx.copy_(x)
+        sc.copy_(c)
+        graph.replay()
+        return [o.clone() for o in outs]
+
+    def check_positions(self, coords_list):
+        """Raise IndexError if any tile of any slide maps outside pos_embed (reference :200 indexing);
+        one small kernel per slide, one host sync for all of them."""
+        dev = self.cls_token.device
+        err = torch.zeros(1, dtype=torch.int32, device=dev)
+        for c in coords_list:
+            pos = torch.empty(c.numel() // 2, dtype=torch.int64, device=dev)
             _hip.coords_to_pos(c.contiguous(), self.slide_ngrids, self.tile_size, pos, err)
-            if int(err.item()) > 0:
-                raise IndexError("coords map outside pos_embed (%d rows): %d tiles" %
-                                 (self.slide_ngrids ** 2 + 1, int(err.item())))
+        if int(err.item()) > 0:
+            raise IndexError("coords map outside pos_embed (%d rows): %d tiles" %
+                             (self.slide_ngrids ** 2 + 1, int(err.item())))
+
+    def graph_stream(self):
+        """The side stream graphs are captured on (one per device)."""
+        dev = self.cls_token.device
+        if str(dev) not in self._capture_streams:
+            self._capture_streams[str(dev)] = torch.cuda.Stream(device=dev)
+        return self._capture_streams[str(dev)]
+
+    def graph_entry(self, x, c, all_layer_embed):
+        """(graph, static x, static coords, static outputs) for this input shape, captured if not
+        cached.  No validation, no replay."""
+        dev = self.cls_token.device
         self._packed_top(dev)
         self.encoder.engine.pack(self.encoder, dev)
         key = (str(dev), tuple(x.shape), x.dtype, c.dtype, bool(all_layer_embed), bool(self.global_pool),
                self._top_sig, self.encoder.engine._sig)
         ent = self._graphs.get(key)
         if ent is None:
-            ent = self._capture(key, x, c, all_layer_embed)
-        graph, sx, sc, outs = ent
-        sx.copy_(x)
-        sc.copy_(c)
-        graph.replay()
-        return [o.clone() for o in outs]
+            ent = self._capture(key, x, c, all_layer_embed, self.graph_stream())
+        return ent
 
-    def _capture(self, key, x, c, all_layer_embed):
+    def _capture(self, key, x, c, all_layer_embed, stream):
         while len(self._graphs) >= self.max_hip_graphs:          # oldest first (insertion order)
             old = next(iter(self._graphs))
             self._graphs.pop(old)
             self._graph_ws.pop(old, None)
         sx, sc = x.detach().clone(), c.detach().clone().contiguous()
         cur = torch.cuda.current_stream()
-        side = torch.cuda.Stream(device=sx.device)
-        side.wait_stream(cur)
-        with torch.cuda.stream(side):                             # warm-up: allocations, TunableOp lookups
+        stream.wait_stream(cur)
+        with torch.cuda.stream(stream):                           # warm-up: allocations, TunableOp lookups
             self._forward_device(sx, sc, all_layer_embed, False)
-        cur.wait_stream(side)
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
+        with torch.cuda.graph(graph, stream=stream, capture_error_mode="thread_local"):
             outs = self._forward_device(sx, sc, all_layer_embed, False)
+        cur.wait_stream(stream)
         # the graph bakes this shape's workspace: keep it alive with the graph
         ent = (graph, sx, sc, outs)
         self._graphs[key] = ent
