@@ -350,6 +350,11 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
   constexpr bool kMK = (VAR & 8) != 0;       // running max in an extra k-step
   static_assert(!kMK || (D == 48 && kPre), "VAR 8 needs D = 48 and a pre-scaled q");
   constexpr int KSS = kMK ? KS + 1 : KS;     // k-steps of S
+  // VAR & 4096: the -m_run start block of S comes from ONE extra MFMA per 64-key sub-tile,
+  // [1, 0 ...] (A) x [-m_run, 0 ...] (B) with C = 0, instead of 16 v_mov per sub-tile (the loop
+  // is VALU-issue bound; the MFMA pipe has slack); m_run kept bf16-exact as with VAR 8
+  constexpr bool kMI = (VAR & 4096) != 0;
+  static_assert(!kMI || (D == 48 && kPre && !kMK && (VAR & 1) == 0), "VAR 4096 needs D = 48, kPre, no VAR 8/1");
   constexpr int KROWB = (kMK ? 64 : D) * 2 + 16;   // K image row bytes (padded)
   constexpr int VROWB = 128;                 // V image row bytes (64 bf16, swizzled 32-B blocks)
   constexpr int KTILE = KT * KROWB;
@@ -429,8 +434,32 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
       loff[u] = tsel ? KTILE + row * VROWB + 32 * ((ch >> 1) ^ (row & 3)) + 16 * (ch & 1) : row * KROWB + ch * 16;
     }
   }
+  // VAR & 2048: byte offset of every staging chunk from the K row of key 0 (V chunks at kv_dv)
+  const int64_t kv_dv = (int64_t)((const char*)vbase - (const char*)kbase);
+  int lvo[LPT];
+  if constexpr ((VAR & 2048) != 0) {
+#pragma unroll
+    for (int u = 0; u < LPT; ++u) {
+      const int idx = (threadIdx.x + NT * u) % TOT;
+      const int tsel = idx / (KT * CH);
+      const int rem = idx % (KT * CH);
+      lvo[u] = (int)(tsel * kv_dv + (int64_t)(rem / CH) * kvstride * 2 + (rem % CH) * 16);
+    }
+  }
   auto load_tile = [&](int kv0) {
-    if constexpr ((VAR & 2) != 0) {
+    if constexpr ((VAR & 2048) != 0) {
+      // buffer loads through a per-tile descriptor whose record count ends at the last valid key
+      // row: rows past c read as zero in hardware (no branch, no zero-filled stage registers,
+      // so the compiler has no reason to wait on the loads before the tile's compute)
+      const int64_t tb = (int64_t)kv0 * kvstride * 2;                    // bytes, wave-uniform
+      const int64_t nrec = (int64_t)(c - kv0 - 1) * kvstride * 2 + kv_dv + 2 * D;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)((const char*)kbase + tb), (short)0, (int)(nrec < 0x7fffffff ? nrec : 0x7fffffff), 0x00020000);
+#pragma unroll
+      for (int u = 0; u < LPT; ++u)
+        if (TOT % NT == 0 || threadIdx.x + NT * u < TOT)
+          stage[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, lvo[u], 0, 0));
+    } else if constexpr ((VAR & 2) != 0) {
       const int64_t toff = (int64_t)kv0 * kvstride;      // wave-uniform
       if (kv0 + KT <= c) {                                // full tile: no per-key bound checks
 #pragma unroll
@@ -477,6 +506,10 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
     }
   };
 
+  bf16x8 onesA = {}, mqB = {};    // kMI operands
+  if constexpr (kMI) {
+    if (h == 0) onesA[0] = (__bf16)1.0f;
+  }
   float m_run = -INFINITY;   // running max, log2 domain, of query l32
   float lsum = 0.f;          // row sum (VALU path, D % 32 == 0 only)
   f32x16 minit;              // kPre: -m_run (0 before the first tile); else 0
@@ -493,6 +526,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
   // waits in the other set), the loop unrolled by 2 so each set is a compile-time choice
   constexpr bool kPF2 = (VAR & 1024) != 0;
   static_assert(!kPF2 || (VAR & 2) != 0, "VAR 1024 builds on VAR 2");
+  static_assert((VAR & 2048) == 0 || (VAR & 2) != 0, "VAR 2048 builds on VAR 2");
   uint4 stage2[kPF2 ? 2 : 1][LPT];
   auto load_into = [&](uint4 (&st)[LPT], int kv0) {
     const int64_t toff = (int64_t)kv0 * kvstride;
@@ -522,6 +556,11 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
     }
   }
   __syncthreads();
+  // every vector load so far (Q fragments, tile 0) is complete here; saying so with a real
+  // s_waitcnt (vmcnt 0) lets the compiler's wait insertion drop its "Q may still be in flight"
+  // state at the loop head, which otherwise forces vmcnt(0) -- a wait on the next tile's
+  // prefetch -- before the first MFMA of every tile
+  __builtin_amdgcn_s_waitcnt(0x0f70);
 
   auto tile_step = [&](int t, auto setc) {
     constexpr int SET = decltype(setc)::value;
@@ -546,6 +585,13 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
       // VAR & 1: the first k-step takes its C operand from minit (= -m_run in every element, kept
       // in its own registers, rewritten only on a rescale) instead of initialising per tile
       const float init = (kPre && sub > 0) ? -m_run : 0.f;
+      f32x16 ini;
+      if constexpr (kMI) {
+        f32x16 zero;
+  #pragma unroll
+        for (int r = 0; r < 16; ++r) zero[r] = 0.f;
+        ini = __builtin_amdgcn_mfma_f32_32x32x16_bf16(onesA, mqB, zero, 0, 0, 0);
+      }
       bf16x8 kf[2][KSS];
       if constexpr ((VAR & 4) != 0) {      // all K fragments first: one LDS wait, not one per MFMA
   #pragma unroll
@@ -558,7 +604,9 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
   #pragma unroll
       for (int u = 0; u < 2; ++u) {
         f32x16 acc;
-        if constexpr (kMK) {
+        if constexpr (kMI) {
+          acc = ini;
+        } else if constexpr (kMK) {
   #pragma unroll
           for (int r = 0; r < 16; ++r) acc[r] = 0.f;
         } else if constexpr ((VAR & 1) == 0) {
@@ -605,7 +653,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
         // (tile 0: always, which sets m_run to that tile's exact max)
         const bool need = (sub == 0) || (mx > kThr);
         if (__builtin_amdgcn_ballot_w64(need)) {
-          if constexpr (kMK) {
+          if constexpr (kMK || kMI) {
             // m stays exactly representable in bf16 (it enters the MFMA through q); the shift
             // applied is the rounded one, so numerator and denominator stay consistent
             const float m_old = (sub == 0) ? 0.f : m_run;
@@ -624,7 +672,11 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
             for (int u = 0; u < 2; ++u)
   #pragma unroll
               for (int r = 0; r < 16; ++r) sacc[u][r] -= d;
-            if (h == 0) qf[KS][0] = (__bf16)(-m_run);
+            if constexpr (kMK) {
+              if (h == 0) qf[KS][0] = (__bf16)(-m_run);
+            } else {
+              if (h == 0) mqB[0] = (__bf16)(-m_run);
+            }
           } else {
             const float delta = need ? mx : 0.f;
             const float alpha = fast_exp2(-delta);
@@ -749,6 +801,317 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
         }
       }
     if (h == 0) br.lse[((int64_t)bn * a.H + hh) * g.m + i] = (mr + __builtin_amdgcn_logf(l)) * 0.69314718055994530942f;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// v4 (D = 48, q pre-scaled): the v2 math with TWO 32-query blocks per wave (64 queries, 256 per
+// workgroup).  Every K fragment (ds_read_b128) and V^T fragment (2 x ds_read_b64_tr_b16) read
+// from LDS feeds two MFMAs, and a staged 64-key tile serves 256 queries: half the LDS reads
+// and writes (and half the K/V fetches) per FLOP of v2.  K/V tiles are staged with buffer loads
+// through a per-tile descriptor whose record count ends at the last valid key row, so rows past
+// c read as zero in hardware (no branch, no zero-filled registers).  Two waves per SIMD.
+// WV bits (A/B): 1 = all six K fragments read before the S MFMAs; 2 = one rescale decision (and
+// branch) for both query blocks, so the exps of both blocks and the PV MFMAs share one block.
+template <int NW, int WV = 0>
+__global__ __launch_bounds__(NW * 64, 2) void dilated_attn_w64_kernel(const AttnArgs a) {
+  constexpr int D = 48;
+  constexpr int NT = NW * 64;
+  constexpr int QB = NW * 64;                // query rows per workgroup
+  constexpr int KT = 64;                     // keys per staged tile
+  constexpr int KS = D / 16;
+  constexpr int KROWB = D * 2 + 16;          // K image row bytes (16-B pad: conflict-free b128 reads)
+  constexpr int VROWB = 128;                 // V image row: 64 bf16 (48 values + 16 ones), swizzled blocks
+  constexpr int KTILE = KT * KROWB;
+  constexpr int VTILE = KT * VROWB;
+  constexpr int BUF = KTILE + VTILE;
+  constexpr int CH = D / 8;
+  constexpr int TOT = 2 * KT * CH;           // 16-byte chunks of one K tile + one V tile
+  constexpr int LPT = (TOT + NT - 1) / NT;
+  constexpr float kThr = 8.0f;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+
+  WorkItem wi;
+  decode_item(a, (int)xcd_group(blockIdx.x, gridDim.x), wi);
+  const GpBranch g = a.br[wi.bi].g;
+  const int hh = wi.hh, c = wi.c, bn = wi.bn;
+  const int rows_needed = wi.i_hi;
+  const int q0 = wi.i_lo + wi.qb * QB;
+  if (q0 >= rows_needed) return;
+  const int qvalid = c < rows_needed ? c : rows_needed;
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int l32 = lane & 31, h = lane >> 5;
+  const AttnBranch& brr = a.br[wi.bi];
+  const int64_t tok0 = (int64_t)wi.bidx * a.L + (int64_t)wi.n * g.s + wi.j;
+  const int64_t qstride = (int64_t)g.r * a.q_stride;
+  const int64_t kvstride = (int64_t)g.r * brr.kv_stride;
+  const int kcol = brr.kv_sparse ? (hh % g.hpg) * D : hh * D;
+  const uint16_t* qbase = a.q + (tok0 - a.q_tok_base) * a.q_stride + hh * D;
+  const uint16_t* kbase = brr.k + (tok0 - brr.kv_tok_base) * brr.kv_stride + kcol;
+  const int64_t kv_dv = (int64_t)((const char*)(brr.v + (tok0 - brr.kv_tok_base) * brr.kv_stride + kcol) -
+                                  (const char*)kbase);
+
+  // V images: d-columns 48..63 of every row hold bf16 1.0 (the MFMA then yields the row sum)
+  for (int idx = threadIdx.x; idx < 2 * KT * 2; idx += NT) {
+    const int buf = idx / (2 * KT), rem = idx % (2 * KT), row = rem >> 1, half = rem & 1;
+    const uint4 ones = make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
+    *reinterpret_cast<uint4*>(smem + buf * BUF + KTILE + row * VROWB + 32 * (3 ^ (row & 3)) + 16 * half) = ones;
+  }
+
+  // Q fragments of both query blocks: lane holds Q[q = l32][d = 16ks + 8h .. +7]
+  bf16x8 qf[2][KS];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int i = q0 + w * 64 + qb * 32 + l32;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      bf16x8 z = {};
+      if (i < qvalid) z = *reinterpret_cast<const bf16x8*>(qbase + (int64_t)i * qstride + 16 * ks + 8 * h);
+      qf[qb][ks] = z;
+    }
+  }
+
+  // staging chunks: byte offset from key 0's K row (V chunks at kv_dv) and LDS offset
+  int lvo[LPT], loff[LPT];
+#pragma unroll
+  for (int u = 0; u < LPT; ++u) {
+    const int idx = (threadIdx.x + NT * u) % TOT;
+    const int tsel = idx / (KT * CH);
+    const int rem = idx % (KT * CH);
+    const int row = rem / CH, ch = rem % CH;
+    lvo[u] = (int)(tsel * kv_dv + (int64_t)row * kvstride * 2 + ch * 16);
+    loff[u] = tsel ? KTILE + row * VROWB + 32 * ((ch >> 1) ^ (row & 3)) + 16 * (ch & 1) : row * KROWB + ch * 16;
+  }
+  uint4 stage[LPT];
+  auto load_tile = [&](int kv0) {
+    const int64_t tb = (int64_t)kv0 * kvstride * 2;
+    const int64_t nrec = (int64_t)(c - kv0 - 1) * kvstride * 2 + kv_dv + 2 * D;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((const char*)kbase + tb), (short)0, (int)(nrec < 0x7fffffff ? nrec : 0x7fffffff), 0x00020000);
+#pragma unroll
+    for (int u = 0; u < LPT; ++u)
+      if (TOT % NT == 0 || threadIdx.x + NT * u < TOT)
+        stage[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, lvo[u], 0, 0));
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < LPT; ++u) {
+      if (TOT % NT != 0 && threadIdx.x + NT * u >= TOT) continue;
+      *reinterpret_cast<uint4*>(smem + buf * BUF + loff[u]) = stage[u];
+    }
+  };
+
+  float m_run[2] = {0.f, 0.f};   // running max (log2 domain) of query l32 of each block
+  f32x16 oacc[2][2];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) oacc[qb][mt][r] = 0.f;
+
+  // WV & 4: persistent C blocks holding -m_run of each query block (0 before the first tile):
+  // S's first k-step reads them, so no per-tile accumulator initialisation
+  f32x16 minit[2];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) minit[qb][r] = 0.f;
+  const int ntiles = (c + KT - 1) / KT;
+  if (ntiles > 0) {
+    load_tile(0);
+    store_tile(0);
+  }
+  __syncthreads();
+  __builtin_amdgcn_s_waitcnt(0x0f70);    // vmcnt(0): see dilated_attn32_kernel
+
+  for (int t = 0; t < ntiles; ++t) {
+    if (t + 1 < ntiles) load_tile((t + 1) * KT);
+    const int kv0 = t * KT;
+    const char* Kb = smem + (t & 1) * BUF;
+    const char* Vb = Kb + KTILE;
+    // ---- S^T = K.Q^T for 2 key halves x 2 query blocks; accumulators start at -m_run
+    f32x16 sacc[2][2];
+    if constexpr ((WV & 4) == 0) {
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        const float init = (t > 0) ? -m_run[qb] : 0.f;
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) sacc[qb][u][r] = init;
+      }
+    }
+    bf16x8 kf[2][KS];
+    if constexpr ((WV & 1) != 0) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+          kf[u][ks] = *reinterpret_cast<const bf16x8*>(Kb + (32 * u + l32) * KROWB + 32 * ks + 16 * h);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const bf16x8 kk = ((WV & 1) != 0) ? kf[u][ks]
+                                          : *reinterpret_cast<const bf16x8*>(Kb + (32 * u + l32) * KROWB + 32 * ks + 16 * h);
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+          sacc[qb][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kk, qf[qb][ks],
+                                                                ((WV & 4) != 0 && ks == 0) ? minit[qb] : sacc[qb][u], 0, 0, 0);
+      }
+    if (kv0 + KT > c) {      // keys >= c: zero pads, added analytically at the end
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (kv0 + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * h >= c) sacc[qb][u][r] = -INFINITY;
+    }
+    // ---- online softmax with deferred rescale, per query block
+    bf16x8 pf[2][2][2];
+    if constexpr ((WV & 2) != 0) {
+      float mxq[2];
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        float mxa = sacc[qb][0][0], mxb = sacc[qb][1][0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) {
+          mxa = fmaxf(mxa, sacc[qb][0][r]);
+          mxb = fmaxf(mxb, sacc[qb][1][r]);
+        }
+        float mx = fmaxf(mxa, mxb);
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+        mxq[qb] = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+      }
+      const bool need0 = (t == 0) || (mxq[0] > kThr), need1 = (t == 0) || (mxq[1] > kThr);
+      if (__builtin_amdgcn_ballot_w64(need0 || need1)) {
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+          const float delta = (qb ? need1 : need0) ? mxq[qb] : 0.f;
+          if (t > 0) {
+            const float alpha = fast_exp2(-delta);
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+              for (int r = 0; r < 16; ++r) oacc[qb][mt][r] *= alpha;
+          }
+          m_run[qb] = (t == 0) ? delta : m_run[qb] + delta;
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sacc[qb][u][r] -= delta;
+          if constexpr ((WV & 4) != 0) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) minit[qb][r] = -m_run[qb];
+          }
+        }
+      }
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) pf[qb][u][s2][e] = (__bf16)fast_exp2(sacc[qb][u][8 * s2 + e]);
+    } else
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      float mxa = sacc[qb][0][0], mxb = sacc[qb][1][0];
+#pragma unroll
+      for (int r = 1; r < 16; ++r) {
+        mxa = fmaxf(mxa, sacc[qb][0][r]);
+        mxb = fmaxf(mxb, sacc[qb][1][r]);
+      }
+      float mx = fmaxf(mxa, mxb);
+      {
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+        mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+      }
+      const bool need = (t == 0) || (mx > kThr);
+      if (__builtin_amdgcn_ballot_w64(need)) {
+        const float delta = need ? mx : 0.f;
+        if (t > 0) {
+          const float alpha = fast_exp2(-delta);
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) oacc[qb][mt][r] *= alpha;
+        }
+        m_run[qb] = (t == 0) ? delta : m_run[qb] + delta;
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) sacc[qb][u][r] -= delta;
+        if constexpr ((WV & 4) != 0) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) minit[qb][r] = -m_run[qb];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) pf[qb][u][s2][e] = (__bf16)fast_exp2(sacc[qb][u][8 * s2 + e]);
+    }
+    // ---- O^T += V^T . P^T: each V^T fragment feeds both query blocks
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int row = 32 * u + 16 * s2 + 4 * (lane >> 5) + ((lane >> 2) & 3);
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          const int blk = 2 * mt + ((lane >> 4) & 1);
+          const char* p0 = Vb + row * VROWB + 32 * (blk ^ (row & 3)) + 8 * (lane & 3);
+          const char* p1 = p0 + 8 * VROWB;
+          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
+          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p1);
+          const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+          for (int qb = 0; qb < 2; ++qb)
+            oacc[qb][mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[qb][u][s2], oacc[qb][mt], 0, 0, 0);
+        }
+      }
+    if (t + 1 < ntiles) store_tile((t + 1) & 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue (per query block)
+  const AttnBranch& br = a.br[wi.bi];
+  const int npad = g.m - c;
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    float l = oacc[qb][1][8];               // d-row 48 (+4h): the ones row = sum_k P
+    float mr = m_run[qb], so = 1.f;
+    if (npad > 0) {
+      const float mf = fmaxf(mr, 0.f);
+      so = fast_exp2(mr - mf);
+      l = l * so + (float)npad * fast_exp2(-mf);
+      mr = mf;
+    }
+    const float inv = so / l;
+    const int i = q0 + w * 64 + qb * 32 + l32;
+    if (i < rows_needed) {
+      uint16_t* orow = br.o + (((int64_t)bn * g.m + i) * a.H + hh) * (int64_t)D;
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int rg = 0; rg < 4; ++rg) {
+          const int d0 = 32 * mt + 8 * rg + 4 * h;
+          if (d0 < D) {
+            float vv[4] = {oacc[qb][mt][4 * rg] * inv, oacc[qb][mt][4 * rg + 1] * inv,
+                           oacc[qb][mt][4 * rg + 2] * inv, oacc[qb][mt][4 * rg + 3] * inv};
+            store_bf16<4>(orow + d0, vv);
+          }
+        }
+      if (h == 0) br.lse[((int64_t)bn * a.H + hh) * g.m + i] = (mr + __builtin_amdgcn_logf(l)) * 0.69314718055994530942f;
+    }
   }
 }
 
@@ -1222,12 +1585,25 @@ extern "C" int gp_dilated_attn_fwd_ex(const uint16_t* q, int64_t q_row_stride, i
   a.c_log2 = q_log2_prescaled ? 1.0f : scale * 1.44269504088896340736f;
   const char* impl_env = getenv("GP_ATTN_IMPL");   // A/B switch: 1 = 16x16x32 kernel, 2 = 32x32x16 kernel
   const int impl = (D == 96) ? 1 : (impl_env ? atoi(impl_env) : 2);
-  GP_REQUIRE(impl == 1 || impl == 2 || impl == 3, "gp_dilated_attn_fwd: GP_ATTN_IMPL must be 1, 2 or 3");
+  GP_REQUIRE(impl >= 1 && impl <= 4, "gp_dilated_attn_fwd: GP_ATTN_IMPL must be 1..4");
+  GP_REQUIRE(impl != 4 || (D == 48 && q_log2_prescaled), "gp_dilated_attn_fwd: GP_ATTN_IMPL=4 needs D = 48, prescaled q");
   GP_REQUIRE(impl != 3 || q_log2_prescaled, "gp_dilated_attn_fwd: GP_ATTN_IMPL=3 needs q_log2_prescaled");
   GP_REQUIRE(!q_log2_prescaled || impl != 1, "gp_dilated_attn_fwd: q_log2_prescaled needs D in {48, 64}");
   const char* var_env = getenv("GP_ATTN_VAR");
   const int var = var_env ? atoi(var_env) : 0;
-  const int qblk = (impl == 2 && var >= 512 && (var & 512)) ? 256 : 128;   // query rows per workgroup
+  // buffer-descriptor staging (impl 4, VAR 2048) addresses V as K + dv inside one descriptor whose
+  // record count ends at the last valid row: needs v at or after k in memory, a row stride that
+  // covers dv + one head (rows past c then fall outside the records), 32-bit tile offsets
+  bool kv_desc_ok = true;
+  for (int b = 0; b < nbranch; ++b) {
+    const GpAttnBranch& d = branches[b];
+    const int64_t dv = (int64_t)((const char*)d.v - (const char*)d.k);
+    const int64_t rs2 = 2 * d.kv_row_stride;
+    kv_desc_ok = kv_desc_ok && dv >= 0 && rs2 >= dv + 2 * D && dv + 64 * (int64_t)d.ratio * rs2 < 0x7fffffff;
+  }
+  GP_REQUIRE(impl != 4 || kv_desc_ok, "gp_dilated_attn_fwd: GP_ATTN_IMPL=4 needs v after k within one row stride");
+  GP_REQUIRE(impl == 4 || !(var & 2048) || kv_desc_ok, "gp_dilated_attn_fwd: GP_ATTN_VAR & 2048 needs v after k within one row stride");
+  const int qblk = (impl == 2 && var >= 512 && (var & 512)) ? 256 : (impl == 4 ? 256 : 128);   // query rows per workgroup
   // order branches by keys per work item (descending) so the longest items start first
   int order[GP_MAX_BRANCHES];
   GpBranch geo[GP_MAX_BRANCHES];
@@ -1291,6 +1667,16 @@ extern "C" int gp_dilated_attn_fwd_ex(const uint16_t* q, int64_t q_row_stride, i
       case 64: dilated_attn_kernel<64><<<(unsigned)items, 256, 0, s>>>(a); break;
       case 96: dilated_attn_kernel<96><<<(unsigned)items, 256, 0, s>>>(a); break;
     }
+  } else if (impl == 4) {
+    switch (var) {
+      case 0: dilated_attn_w64_kernel<4, 0><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 1: dilated_attn_w64_kernel<4, 1><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 2: dilated_attn_w64_kernel<4, 2><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 3: dilated_attn_w64_kernel<4, 3><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 6: dilated_attn_w64_kernel<4, 6><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 7: dilated_attn_w64_kernel<4, 7><<<(unsigned)items, 256, 0, s>>>(a); break;
+      default: return gp_set_error("gp_dilated_attn_fwd: impl 4 GP_ATTN_VAR=%d unknown", var), GP_EARG;
+    }
   } else if (impl == 3) {
     if (D == 48) dilated_attn_pp_kernel<48><<<(unsigned)items, 256, 0, s>>>(a);
     else dilated_attn_pp_kernel<64><<<(unsigned)items, 256, 0, s>>>(a);
@@ -1315,13 +1701,20 @@ extern "C" int gp_dilated_attn_fwd_ex(const uint16_t* q, int64_t q_row_stride, i
       case 514: dilated_attn32_kernel<48, true, 8, 514><<<(unsigned)items, 512, 0, s>>>(a); break;
       case 1538: dilated_attn32_kernel<48, true, 8, 1538><<<(unsigned)items, 512, 0, s>>>(a); break;
       case 1026: dilated_attn32_kernel<48, true, 4, 1026><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 2050: dilated_attn32_kernel<48, true, 4, 2050><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 6146: dilated_attn32_kernel<48, true, 4, 6146><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 6150: dilated_attn32_kernel<48, true, 4, 6150><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 2562: dilated_attn32_kernel<48, true, 8, 2562><<<(unsigned)items, 512, 0, s>>>(a); break;
       case 34: dilated_attn32_kernel<48, true, 4, 34><<<(unsigned)items, 256, 0, s>>>(a); break;
       case 26: dilated_attn32_kernel<48, true, 4, 10, 4><<<(unsigned)items, 256, 0, s>>>(a); break;
       case 30: dilated_attn32_kernel<48, true, 4, 14, 4><<<(unsigned)items, 256, 0, s>>>(a); break;
       default: return gp_set_error("gp_dilated_attn_fwd: GP_ATTN_VAR=%d unknown", var), GP_EARG;
     }
-  } else if (q_log2_prescaled) {   // default: VAR 2 (staging addresses hoisted), +2% over VAR 0
-    if (D == 48) dilated_attn32_kernel<48, true, 4, 2><<<(unsigned)items, 256, 0, s>>>(a);
+  } else if (q_log2_prescaled) {
+    // default: VAR 2050 (staging addresses hoisted, K/V staged by buffer loads through a bounded
+    // descriptor: +5-7 % over VAR 2); VAR 2 where the descriptor layout does not fit
+    if (D == 48 && kv_desc_ok) dilated_attn32_kernel<48, true, 4, 2050><<<(unsigned)items, 256, 0, s>>>(a);
+    else if (D == 48) dilated_attn32_kernel<48, true, 4, 2><<<(unsigned)items, 256, 0, s>>>(a);
     else dilated_attn32_kernel<64, true, 4><<<(unsigned)items, 256, 0, s>>>(a);
   } else {
     if (D == 48) dilated_attn32_kernel<48, false, 4><<<(unsigned)items, 256, 0, s>>>(a);

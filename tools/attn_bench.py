@@ -30,6 +30,7 @@ qkv = qkv.to(torch.bfloat16)
 sc = runtime.AttentionScratch(torch.device("cuda"), 1, L, H, D, segs, ratios)
 flops = runtime.attention_valid_flops(L, segs, ratios, H, D)
 res = {}
+first = {}
 for rnd in range(args.iters):
     for impl in args.impls.split(","):
         base, _, var = impl.partition("@")            # "2p@4": impl 2, prescaled q, GP_ATTN_VAR=4
@@ -43,6 +44,15 @@ for rnd in range(args.iters):
         torch.cuda.synchronize()
         if rnd > 0:
             res.setdefault(impl, []).append(e0.elapsed_time(e1))
+        else:      # outputs of every impl, compared with the first one's after the loop
+            first[impl] = ([o.clone() for o in sc.outs], [x.clone() for x in sc.lses])
+ref_impl = next(iter(first))
+for impl, (outs, lses) in first.items():
+    # rows no impl writes (outside every valid query range) hold garbage: compare NaN-equal
+    do = max(float(torch.nan_to_num(a.float() - b.float(), nan=0.0).abs().max()) +
+             float((a.float().isnan() != b.float().isnan()).sum()) for a, b in zip(outs, first[ref_impl][0]))
+    dl = max(float((a - b).abs().max()) for a, b in zip(lses, first[ref_impl][1]))
+    print("impl %s vs %s: max|d out| %.3g  max|d lse| %.3g" % (impl, ref_impl, do, dl))
 for impl, ts in res.items():
     ts.sort()
     med = ts[len(ts) // 2]
