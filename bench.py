@@ -1,10 +1,12 @@
 """Slide-encoder throughput benchmark (BASELINE.json metric) on 1..8 MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--tiles 70000]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--tiles T]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 A step = one gigapath_slide_enc12l768d forward (bf16, inference) over one synthetic slide of
---tiles tiles (default 70,000 = BASELINE config C3), inputs and weights resident in HBM.
+--tiles tiles, inputs and weights resident in HBM.  Default: 70,000 tiles (BASELINE config C3,
+the north star's 1-GPU target) at N = 1; 256,000 tiles (config C4, the north star's 8-GPU
+scaling target) for the sequence-parallel runs at N > 1.
 Multi-GPU (one process per GPU), --mode:
   sp       (default for N > 1) the SAME slide is sharded across the N ranks by sequence
            parallelism (seqpar.py: per-layer sparse K/V exchange over RCCL point-to-point);
@@ -96,7 +98,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--tiles", type=int, default=70000)
+    ap.add_argument("--tiles", type=int, default=None,
+                    help="slide size (default 70000; 256000 for --mode sp at N > 1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--mode", choices=["sp", "replica", "mixed"], default="sp")
@@ -110,6 +113,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     sp = world > 1 and args.mode == "sp"
     mixed = args.mode == "mixed"
+    if args.tiles is None:
+        args.tiles = 256000 if sp else 70000
     # GP_BENCH_BACKEND=gloo: rehearsal of the multi-rank path with several ranks on one GPU
     backend = os.environ.get("GP_BENCH_BACKEND", "nccl")
     if backend != "nccl":
