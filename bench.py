@@ -13,8 +13,8 @@ Multi-GPU (one process per GPU), --mode:
            value = slide tiles / max-over-ranks wall time ("strong" scaling, C4's design);
   replica  every rank encodes its own slide, no collective: value = N x tiles / time ("weak");
   mixed    C5: a batch of 32 slides of 2k-100k tiles (log-uniform, seed 3), LPT-assigned to the
-           ranks (batch.py, data parallel, one all-reduce of the outputs at the end); value =
-           batch tiles / time ("strong").
+           ranks (batch.py, data parallel, one all-reduce of the outputs at the end), each rank's
+           slides varlen-packed into one forward; value = batch tiles / time ("strong").
 Rank 0 prints ONE JSON line including the attention kernel's roofline (HIP events around
 every gp_dilated_attn_fwd launch in the timed region) and a CPU baseline (the fp32 oracle on
 a bounded sample of the same workload, timed on this host).
@@ -192,10 +192,10 @@ def main():
     L = args.tiles + 1
     att_flops_launch = runtime.attention_valid_flops(L, segs, ratios, 16, 48)
     if mixed:
-        # average launch = (all slides' attention FLOPs this rank ran) / (its launches)
+        # varlen packing: one attention launch per layer covers every slide of this rank
         from gigapath import batch as _b
         mine = _b.lpt_assign([_b.slide_cost(n, segs, ratios) for n in sizes], world)[rank]
-        att_flops_launch = sum(runtime.attention_valid_flops(sizes[i] + 1, segs, ratios, 16, 48) for i in mine) / len(mine)
+        att_flops_launch = sum(runtime.attention_valid_flops(sizes[i] + 1, segs, ratios, 16, 48) for i in mine)
     n_att, ms_att = kt.get("attn", (0, 0.0))
     if sp:
         # this rank's attention launches cover its query window: price them with its share of the
@@ -219,7 +219,7 @@ def main():
     if sp:
         merge_tok = b_w - a_w
     elif mixed:
-        merge_tok = sum(sizes[i] + 1 for i in mine) / len(mine)
+        merge_tok = sum(sizes[i] + 1 for i in mine)
     else:
         merge_tok = L
     merge_bytes = runtime.merge_bytes(L, segs, ratios, 16, 48) * merge_tok / L

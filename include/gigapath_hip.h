@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define GP_ABI_VERSION 2
+#define GP_ABI_VERSION 3
 #define GP_EARG (-1)
 #define GP_MAX_BRANCHES 8
 #define GP_MAX_DESTS 8
@@ -171,6 +171,33 @@ int gp_branch_merge_ln(const uint16_t* const* o_in, const float* const* lse_in,
 int gp_branch_merge_ln_window(const uint16_t* const* o_in, const float* const* lse_in,
                               const int32_t* seg_len, const int32_t* ratios, int nbranch, int64_t B,
                               int64_t L, int64_t tok_lo, int64_t n_tok, int H, int D, const float* ln_w,
+                              const float* ln_b, float eps, uint16_t* out, void* stream);
+
+/* ---- Varlen packing (config C5, SURVEY §8e: "concatenate slides with per-slide segment
+ * tables, no cross-slide attention").  nslide slides packed token-major in one qkv buffer
+ * [T, qkv_row_stride] (slide i at rows [tok_off[i], tok_off[i] + L[i]), q | k | v at columns
+ * 0, H*D, 2*H*D), each with its OWN segment schedule s = min(sl, L[i]) -- the reference's
+ * per-slide B = 1 forward (slide_encoder.py:181-223), batched into one launch per layer.
+ * Replaces: one gp_dilated_attn_fwd / gp_branch_merge_ln pair per slide.
+ *
+ * gp_varlen_plan_bytes: size of the host plan buffer.
+ * gp_varlen_plan: with plan_host == NULL, only writes o_elems[b] / lse_elems[b] (elements of the
+ *   packed per-branch output buffers the caller allocates: slide-major [nseg_ib, m_ib, H, D] and
+ *   [nseg_ib, H, m_ib] regions).  Otherwise also fills plan_host with the work table (device
+ *   pointers into qkv / o / lse, not dereferenced here); the caller copies the plan_bytes to a
+ *   16-byte aligned device buffer (plan_dev) that stays alive while launches use it.
+ * gp_dilated_attn_fwd_varlen: every slide's five-branch attention in one launch (D = 48,
+ *   q pre-scaled by D^-1/2 * log2 e).
+ * gp_branch_merge_ln_varlen: every packed token's LSE merge + inner LN (E = 768, D = 48);
+ *   out: [T, E] bf16, row = packed token. */
+int64_t gp_varlen_plan_bytes(int nslide, int nbranch);
+int gp_varlen_plan(const int64_t* L, int nslide, int H, int D, const int32_t* seg_len,
+                   const int32_t* ratios, int nbranch, const uint16_t* qkv, int64_t qkv_row_stride,
+                   uint16_t* const* o_out, float* const* lse_out, void* plan_host, int64_t plan_bytes,
+                   int64_t* o_elems, int64_t* lse_elems);
+int gp_dilated_attn_fwd_varlen(const void* plan_host, const void* plan_dev, int q_log2_prescaled,
+                               void* stream);
+int gp_branch_merge_ln_varlen(const void* plan_host, const void* plan_dev, const float* ln_w,
                               const float* ln_b, float eps, uint16_t* out, void* stream);
 
 /* Residual add fused with the next pre-LN (encoder.py:141,147 / :159,126):

@@ -18,6 +18,10 @@
 #include <math.h>
 #include <type_traits>
 #include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
 
 #include "gp_api.h"
 #include "gp_common.h"
@@ -39,6 +43,9 @@ struct AttnBranch {
   int64_t kv_tok_base;
   uint16_t* o;          // [B*nseg, m, H, D]
   float* lse;           // [B*nseg, H, m]
+  // varlen table entries only (one per (slide, branch); B = 1, window = the whole slide)
+  const uint16_t* q;    // the slide's first query row
+  int64_t L;            // the slide's length (CLS + tiles)
 };
 
 struct AttnArgs {
@@ -52,6 +59,8 @@ struct AttnArgs {
   float c_log2;         // softmax_scale * log2(e)
   int64_t total_items;
   AttnBranch br[GP_MAX_BRANCHES];   // work order (heaviest first)
+  const AttnBranch* tab;            // varlen: ntab (slide, branch) entries in device memory
+  int32_t ntab;
 };
 
 // Work item -> (branch, batch, segment, head, query-row range).  Rows [i_lo, i_hi) of
@@ -85,6 +94,32 @@ GP_DEV void decode_item(const AttnArgs& a, int item, WorkItem& w) {
   w.i_lo = ceil_div_pos(a.win_lo - base, g.r);
   const int hi = ceil_div_pos(a.win_hi - base, g.r);
   w.i_hi = hi < g.m ? hi : g.m;
+}
+
+// Varlen (packed slides): entry = (slide, branch), items ordered by entry (heaviest first);
+// binary search on item_begin (wave-uniform), then the B = 1, whole-slide decode.
+GP_DEV void decode_item_tab(const AttnArgs& a, int item, WorkItem& w, AttnBranch& e) {
+  int lo = 0, hi = a.ntab - 1;
+  while (lo < hi) {                    // last entry with item_begin <= item
+    const int mid = (lo + hi + 1) >> 1;
+    if ((int64_t)item >= a.tab[mid].item_begin) lo = mid; else hi = mid - 1;
+  }
+  e = a.tab[lo];
+  const GpBranch& g = e.g;
+  int local = item - (int)e.item_begin;
+  w.bi = lo;
+  w.qb = local % e.nqb;
+  local /= e.nqb;
+  w.hh = local % a.H;
+  w.n = local / a.H;
+  w.bidx = 0;
+  w.bn = w.n;
+  w.j = w.hh / g.hpg;
+  w.c = gp_valid_rows(g, e.L, w.n, w.j);
+  const int64_t base = (int64_t)w.n * g.g + w.j;
+  w.i_lo = 0;
+  const int hi2 = ceil_div_pos(e.L - base, g.r);
+  w.i_hi = hi2 < g.m ? hi2 : g.m;
 }
 
 constexpr int kWaves = 4;
@@ -336,7 +371,7 @@ GP_DEV float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 // column 48 holds 1.0, Q column 48 holds -m (m kept bf16-exact), so S arrives already shifted
 // with no per-tile accumulator initialisation and no extra registers (2 more MFMAs per tile,
 // ~17 fewer VALU).  OCC = waves per SIMD the register budget must allow.
-template <int D, bool kPre, int NW, int VAR = 0, int OCC = 2>
+template <int D, bool kPre, int NW, int VAR = 0, int OCC = 2, bool kTab = false>
 __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const AttnArgs a) {
   static_assert(D == 48 || D == 64, "v2 kernel covers D = 48 and 64");
   static_assert(NW == 4 || NW == 8, "");
@@ -369,8 +404,11 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
 
   // ---- work item (32-bit index math: items < 2^31, checked on the host)
   WorkItem wi;
-  decode_item(a, (int)xcd_group(blockIdx.x, gridDim.x), wi);
-  const GpBranch g = a.br[wi.bi].g;
+  AttnBranch te;                             // kTab: this item's table entry
+  if constexpr (kTab) decode_item_tab(a, (int)xcd_group(blockIdx.x, gridDim.x), wi, te);
+  else decode_item(a, (int)xcd_group(blockIdx.x, gridDim.x), wi);
+  const AttnBranch& brr = kTab ? te : a.br[wi.bi];
+  const GpBranch g = brr.g;
   const int hh = wi.hh, c = wi.c, bn = wi.bn;
   const int rows_needed = wi.i_hi;
   const int q0 = wi.i_lo + wi.qb * QB;
@@ -379,12 +417,12 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int l32 = lane & 31, h = lane >> 5;
-  const AttnBranch& brr = a.br[wi.bi];
   const int64_t tok0 = (int64_t)wi.bidx * a.L + (int64_t)wi.n * g.s + wi.j;
   const int64_t qstride = (int64_t)g.r * a.q_stride;
   const int64_t kvstride = (int64_t)g.r * brr.kv_stride;
   const int kcol = brr.kv_sparse ? (hh % g.hpg) * D : hh * D;
-  const uint16_t* qbase = a.q + (tok0 - a.q_tok_base) * a.q_stride + hh * D;
+  const uint16_t* qbase = kTab ? brr.q + tok0 * a.q_stride + hh * D
+                               : a.q + (tok0 - a.q_tok_base) * a.q_stride + hh * D;
   const uint16_t* kbase = brr.k + (tok0 - brr.kv_tok_base) * brr.kv_stride + kcol;
   const uint16_t* vbase = brr.v + (tok0 - brr.kv_tok_base) * brr.kv_stride + kcol;
 
@@ -786,7 +824,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
   }
   const float inv = so / l;
   const int i = q0 + w * 32 + l32;
-  const AttnBranch& br = a.br[wi.bi];
+  const AttnBranch& br = brr;
   if (i < rows_needed) {
     uint16_t* orow = br.o + (((int64_t)bn * g.m + i) * a.H + hh) * (int64_t)D;
 #pragma unroll
@@ -1411,6 +1449,11 @@ struct MergeArgs {
   const float* ln_b;
   float eps;
   uint16_t* out;
+  // varlen (packed slides): slide i owns packed tokens [tok_off[i], tok_off[i+1]); its branch b
+  // geometry and o/lse regions are mtab[i * nbranch + b]
+  const MergeBranch* mtab;
+  const int64_t* tok_off;
+  int32_t nslide;
 };
 
 // One wave per run of kTPW consecutive tokens; lane l owns the EPL = E/64 contiguous elements
@@ -1422,13 +1465,27 @@ struct MergeArgs {
 // branch-order accumulation) followed by inner_attn_ln.
 constexpr int kTPW = 1;
 
-template <int EPL, int D>
+template <int EPL, int D, bool kTab = false>
 __global__ __launch_bounds__(256) void branch_merge_kernel(const MergeArgs a) {
   const int lane = threadIdx.x & 63;
   const int run = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + (int)(threadIdx.x >> 6));
   const int total = (int)(a.B * a.ntok);
   const int r0 = run * kTPW;
   if (r0 >= total) return;
+  // kTab: the token's slide (binary search, wave-uniform) and that slide's branch entries
+  MergeBranch tb[kTab ? GP_MAX_BRANCHES : 1];
+  int64_t slide_tok0 = 0;
+  if constexpr (kTab) {
+    int lo = 0, hi = a.nslide - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if ((int64_t)r0 >= a.tok_off[mid]) lo = mid; else hi = mid - 1;
+    }
+    slide_tok0 = a.tok_off[lo];
+#pragma unroll
+    for (int b = 0; b < GP_MAX_BRANCHES; ++b)
+      if (b < a.nbranch) tb[b] = a.mtab[lo * a.nbranch + b];
+  }
   const int nt = (int)a.ntok;
   const int E = 64 * EPL;
   const int col0 = lane * EPL;
@@ -1439,12 +1496,17 @@ __global__ __launch_bounds__(256) void branch_merge_kernel(const MergeArgs a) {
     const int row = r0 + k;
     if (row >= total) break;
     if (k == 0 || p + 1 >= (int)a.tok_lo + nt) {   // (re)derive positions: run start / next batch
-      bidx = row / nt;
-      p = (int)a.tok_lo + (row - bidx * nt);
+      if constexpr (kTab) {
+        bidx = 0;
+        p = (int)(row - slide_tok0);
+      } else {
+        bidx = row / nt;
+        p = (int)a.tok_lo + (row - bidx * nt);
+      }
 #pragma unroll
       for (int b = 0; b < GP_MAX_BRANCHES; ++b)
         if (b < a.nbranch) {
-          const GpBranch& g = a.br[b].g;
+          const GpBranch& g = (kTab ? tb[b] : a.br[b]).g;
           pn[b] = p / g.g;
           pt[b] = p - pn[b] * g.g;
           pi[b] = pt[b] / g.r;
@@ -1455,7 +1517,7 @@ __global__ __launch_bounds__(256) void branch_merge_kernel(const MergeArgs a) {
 #pragma unroll
       for (int b = 0; b < GP_MAX_BRANCHES; ++b)
         if (b < a.nbranch) {
-          const GpBranch& g = a.br[b].g;
+          const GpBranch& g = (kTab ? tb[b] : a.br[b]).g;
           if (++pt[b] == g.g) { pt[b] = 0; ++pn[b]; pi[b] = 0; pj[b] = 0; }
           else if (++pj[b] == g.r) { pj[b] = 0; ++pi[b]; }
         }
@@ -1469,13 +1531,13 @@ __global__ __launch_bounds__(256) void branch_merge_kernel(const MergeArgs a) {
       lse[b] = -1e8f;
       cov[b] = false;
       if (b < a.nbranch) {
-        const GpBranch& g = a.br[b].g;
+        const GpBranch& g = (kTab ? tb[b] : a.br[b]).g;
         const int lph = g.hpg * (D / EPL);        // lanes per head group
         cov[b] = lane >= pj[b] * lph && lane < (pj[b] + 1) * lph;
         if (cov[b]) {
-          lse[b] = a.br[b].lse[((int64_t)(bidx * g.nseg + pn[b]) * a.H + hh) * g.m + pi[b]];
+          lse[b] = (kTab ? tb[b] : a.br[b]).lse[((int64_t)(bidx * g.nseg + pn[b]) * a.H + hh) * g.m + pi[b]];
           const uint2* src = reinterpret_cast<const uint2*>(
-              a.br[b].o + ((int64_t)(bidx * g.nseg + pn[b]) * g.m + pi[b]) * E + col0);
+              (kTab ? tb[b] : a.br[b]).o + ((int64_t)(bidx * g.nseg + pn[b]) * g.m + pi[b]) * E + col0);
 #pragma unroll
           for (int q = 0; q < EPL / 4; ++q) ob[b][q] = src[q];
         }
@@ -1806,6 +1868,171 @@ extern "C" int gp_branch_merge_ln_window(const uint16_t* const* o_in, const floa
       break;
   }
   return gp_check_launch("gp_branch_merge_ln");
+}
+
+// =========================================================================================
+// Varlen packing (config C5): several slides concatenated token-major in one [T, 3E] qkv buffer
+// (slide i at rows [tok_off[i], tok_off[i] + L_i)), one attention launch and one merge launch
+// for all of them.  Every slide keeps its own segment schedule (s = min(sl, L_i), ...) and no
+// query attends across slides, so each slide's outputs are those of its own B = 1 forward.
+// The plan (host bytes, copied by the caller to device memory) holds the work table.
+namespace {
+constexpr int32_t kVarlenMagic = 0x47505631;   // "GPV1"
+struct VarlenHdr {
+  int32_t magic, nslide, nbranch, H, D, ntab;
+  int64_t T, total_items, qkv_stride;
+  int64_t tab_off, mtab_off, tok_off_off, bytes;
+};
+inline int64_t gp_align16(int64_t x) { return (x + 15) & ~int64_t(15); }
+inline void varlen_layout(int nslide, int nbranch, VarlenHdr& h) {
+  h.tab_off = gp_align16(sizeof(VarlenHdr));
+  h.mtab_off = gp_align16(h.tab_off + (int64_t)nslide * nbranch * sizeof(AttnBranch));
+  h.tok_off_off = gp_align16(h.mtab_off + (int64_t)nslide * nbranch * sizeof(MergeBranch));
+  h.bytes = gp_align16(h.tok_off_off + (int64_t)(nslide + 1) * sizeof(int64_t));
+}
+}  // namespace
+
+extern "C" int64_t gp_varlen_plan_bytes(int nslide, int nbranch) {
+  if (nslide < 1 || nbranch < 1 || nbranch > GP_MAX_BRANCHES) return -1;
+  VarlenHdr h;
+  varlen_layout(nslide, nbranch, h);
+  return h.bytes;
+}
+
+extern "C" int gp_varlen_plan(const int64_t* L, int nslide, int H, int D, const int32_t* seg_len,
+                              const int32_t* ratios, int nbranch, const uint16_t* qkv, int64_t qkv_row_stride,
+                              uint16_t* const* o_out, float* const* lse_out, void* plan_host, int64_t plan_bytes,
+                              int64_t* o_elems, int64_t* lse_elems) {
+  GP_REQUIRE(nslide >= 1 && L && seg_len && ratios && o_elems && lse_elems, "gp_varlen_plan: bad arguments");
+  GP_REQUIRE(nbranch >= 1 && nbranch <= GP_MAX_BRANCHES, "gp_varlen_plan: nbranch must be 1..%d", GP_MAX_BRANCHES);
+  GP_REQUIRE(H > 0 && D > 0 && qkv_row_stride >= 3LL * H * D && qkv_row_stride % 8 == 0, "gp_varlen_plan: bad sizes");
+  int64_t T = 0;
+  for (int i = 0; i < nslide; ++i) {
+    GP_REQUIRE(L[i] > 0, "gp_varlen_plan: slide %d has L = %lld", i, (long long)L[i]);
+    T += L[i];
+  }
+  GP_REQUIRE(T < (int64_t)0x7fffffff, "gp_varlen_plan: %lld packed tokens is too many", (long long)T);
+  const int qblk = 128;                            // query rows per work item (v2 kernel)
+  for (int b = 0; b < nbranch; ++b) { o_elems[b] = 0; lse_elems[b] = 0; }
+  // per (slide, branch) output region offsets, in slide order
+  std::vector<int64_t> ooff((size_t)nslide * nbranch), loff((size_t)nslide * nbranch);
+  std::vector<GpBranch> geo((size_t)nslide * nbranch);
+  for (int i = 0; i < nslide; ++i)
+    for (int b = 0; b < nbranch; ++b) {
+      GP_REQUIRE(seg_len[b] > 0 && ratios[b] > 0, "gp_varlen_plan: branch %d has sl=%d r=%d", b, seg_len[b], ratios[b]);
+      const GpBranch g = gp_make_branch(L[i], seg_len[b], ratios[b], H);
+      geo[(size_t)i * nbranch + b] = g;
+      ooff[(size_t)i * nbranch + b] = o_elems[b];
+      loff[(size_t)i * nbranch + b] = lse_elems[b];
+      o_elems[b] += (int64_t)g.nseg * g.m * H * D;
+      lse_elems[b] += (int64_t)g.nseg * H * g.m;
+    }
+  if (plan_host == nullptr) return 0;               // sizing call
+  VarlenHdr h;
+  varlen_layout(nslide, nbranch, h);
+  GP_REQUIRE(plan_bytes >= h.bytes, "gp_varlen_plan: plan buffer %lld < %lld bytes", (long long)plan_bytes,
+             (long long)h.bytes);
+  GP_REQUIRE(qkv && o_out && lse_out, "gp_varlen_plan: null device pointer");
+  for (int b = 0; b < nbranch; ++b) GP_REQUIRE(o_out[b] && lse_out[b], "gp_varlen_plan: branch %d output null", b);
+  char* base = static_cast<char*>(plan_host);
+  memset(base, 0, (size_t)h.bytes);
+  AttnBranch* tab = reinterpret_cast<AttnBranch*>(base + h.tab_off);
+  MergeBranch* mtab = reinterpret_cast<MergeBranch*>(base + h.mtab_off);
+  int64_t* tok_off = reinterpret_cast<int64_t*>(base + h.tok_off_off);
+  tok_off[0] = 0;
+  for (int i = 0; i < nslide; ++i) tok_off[i + 1] = tok_off[i] + L[i];
+  // attention entries heaviest first (keys per item), stable
+  std::vector<int> order((size_t)nslide * nbranch);
+  for (size_t x = 0; x < order.size(); ++x) order[x] = (int)x;
+  std::stable_sort(order.begin(), order.end(), [&](int u, int v) { return geo[u].m > geo[v].m; });
+  const int E = H * D;
+  int64_t items = 0;
+  for (size_t x = 0; x < order.size(); ++x) {
+    const int id = order[x], i = id / nbranch, b = id % nbranch;
+    const GpBranch& g = geo[id];
+    AttnBranch& e = tab[x];
+    e.g = g;
+    e.nqb = (g.m + qblk - 1) / qblk;
+    e.n_lo = 0;
+    e.nseg_w = g.nseg;
+    e.kv_sparse = 0;
+    e.item_begin = items;
+    const uint16_t* row0 = qkv + tok_off[i] * qkv_row_stride;
+    e.q = row0;
+    e.k = row0 + E;
+    e.v = row0 + 2 * E;
+    e.kv_stride = qkv_row_stride;
+    e.kv_tok_base = 0;
+    e.o = o_out[b] + ooff[id];
+    e.lse = lse_out[b] + loff[id];
+    e.L = L[i];
+    items += (int64_t)g.nseg * H * e.nqb;
+  }
+  for (int i = 0; i < nslide; ++i)
+    for (int b = 0; b < nbranch; ++b) {
+      MergeBranch& m = mtab[(size_t)i * nbranch + b];
+      m.g = geo[(size_t)i * nbranch + b];
+      m.o = o_out[b] + ooff[(size_t)i * nbranch + b];
+      m.lse = lse_out[b] + loff[(size_t)i * nbranch + b];
+    }
+  GP_REQUIRE(items < (int64_t)0x7fffffff, "gp_varlen_plan: too many work items");
+  VarlenHdr* hp = reinterpret_cast<VarlenHdr*>(base);
+  *hp = h;
+  hp->magic = kVarlenMagic;
+  hp->nslide = nslide;
+  hp->nbranch = nbranch;
+  hp->H = H;
+  hp->D = D;
+  hp->ntab = nslide * nbranch;
+  hp->T = T;
+  hp->total_items = items;
+  hp->qkv_stride = qkv_row_stride;
+  return 0;
+}
+
+static int varlen_header(const void* plan_host, const void* plan_dev, const char* who, VarlenHdr& h) {
+  GP_REQUIRE(plan_host && plan_dev && gp_aligned(plan_dev, 16), "%s: null/misaligned plan", who);
+  h = *static_cast<const VarlenHdr*>(plan_host);
+  GP_REQUIRE(h.magic == kVarlenMagic, "%s: not a gp_varlen_plan buffer", who);
+  return 0;
+}
+
+extern "C" int gp_dilated_attn_fwd_varlen(const void* plan_host, const void* plan_dev, int q_log2_prescaled,
+                                          void* stream) {
+  VarlenHdr h;
+  if (int rc = varlen_header(plan_host, plan_dev, "gp_dilated_attn_fwd_varlen", h)) return rc;
+  GP_REQUIRE(h.D == 48 && q_log2_prescaled, "gp_dilated_attn_fwd_varlen: needs D = 48 and a pre-scaled q (D=%d)", h.D);
+  if (h.total_items == 0) return 0;
+  AttnArgs a;
+  memset(&a, 0, sizeof(a));
+  a.q_stride = h.qkv_stride;
+  a.H = h.H;
+  a.nbranch = h.nbranch;
+  a.c_log2 = 1.0f;
+  a.total_items = h.total_items;
+  a.tab = reinterpret_cast<const AttnBranch*>(static_cast<const char*>(plan_dev) + h.tab_off);
+  a.ntab = h.ntab;
+  dilated_attn32_kernel<48, true, 4, 2050, 2, true><<<(unsigned)h.total_items, 256, 0, gp_stream(stream)>>>(a);
+  return gp_check_launch("gp_dilated_attn_fwd_varlen");
+}
+
+extern "C" int gp_branch_merge_ln_varlen(const void* plan_host, const void* plan_dev, const float* ln_w,
+                                         const float* ln_b, float eps, uint16_t* out, void* stream) {
+  VarlenHdr h;
+  if (int rc = varlen_header(plan_host, plan_dev, "gp_branch_merge_ln_varlen", h)) return rc;
+  GP_REQUIRE(h.H * h.D == 768 && h.D == 48, "gp_branch_merge_ln_varlen: needs H*D = 768, D = 48");
+  GP_REQUIRE(out && (ln_w == nullptr || ln_b != nullptr), "gp_branch_merge_ln_varlen: bad output / LN arguments");
+  MergeArgs a;
+  memset(&a, 0, sizeof(a));
+  a.B = 1; a.L = h.T; a.tok_lo = 0; a.ntok = h.T;
+  a.H = h.H; a.D = h.D; a.E = h.H * h.D; a.nbranch = h.nbranch;
+  a.ln_w = ln_w; a.ln_b = ln_b; a.eps = eps; a.out = out;
+  a.mtab = reinterpret_cast<const MergeBranch*>(static_cast<const char*>(plan_dev) + h.mtab_off);
+  a.tok_off = reinterpret_cast<const int64_t*>(static_cast<const char*>(plan_dev) + h.tok_off_off);
+  a.nslide = h.nslide;
+  const unsigned nb = (unsigned)((h.T + 4 * kTPW - 1) / (4 * kTPW));
+  branch_merge_kernel<12, 48, true><<<nb, 256, 0, gp_stream(stream)>>>(a);
+  return gp_check_launch("gp_branch_merge_ln_varlen");
 }
 
 // =========================================================================================

@@ -15,7 +15,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GIGAPATH_HIP_LIB", os.path.join(_HERE, "_lib", "libgigapath_hip.so"))
-ABI_VERSION = 2
+ABI_VERSION = 3
 MAX_BRANCHES = 8
 MAX_DESTS = 8
 
@@ -55,7 +55,12 @@ SIGNATURES = {
     "gp_gelu_layernorm": [c_vp, c_vp, c_vp, c_f32, c_vp, c_i64, c_i32, c_vp],
     "gp_layernorm_f32": [c_vp, c_i64, c_vp, c_vp, c_f32, c_vp, c_i64, c_i32, c_vp],
     "gp_mean_tokens": [c_vp, c_i64, c_i64, c_i32, c_i64, c_vp, c_vp],
+    "gp_varlen_plan_bytes": [c_i32, c_i32],
+    "gp_varlen_plan": [c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp],
+    "gp_dilated_attn_fwd_varlen": [c_vp, c_vp, c_i32, c_vp],
+    "gp_branch_merge_ln_varlen": [c_vp, c_vp, c_vp, c_vp, c_f32, c_vp, c_vp],
 }
+_RESTYPES = {"gp_last_error_string": ctypes.c_char_p, "gp_varlen_plan_bytes": c_i64}
 
 _lib = None
 
@@ -78,7 +83,7 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     for name, args in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.argtypes = args
-        fn.restype = ctypes.c_char_p if name == "gp_last_error_string" else ctypes.c_int
+        fn.restype = _RESTYPES.get(name, ctypes.c_int)
     if lib.gp_abi_version() != ABI_VERSION:
         raise HipLibraryError("ABI mismatch: library %d, binding %d" % (lib.gp_abi_version(), ABI_VERSION))
     if path is None:
@@ -271,3 +276,64 @@ def mean_tokens(x, B, L, E, start, out):
     lib = load_library()
     _dev(x, torch.float32, "x"); _dev(out, torch.float32, "out")
     _check(lib.gp_mean_tokens(_ptr(x), B, L, E, start, _ptr(out), _stream()), "gp_mean_tokens")
+
+
+# ------------------------------------------------------------------------------------------
+# varlen packing (several slides in one launch per op; include/gigapath_hip.h "Varlen packing")
+# ------------------------------------------------------------------------------------------
+class VarlenPlan:
+    """Work table of `Ls` slides packed token-major in one [T, 3E] qkv buffer.
+
+    ``VarlenPlan(Ls, H, D, segs, ratios)`` sizes the packed per-branch outputs (``o_elems``,
+    ``lse_elems``); ``bind(qkv, outs, lses)`` writes the table (device pointers into those
+    tensors) and copies it to the device.  The tensors must outlive every launch using the plan."""
+
+    def __init__(self, Ls: Sequence[int], H: int, D: int, segs: Sequence[int], ratios: Sequence[int]):
+        lib = load_library()
+        self.Ls = [int(x) for x in Ls]
+        self.H, self.D, self.segs, self.ratios = H, D, list(segs), list(ratios)
+        nb = len(self.segs)
+        self._L = (c_i64 * len(self.Ls))(*self.Ls)
+        o_el, l_el = (c_i64 * nb)(), (c_i64 * nb)()
+        _check(lib.gp_varlen_plan(self._L, len(self.Ls), H, D, _i32_array(self.segs), _i32_array(self.ratios), nb,
+                                  None, 3 * H * D, None, None, None, 0, o_el, l_el), "gp_varlen_plan")
+        self.o_elems, self.lse_elems = list(o_el), list(l_el)
+        self.nbytes = int(lib.gp_varlen_plan_bytes(len(self.Ls), nb))
+        self.tok_off = [0]
+        for L in self.Ls:
+            self.tok_off.append(self.tok_off[-1] + L)
+        self.host = None
+        self.dev = None
+
+    def bind(self, qkv: torch.Tensor, outs: Sequence[torch.Tensor], lses: Sequence[torch.Tensor]):
+        lib = load_library()
+        _dev(qkv, torch.bfloat16, "qkv")
+        if qkv.shape[0] < self.tok_off[-1] or qkv.shape[1] != 3 * self.H * self.D:
+            raise ValueError("VarlenPlan.bind: qkv must be [>= %d, %d]" % (self.tok_off[-1], 3 * self.H * self.D))
+        for b, (o, l) in enumerate(zip(outs, lses)):
+            _dev(o, torch.bfloat16, "o[%d]" % b); _dev(l, torch.float32, "lse[%d]" % b)
+            if o.numel() < self.o_elems[b] or l.numel() < self.lse_elems[b]:
+                raise ValueError("VarlenPlan.bind: branch %d outputs too small" % b)
+        host = (ctypes.c_uint8 * self.nbytes)()
+        o_el, l_el = (c_i64 * len(self.segs))(), (c_i64 * len(self.segs))()
+        _check(lib.gp_varlen_plan(self._L, len(self.Ls), self.H, self.D, _i32_array(self.segs),
+                                  _i32_array(self.ratios), len(self.segs), _ptr(qkv), 3 * self.H * self.D,
+                                  _ptr_array(outs), _ptr_array(lses), host, self.nbytes, o_el, l_el),
+               "gp_varlen_plan")
+        self.host = host
+        self.dev = torch.frombuffer(bytearray(bytes(host)), dtype=torch.uint8).to(qkv.device)
+        self._keep = (qkv, list(outs), list(lses))
+        return self
+
+
+def dilated_attn_fwd_varlen(plan: VarlenPlan, q_log2_prescaled: bool = True):
+    lib = load_library()
+    _check(lib.gp_dilated_attn_fwd_varlen(plan.host, _ptr(plan.dev), int(bool(q_log2_prescaled)), _stream()),
+           "gp_dilated_attn_fwd_varlen")
+
+
+def branch_merge_ln_varlen(plan: VarlenPlan, ln_w, ln_b, eps, out):
+    lib = load_library()
+    _dev(out, torch.bfloat16, "out")
+    _check(lib.gp_branch_merge_ln_varlen(plan.host, _ptr(plan.dev), _ptr(ln_w), _ptr(ln_b), eps, _ptr(out),
+                                         _stream()), "gp_branch_merge_ln_varlen")

@@ -42,22 +42,44 @@ def lpt_assign(costs: Sequence[float], world: int) -> List[List[int]]:
     return out
 
 
+def pack_groups(sizes: Sequence[int], order: Sequence[int], max_tokens: int) -> List[List[int]]:
+    """Split `order` (slide indices) into consecutive groups of at most max_tokens packed tokens
+    (N_i + 1 each); a slide larger than the budget forms its own group."""
+    groups, cur, tok = [], [], 0
+    for i in order:
+        L = int(sizes[i]) + 1
+        if cur and tok + L > max_tokens:
+            groups.append(cur)
+            cur, tok = [], 0
+        cur.append(i)
+        tok += L
+    if cur:
+        groups.append(cur)
+    return groups
+
+
 def encode_slides(model, slides: Sequence[Tuple[torch.Tensor, torch.Tensor]], all_layer_embed: bool = False,
-                  group=None, encode_fn: Optional[Callable] = None) -> List[List[torch.Tensor]]:
+                  group=None, encode_fn: Optional[Callable] = None, packed: Optional[bool] = None,
+                  max_packed_tokens: int = 1 << 21) -> List[List[torch.Tensor]]:
     """Encode a list of (tile_embed [N_i, C] or [1, N_i, C], coords [N_i, 2] or [1, N_i, 2]) slides.
 
-    Single process: sequential B = 1 forwards.  Under torch.distributed (one process per GPU,
+    Single process: every slide of this rank in one varlen-packed forward (model.forward_packed:
+    per-token work over all slides' rows at once, one attention and one merge launch per layer
+    with per-slide segment tables; groups of at most max_packed_tokens tokens), or, with
+    packed=False or a custom encode_fn, sequential B = 1 forwards.  Under torch.distributed (one process per GPU,
     every rank passing the same list): LPT-sharded across the ranks of `group`, results
     all-reduced so every rank returns every slide's outputs.  Returns, per slide, the list the
     model's forward returns (1 or 1 + depth tensors of [1, E]).
 
-    With ``model.use_hip_graphs`` each slide is a replay of its shape's captured forward.  The
-    replays run one after another on one stream: replaying graphs of different slides concurrently
-    on several streams hung the GPU on MI355X (32 slides over 4 streams; GEMM kernels that assume
-    their workgroups are co-resident are the suspect), so there is no cross-slide concurrency."""
+    With ``model.use_hip_graphs`` each forward (packed group or slide) is a replay of its captured
+    graph, one after another on one stream: replaying graphs of different slides concurrently on
+    several streams hung the GPU on MI355X (32 slides over 4 streams; GEMM kernels that assume
+    their workgroups are co-resident are the suspect) -- packing is the cross-slide batching."""
     import torch.distributed as dist
     if getattr(model, "_sp", None) is not None:
         raise ValueError("encode_slides is data parallel: call model.disable_sequence_parallel() first")
+    if packed is None:
+        packed = encode_fn is None and hasattr(model, "forward_packed")
     encode_fn = encode_fn or (lambda x, c: model(x, c, all_layer_embed=all_layer_embed))
     dist_on = dist.is_available() and dist.is_initialized()
     world = dist.get_world_size(group) if dist_on else 1
@@ -79,10 +101,16 @@ def encode_slides(model, slides: Sequence[Tuple[torch.Tensor, torch.Tensor]], al
         return x, (c if c.dtype in (torch.float32, torch.float64) else c.float())
 
     with torch.no_grad():
-        for i in mine:
-            x, c = shaped(i)
-            outs = encode_fn(x, c)
-            table[i] = torch.stack([o.reshape(E).float() for o in outs])
+        if packed:
+            for grp in pack_groups(sizes, mine, max_packed_tokens):
+                outs = model.forward_packed([slides[i] for i in grp], all_layer_embed)
+                for i, o in zip(grp, outs):
+                    table[i] = torch.stack([t.reshape(E).float() for t in o])
+        else:
+            for i in mine:
+                x, c = shaped(i)
+                outs = encode_fn(x, c)
+                table[i] = torch.stack([o.reshape(E).float() for o in outs])
     if world > 1:
         if dist.get_backend(group) == "nccl" or not table.is_cuda:
             dist.all_reduce(table, group=group)

@@ -220,10 +220,31 @@ class AttentionScratch:
             self.lses.append(torch.empty(B * nseg * H * m, dtype=torch.float32, device=dev))
 
 
+class VarlenScratch:
+    """Packed per-branch outputs of several slides (slide-major regions) and the varlen work table
+    bound to one qkv buffer (config C5 packing, _hip.VarlenPlan)."""
+
+    def __init__(self, dev, Ls: Sequence[int], H: int, D: int, segs, ratios, qkv: torch.Tensor):
+        self.plan = _hip.VarlenPlan(Ls, H, D, segs, ratios)
+        self.outs = [torch.empty(n, dtype=torch.bfloat16, device=dev) for n in self.plan.o_elems]
+        self.lses = [torch.empty(n, dtype=torch.float32, device=dev) for n in self.plan.lse_elems]
+        self.plan.bind(qkv, self.outs, self.lses)
+
+
 def dilated_attention_core(pa: PackedAttention, qkv: torch.Tensor, B: int, L: int, scratch: AttentionScratch,
                            out: torch.Tensor, inner_ln: bool = True):
-    """qkv: [B*L, 3E] bf16 (q | k | v); out: [B*L, E] bf16 = inner_attn_ln(merge(branches))."""
+    """qkv: [B*L, 3E] bf16 (q | k | v); out: [B*L, E] bf16 = inner_attn_ln(merge(branches)).
+    With a VarlenScratch (bound to this qkv), every packed slide in one launch each."""
     E, H, D = pa.E, pa.H, pa.D
+    if isinstance(scratch, VarlenScratch):
+        if not pa.prescaled:
+            raise RuntimeError("varlen packing needs the pre-scaled q of D = 48")
+        with TIMER.span("attn"):
+            _hip.dilated_attn_fwd_varlen(scratch.plan, True)
+        with TIMER.span("merge"):
+            _hip.branch_merge_ln_varlen(scratch.plan, pa.ln_w if inner_ln else None, pa.ln_b if inner_ln else None,
+                                        pa.ln_eps, out)
+        return
     with TIMER.span("attn"):
         _hip.dilated_attn_fwd(qkv, qkv[:, E:], qkv[:, 2 * E:], 3 * E, B, L, H, D, pa.segs, pa.ratios,
                               scratch.outs, scratch.lses, 0.0, pa.prescaled)
@@ -247,6 +268,25 @@ class Workspace:
         self.attn = AttentionScratch(dev, B, L, H, E // H, segs, ratios)
 
 
+class PackedWorkspace(Workspace):
+    """Workspace of several slides packed token-major: T = sum(L_i) rows, slide i at rows
+    [tok_off[i], tok_off[i] + L_i) with its CLS first; attention through a VarlenScratch."""
+
+    def __init__(self, dev, Ls: Sequence[int], E: int, F: int, H: int, segs, ratios):
+        self.Ls = [int(x) for x in Ls]
+        T = sum(self.Ls)
+        M = T
+        self.key = (str(dev), tuple(self.Ls), E, F, H, tuple(segs), tuple(ratios))
+        self.x = torch.empty(M, E, dtype=torch.float32, device=dev)
+        self.a = torch.empty(M, E, dtype=torch.bfloat16, device=dev)
+        self.qkv = torch.empty(M, 3 * E, dtype=torch.bfloat16, device=dev)
+        self.y = torch.empty(M, E, dtype=torch.bfloat16, device=dev)
+        self.f = torch.empty(M, F, dtype=torch.bfloat16, device=dev)
+        self.attn = VarlenScratch(dev, self.Ls, H, E // H, segs, ratios, self.qkv)
+        self.tok_off = self.attn.plan.tok_off
+        self.cls_idx = torch.tensor(self.tok_off[:-1], dtype=torch.int64, device=dev)
+
+
 class EncoderEngine:
     """Runs the 12-layer (or 24-) LongNet stack on one device for inputs already embedded."""
 
@@ -254,6 +294,7 @@ class EncoderEngine:
         self._sig = None
         self.layers: List[PackedLayer] = []
         self.ws: Optional[Workspace] = None
+        self.pws: Optional[PackedWorkspace] = None
 
     def pack(self, encoder, dev):
         use_tuned_gemms(dev)
@@ -269,6 +310,13 @@ class EncoderEngine:
             self.ws = None
             self.ws = Workspace(dev, B, L, E, F, H, segs, ratios)
         return self.ws
+
+    def workspace_packed(self, dev, Ls, E, F, H, segs, ratios) -> PackedWorkspace:
+        key = (str(dev), tuple(int(x) for x in Ls), E, F, H, tuple(segs), tuple(ratios))
+        if self.pws is None or self.pws.key != key:
+            self.pws = None
+            self.pws = PackedWorkspace(dev, Ls, E, F, H, segs, ratios)
+        return self.pws
 
     def run_layers(self, ws: Workspace, B: int, L: int, layer_hook=None):
         """ws.x holds the fp32 embedding and ws.a = LN1_0(ws.x) (bf16).  Runs every layer in

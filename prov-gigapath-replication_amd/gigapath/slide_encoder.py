@@ -229,28 +229,138 @@ class LongNetViT(nn.Module):
                self._top_sig, self.encoder.engine._sig)
         ent = self._graphs.get(key)
         if ent is None:
-            ent = self._capture(key, x, c, all_layer_embed, self.graph_stream())
+            ent = self._capture(key, x, c, lambda sx, sc: self._forward_device(sx, sc, all_layer_embed, False))
         return ent
 
-    def _capture(self, key, x, c, all_layer_embed, stream):
+    def _capture(self, key, x, c, run):
+        """Capture run(static_x, static_coords) -> outputs on the side stream (after one eager
+        warm-up run there: allocations, TunableOp lookups) and cache it under `key`."""
         while len(self._graphs) >= self.max_hip_graphs:          # oldest first (insertion order)
             old = next(iter(self._graphs))
             self._graphs.pop(old)
             self._graph_ws.pop(old, None)
+        stream = self.graph_stream()
         sx, sc = x.detach().clone(), c.detach().clone().contiguous()
         cur = torch.cuda.current_stream()
         stream.wait_stream(cur)
-        with torch.cuda.stream(stream):                           # warm-up: allocations, TunableOp lookups
-            self._forward_device(sx, sc, all_layer_embed, False)
+        with torch.cuda.stream(stream):
+            run(sx, sc)
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph, stream=stream, capture_error_mode="thread_local"):
-            outs = self._forward_device(sx, sc, all_layer_embed, False)
+            outs = run(sx, sc)
         cur.wait_stream(stream)
-        # the graph bakes this shape's workspace: keep it alive with the graph
+        # the graph bakes this shape's workspace(s): keep them alive with the graph
         ent = (graph, sx, sc, outs)
         self._graphs[key] = ent
-        self._graph_ws[key] = self.encoder.engine.ws
+        self._graph_ws[key] = (self.encoder.engine.ws, self.encoder.engine.pws)
         return ent
+
+    # ---------------------------------------------------------------- varlen packing (C5)
+    def forward_packed(self, slides, all_layer_embed=False):
+        """Several slides in ONE forward (config C5 "varlen segment packing").
+
+        slides: [(x_i [N_i, C] or [1, N_i, C], coords_i [N_i, 2] or [1, N_i, 2]), ...].  The tokens
+        of all slides are packed into T = sum(N_i + 1) rows (each slide's CLS first); every
+        per-token op (GEMMs, LNs, GELU, residuals) runs once over the T rows, and the dilated
+        attention and branch merge run as one varlen launch each in which every slide keeps its
+        own segment schedule (s = min(sl, L_i), no cross-slide attention).  Each slide's outputs
+        are therefore those of its own B = 1 forward (up to the GEMMs' row-count-dependent
+        rounding).  Returns one output list per slide, as forward(x_i[None], c_i[None])."""
+        self.encoder.check_eval()
+        dev = self.cls_token.device
+        xs, cs = [], []
+        for x, c in slides:
+            x = x[0] if x.dim() == 3 else x
+            c = c[0] if c.dim() == 3 else c
+            if x.device != dev or c.device != dev:
+                raise RuntimeError("forward_packed: slides must be on the model's device %s" % dev)
+            if c.shape != (x.shape[0], 2):
+                raise ValueError("forward_packed: coords must be [N, 2] per slide")
+            xs.append(x)
+            cs.append(c if c.dtype in (torch.float32, torch.float64) else c.float())
+        if not xs:
+            return []
+        if self._sp is not None and self._sp.world > 1:
+            raise ValueError("forward_packed is single-device: disable sequence parallelism first")
+        if self.encoder.layers[0].self_attn.head_dim != 48 or len({c.dtype for c in cs}) != 1 or \
+                len({x.dtype for x in xs}) != 1:
+            # the varlen kernels cover D = 48 (the 12L768d arch): other archs run slide by slide
+            return [self.forward(x[None], c[None], all_layer_embed) for x, c in zip(xs, cs)]
+        Ns = tuple(int(x.shape[0]) for x in xs)
+        x_cat = torch.cat(xs, 0)
+        c_cat = torch.cat(cs, 0)
+        if self.validate_positions:
+            self.check_positions([c_cat])
+        if self.use_hip_graphs and not runtime.TIMER.enabled:
+            self._packed_top(dev)
+            self.encoder.engine.pack(self.encoder, dev)
+            key = ("packed", str(dev), Ns, x_cat.dtype, c_cat.dtype, bool(all_layer_embed), bool(self.global_pool),
+                   self._top_sig, self.encoder.engine._sig)
+            ent = self._graphs.get(key)
+            if ent is None:
+                ent = self._capture(key, x_cat, c_cat,
+                                    lambda sx, sc: self._forward_packed_device(sx, sc, Ns, all_layer_embed))
+            graph, sx, sc, res = ent
+            sx.copy_(x_cat)
+            sc.copy_(c_cat)
+            graph.replay()
+            res = res.clone()
+        else:
+            res = self._forward_packed_device(x_cat, c_cat, Ns, all_layer_embed)
+        out_dtype = self.norm.weight.dtype
+        return [[res[k, i:i + 1].to(out_dtype) for k in range(res.shape[0])] for i in range(len(Ns))]
+
+    def _forward_packed_device(self, x_cat, c_cat, Ns, all_layer_embed):
+        """Eager packed forward (captured as is by forward_packed): x_cat [sum N_i, C], c_cat
+        [sum N_i, 2] -> [n_out, S, E] fp32."""
+        dev = self.cls_token.device
+        E, S = self.embed_dim, len(Ns)
+        Ls = [n + 1 for n in Ns]
+        top = self._packed_top(dev)
+        eng = self.encoder.engine
+        layers = eng.pack(self.encoder, dev)
+        pa = layers[0].attn
+        ws = eng.workspace_packed(dev, Ls, E, self.encoder.args.encoder_ffn_embed_dim, pa.H, pa.segs, pa.ratios)
+        Nt, T = int(sum(Ns)), int(sum(Ls))
+        if not hasattr(ws, "pos"):
+            ws.pos = torch.empty(Nt, dtype=torch.int64, device=dev)
+        xp = ws.y[:Nt]
+        with runtime.TIMER.span("gemm_patch"):
+            torch.addmm(top["bp"], x_cat.to(torch.bfloat16), top["wp"].t(), out=xp)
+        _hip.coords_to_pos(c_cat.contiguous(), self.slide_ngrids, self.tile_size, ws.pos, None)
+        with runtime.TIMER.span("posembed"):
+            n0 = 0
+            for i, n in enumerate(Ns):            # slide i's CLS + tiles -> packed rows tok_off[i] ..
+                t0 = ws.tok_off[i]
+                _hip.posembed_cls_ln(xp[n0:n0 + n], ws.pos[n0:n0 + n], top["tab"], top["cls"], 1, n, E,
+                                     self.slide_ngrids, top["ln1_w"], top["ln1_b"], top["ln1_eps"],
+                                     ws.x[t0:t0 + n + 1], ws.a[t0:t0 + n + 1])
+                n0 += n
+        n_out = (1 + len(layers)) if all_layer_embed else 1
+        res = torch.empty(n_out, S, E, dtype=torch.float32, device=dev)
+        pool = torch.empty(S, E, dtype=torch.float32, device=dev)
+
+        def readout(slot: int):
+            if self.global_pool:
+                for i, L in enumerate(Ls):
+                    t0 = ws.tok_off[i]
+                    _hip.mean_tokens(ws.x[t0:t0 + L], 1, L, E, 1, pool[i:i + 1])
+            else:
+                torch.index_select(ws.x, 0, ws.cls_idx, out=pool)
+            _hip.layernorm_f32(pool, E, top["norm_w"], top["norm_b"], top["norm_eps"], res[slot], S, E)
+
+        if all_layer_embed:
+            readout(0)
+        eng.run_layers(ws, 1, T, readout if all_layer_embed else None)
+        if not all_layer_embed:
+            if self.global_pool:
+                _hip.layernorm_f32(ws.x, E, top["enc_w"], top["enc_b"], top["enc_eps"], ws.x, T, E)
+                readout(0)
+            else:
+                cls_rows = torch.index_select(ws.x, 0, ws.cls_idx)
+                _hip.layernorm_f32(cls_rows, E, top["enc_w"], top["enc_b"], top["enc_eps"], cls_rows, S, E)
+                _hip.layernorm_f32(cls_rows, E, top["norm_w"], top["norm_b"], top["norm_eps"], res[0], S, E)
+        return res
 
     def _forward_device(self, x, coords, all_layer_embed, validate):
         """The eager forward: every launch on the current stream (captured as is by _capture)."""

@@ -78,6 +78,32 @@ def test_argument_errors_are_reported_without_gpu():
     assert rc == -1
 
 
+def test_varlen_plan_host_side():
+    """gp_varlen_plan is host-only: sizes of the packed per-branch outputs follow each slide's own
+    schedule (runtime.branch_geometry), the plan header is checked before any launch."""
+    _lib_path()
+    from gigapath import _hip, runtime
+    segs, ratios = [1024, 5792, 32768, 185363, 1048576], [1, 2, 4, 8, 16]
+    Ls = [1025, 2897, 700, 70001, 6001]
+    plan = _hip.VarlenPlan(Ls, 16, 48, segs, ratios)
+    for b, (sl, r) in enumerate(zip(segs, ratios)):
+        geo = [runtime.branch_geometry(L, sl, r) for L in Ls]
+        assert plan.o_elems[b] == sum(n * m * 16 * 48 for _, n, m in geo)
+        assert plan.lse_elems[b] == sum(n * 16 * m for _, n, m in geo)
+    assert plan.tok_off == [0, 1025, 3922, 4622, 74623, 80624]
+    assert plan.nbytes > 0 and plan.nbytes % 16 == 0
+    lib = _hip.load_library()
+    assert lib.gp_varlen_plan_bytes(0, 5) == -1
+    fake = (ctypes.c_uint8 * 64)()
+    rc = lib.gp_dilated_attn_fwd_varlen(fake, 16, 1, None)
+    assert rc == -1 and b"not a gp_varlen_plan" in lib.gp_last_error_string()
+    L_bad = (ctypes.c_int64 * 1)(0)
+    el = (ctypes.c_int64 * 5)()
+    rc = lib.gp_varlen_plan(L_bad, 1, 16, 48, (ctypes.c_int32 * 5)(*segs), (ctypes.c_int32 * 5)(*ratios), 5,
+                            None, 2304, None, None, None, 0, el, el)
+    assert rc == -1 and b"L = 0" in lib.gp_last_error_string()
+
+
 # ------------------------------------------------------------------ Python drop-in surface
 @pytest.fixture(scope="module")
 def model():

@@ -34,6 +34,18 @@ def test_lpt_assignment_balances_and_covers():
             assert [costs[i] for i in r] == sorted((costs[i] for i in r), reverse=True)
 
 
+def test_pack_groups_respect_the_token_budget():
+    sizes = batch.mixed_batch_sizes()
+    order = list(range(len(sizes)))
+    for budget in (50000, 200000, 1 << 21):
+        groups = batch.pack_groups(sizes, order, budget)
+        assert [i for g in groups for i in g] == order            # order kept, every slide once
+        for g in groups:
+            assert len(g) == 1 or sum(sizes[i] + 1 for i in g) <= budget
+    assert len(batch.pack_groups(sizes, order, 1 << 21)) == 1       # the whole C5 batch fits one pack
+    assert batch.pack_groups([10, 10], [0, 1], 5) == [[0], [1]]     # oversize slides stand alone
+
+
 def test_cost_grows_superlinearly_with_tiles():
     c1, c2 = batch.slide_cost(10000, SEGS, RATIOS), batch.slide_cost(100000, SEGS, RATIOS)
     assert c2 > 10 * c1
