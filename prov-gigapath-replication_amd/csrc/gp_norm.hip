@@ -233,6 +233,98 @@ __global__ __launch_bounds__(256) void gelu_ln_wave_kernel(const uint16_t* h, co
   }
 }
 
+// GELU + LN v2, one wave per row, grid-stride over rows with the NEXT row's 16-byte loads
+// issued before the current row's math (memory-level parallelism at the occupancy the
+// registers allow).  The GELU outputs are rounded to bf16 in place -- as the reference's
+// gelu(x.float()).type_as(x) does before ffn_layernorm (feedforward_network.py:135-137) -- so
+// a row lives in EPL/2 registers, and the LN statistics are taken over those rounded values.
+GP_DEV void unpack8(const uint4 u, float* v) {
+  const uint32_t w4[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w4[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w4[i] & 0xffff0000u);
+  }
+}
+GP_DEV uint4 pack8(const float* v) {
+  uint4 u;
+  u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+  u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+  u.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+  u.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+  return u;
+}
+
+template <int EPL>
+__global__ __launch_bounds__(256) void gelu_ln_wave2_kernel(const uint16_t* h, const float* __restrict__ ln_w,
+                                                            const float* __restrict__ ln_b, float eps,
+                                                            uint16_t* out, int64_t rows) {
+  constexpr int C = 64 * EPL, NK = EPL / 8;
+  // LN weights in LDS once per block (in registers they would be loop-invariant across the
+  // grid-stride loop: 2*EPL VGPRs held for the whole kernel)
+  __shared__ __attribute__((aligned(16))) float sw[C], sb[C];
+  for (int i = threadIdx.x * 4; i < C; i += 256 * 4) {
+    *reinterpret_cast<float4*>(sw + i) = *reinterpret_cast<const float4*>(ln_w + i);
+    *reinterpret_cast<float4*>(sb + i) = *reinterpret_cast<const float4*>(ln_b + i);
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int64_t stride = (int64_t)gridDim.x * 4;
+  int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  uint4 cur[NK], nxt[NK];
+  if (row < rows) {
+#pragma unroll
+    for (int k = 0; k < NK; ++k) cur[k] = *reinterpret_cast<const uint4*>(h + row * C + k * 512 + 8 * lane);
+  }
+  for (; row < rows; row += stride) {
+    if (row + stride < rows) {
+#pragma unroll
+      for (int k = 0; k < NK; ++k)
+        nxt[k] = *reinterpret_cast<const uint4*>(h + (row + stride) * C + k * 512 + 8 * lane);
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      float v[8];
+      unpack8(cur[k], v);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = gelu_erf(v[i]);
+      cur[k] = pack8(v);
+      unpack8(cur[k], v);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s += v[i];
+      __builtin_amdgcn_sched_barrier(0);   // one chunk's GELU temporaries live at a time
+    }
+    const float mean = wave_sum(s) / (float)C;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      float v[8];
+      unpack8(cur[k], v);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float d = v[i] - mean;
+        q += d * d;
+      }
+    }
+    const float rstd = rsqrtf(wave_sum(q) / (float)C + eps);
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      float v[8], wv[8], bv[8];
+      unpack8(cur[k], v);
+      *reinterpret_cast<float4*>(wv) = *reinterpret_cast<const float4*>(sw + k * 512 + 8 * lane);
+      *reinterpret_cast<float4*>(wv + 4) = *reinterpret_cast<const float4*>(sw + k * 512 + 8 * lane + 4);
+      *reinterpret_cast<float4*>(bv) = *reinterpret_cast<const float4*>(sb + k * 512 + 8 * lane);
+      *reinterpret_cast<float4*>(bv + 4) = *reinterpret_cast<const float4*>(sb + k * 512 + 8 * lane + 4);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = (v[i] - mean) * rstd * wv[i] + bv[i];
+      *reinterpret_cast<uint4*>(out + row * C + k * 512 + 8 * lane) = pack8(v);
+    }
+#pragma unroll
+    for (int k = 0; k < NK; ++k) cur[k] = nxt[k];
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 template <int EPL>
 __global__ __launch_bounds__(256) void layernorm_f32_kernel(const float* __restrict__ x, int64_t row_stride,
@@ -340,8 +432,19 @@ extern "C" int gp_gelu_layernorm(const uint16_t* h, const float* ln_w, const flo
   GP_REQUIRE(h && ln_w && ln_b && out, "gp_gelu_layernorm: null pointer");
   hipStream_t s = gp_stream(stream);
   GP_REQUIRE(rows < (int64_t)0x7fffffff, "gp_gelu_layernorm: too many rows");
-  const char* impl = getenv("GP_GELU_IMPL");    // A/B: 1 = block-per-row kernel
-  if (impl && atoi(impl) == 1) {
+  const char* impl_env = getenv("GP_GELU_IMPL");    // A/B: 1 = block per row, 2 = wave per row (v1)
+  const int impl = impl_env ? atoi(impl_env) : 3;
+  if (impl == 3) {     // default: wave per row, grid-stride with next-row prefetch, bf16-rounded GELU
+    const int64_t want = (rows + 3) / 4;
+    const unsigned nb = (unsigned)(want < 1024 ? want : 1024);
+    switch (cols / 64) {
+      case 48: gelu_ln_wave2_kernel<48><<<nb, 256, 0, s>>>(h, ln_w, ln_b, eps, out, rows); break;
+      case 64: gelu_ln_wave2_kernel<64><<<nb, 256, 0, s>>>(h, ln_w, ln_b, eps, out, rows); break;
+      case 96: gelu_ln_wave2_kernel<96><<<nb, 256, 0, s>>>(h, ln_w, ln_b, eps, out, rows); break;
+    }
+    return gp_check_launch("gp_gelu_layernorm");
+  }
+  if (impl == 1) {
     switch (cols / 256) {
       case 12: gelu_ln_kernel<12><<<(unsigned)rows, 256, 0, s>>>(h, ln_w, ln_b, eps, out, rows, cols); break;
       case 16: gelu_ln_kernel<16><<<(unsigned)rows, 256, 0, s>>>(h, ln_w, ln_b, eps, out, rows, cols); break;

@@ -300,6 +300,22 @@ def test_branch_merge_vs_oracle(name, B, L, segs, ratios, with_ln):
 
 
 # ------------------------------------------------------------------ row kernels
+@pytest.mark.parametrize("F", [3072, 4096, 6144])
+def test_gelu_layernorm_grid_stride_rows(F):
+    """Enough rows that every wave walks several (grid-stride + next-row prefetch), in place."""
+    h = _hip()
+    g = torch.Generator().manual_seed(F)
+    M = 9001
+    f = (torch.randn(M, F, generator=g) * 2).bfloat16()
+    fw = 1 + 0.1 * torch.randn(F, generator=g)
+    fb = 0.1 * torch.randn(F, generator=g)
+    fd = f.to(DEV)
+    h.gelu_layernorm(fd, fw.to(DEV), fb.to(DEV), 1e-5, fd, M, F)
+    ref = torch.nn.functional.layer_norm(torch.nn.functional.gelu(f.float()).bfloat16().float(), (F,), fw, fb, 1e-5)
+    err = (fd.float().cpu() - ref).abs().max().item()
+    assert err <= 2 ** -8 * ref.abs().max().item(), err
+
+
 def test_residual_gelu_layernorm_kernels():
     h = _hip()
     rng = np.random.default_rng(0)
@@ -324,6 +340,11 @@ def test_residual_gelu_layernorm_kernels():
     h.gelu_layernorm(fd, fw.to(DEV), fb.to(DEV), 1e-5, fd, M, F)     # in place
     f_ref = torch.nn.functional.layer_norm(torch.nn.functional.gelu(f.float()), (F,), fw, fb, 1e-5)
     assert (fd.float().cpu() - f_ref).abs().max().item() <= 2 ** -7 * f_ref.abs().max().item()
+
+    # the reference's bf16 semantics: gelu(x.float()).type_as(x) rounds to bf16 before the LN
+    f_ref16 = torch.nn.functional.layer_norm(torch.nn.functional.gelu(f.float()).bfloat16().float(), (F,), fw, fb,
+                                             1e-5)
+    assert (fd.float().cpu() - f_ref16).abs().max().item() <= 2 ** -8 * f_ref16.abs().max().item()
 
     out = torch.empty(4, E, dtype=torch.float32, device=DEV)
     h.layernorm_f32(xd, 80 * E, w.to(DEV), b.to(DEV), 1e-6, out, 4, E)       # rows 0, 80, 160, 240

@@ -18,11 +18,14 @@ ap.add_argument("--L", type=int, default=70001)
 ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--impls", default="2p,3p")
 ap.add_argument("--D", type=int, default=48)
+ap.add_argument("--branches", default="0,1,2,3,4", help="subset of the 5 branches to run")
 args = ap.parse_args()
 H, D = 16, args.D
 E = H * D
 L = args.L
 segs, ratios = [1024, 5792, 32768, 185363, 1048576], [1, 2, 4, 8, 16]
+_sel = [int(b) for b in args.branches.split(",")]
+segs, ratios = [segs[b] for b in _sel], [ratios[b] for b in _sel]
 g = torch.Generator(device="cuda").manual_seed(0)
 qkv = torch.randn(L, 3 * E, device="cuda", generator=g)
 qkv[:, :E] *= 0.35      # typical projected-q scale so pre-scaled logits stay in a realistic range
