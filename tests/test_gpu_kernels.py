@@ -183,10 +183,15 @@ def test_dilated_attention_vs_oracle(name, B, L, segs, ratios, attn_impl):
 LSE_ATOL = 2.5e-3
 
 
-@pytest.mark.parametrize("impl", ["2", "3"])
+@pytest.mark.parametrize("impl", ["2", "3", "2@2", "4@7"])
 @pytest.mark.parametrize("name,B,L,segs,ratios", ATTN_CASES)
 def test_dilated_attention_prescaled_q(name, B, L, segs, ratios, impl, monkeypatch):
-    monkeypatch.setenv("GP_ATTN_IMPL", impl)
+    # "2": the default (buffer-descriptor staging); "2@2": global-load staging; "4@7": two query
+    # blocks per wave; "3": software-pipelined
+    base, _, var = impl.partition("@")
+    monkeypatch.setenv("GP_ATTN_IMPL", base)
+    if var:
+        monkeypatch.setenv("GP_ATTN_VAR", var)
     """Product path: q pre-multiplied by D^-0.5 * log2(e) (folded into the Q projection)."""
     h = _hip()
     H, D = 16, 48
