@@ -117,7 +117,7 @@ def main():
         args.tiles = 256000 if sp else 70000
     # GP_BENCH_BACKEND=gloo: rehearsal of the multi-rank path with several ranks on one GPU
     backend = os.environ.get("GP_BENCH_BACKEND", "nccl")
-    if backend != "nccl":
+    if backend != "nccl":                  # (RCCL refuses two ranks on one GPU: gloo only)
         local = local % torch.cuda.device_count()
     if world > 1:
         import torch.distributed as dist

@@ -449,6 +449,10 @@ class SeqParallelContext:
 
     def prepare(self, dev, L: int, segs, ratios, H: int, D: int, F: int):
         key = (str(dev), L, tuple(segs), tuple(ratios), H, D, F)
+        if self._key is None:
+            # a collective every rank joins before any point-to-point call: with RCCL the first
+            # P2P on a communicator must not be the first call of the group (torch batch_isend_irecv)
+            self.exchange.all_reduce_(torch.zeros(1, device=dev))
         if key != self._key:
             self.plan = ShardPlan(L, self.world, segs, ratios, H, D, F)
             self.ws = ShardWorkspace(self.plan, self.rank, dev, F)
