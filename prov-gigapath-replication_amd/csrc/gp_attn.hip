@@ -484,8 +484,51 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
       lvo[u] = (int)(tsel * kv_dv + (int64_t)(rem / CH) * kvstride * 2 + (rem % CH) * 16);
     }
   }
+  // VAR & 8192: LDS-DMA staging -- buffer_load ... lds writes each 1 KiB piece (64 lanes x 16 B,
+  // lane-linear) straight into the tile image: no stage registers, no ds_write pass.  K image:
+  // 7 pieces (112-B rows = 6 chunks + 1 pad unit, pad lanes off); V image: 8 pieces (128-B
+  // rows, swizzled 32-B blocks; the lanes of the bf16-ones block are off, the prologue wrote
+  // it).  Piece p of the 15 goes to wave p % 4.
+  constexpr bool kDMA = (VAR & 8192) != 0;
+  static_assert(!kDMA || (D == 48 && NW == 4 && KT == 64 && (VAR & 2048) != 0 && !kMK),
+                "VAR 8192 needs D = 48, 4 waves, 64-key tiles and VAR 2048");
+  constexpr int kPieces = (KT * KROWB + KT * VROWB) / 1024;      // 15
+  int dvo[4];
+  unsigned dmask = 0;
+  if constexpr (kDMA) {
+#pragma unroll
+    for (int sl = 0; sl < 4; ++sl) {
+      const int pc = w + 4 * sl;
+      dvo[sl] = 0;
+      if (pc >= kPieces) continue;
+      if (pc < KTILE / 1024) {
+        const int unit = pc * 64 + lane, row = unit / 7, ch = unit % 7;
+        dvo[sl] = (int)((int64_t)row * kvstride * 2 + (ch < 6 ? ch : 0) * 16);
+        if (ch < 6) dmask |= 1u << sl;
+      } else {
+        const int unit = (pc - KTILE / 1024) * 64 + lane, row = unit / 8, slot = unit % 8;
+        const int b = (slot >> 1) ^ (row & 3);
+        dvo[sl] = (int)(kv_dv + (int64_t)row * kvstride * 2 + (2 * (b < 3 ? b : 0) + (slot & 1)) * 16);
+        if (b < 3) dmask |= 1u << sl;
+      }
+    }
+  }
   auto load_tile = [&](int kv0) {
-    if constexpr ((VAR & 2048) != 0) {
+    if constexpr (kDMA) {
+      const int64_t tb = (int64_t)kv0 * kvstride * 2;
+      const int64_t nrec = (int64_t)(c - kv0 - 1) * kvstride * 2 + kv_dv + 2 * D;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)((const char*)kbase + tb), (short)0, (int)(nrec < 0x7fffffff ? nrec : 0x7fffffff), 0x00020000);
+      char* bufp = smem + ((kv0 / KT) & 1) * BUF;
+#pragma unroll
+      for (int sl = 0; sl < 4; ++sl) {
+        const int pc = w + 4 * sl;
+        if (pc < kPieces && ((dmask >> sl) & 1u))
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(
+              rs, (__attribute__((address_space(3))) void*)(bufp + (pc < KTILE / 1024 ? pc * 1024 : KTILE + (pc - KTILE / 1024) * 1024)),
+              16, dvo[sl], 0, 0, 0);
+      }
+    } else if constexpr ((VAR & 2048) != 0) {
       // buffer loads through a per-tile descriptor whose record count ends at the last valid key
       // row: rows past c read as zero in hardware (no branch, no zero-filled stage registers,
       // so the compiler has no reason to wait on the loads before the tile's compute)
@@ -527,6 +570,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
     }
   };
   auto store_tile = [&](int buf) {
+    if constexpr (kDMA) return;
 #pragma unroll
     for (int u = 0; u < LPT; ++u) {
       int off;
@@ -607,7 +651,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
     // no barrier / no exp
     if constexpr (kPF2) {
       if (t + 2 < ntiles) load_into(stage2[SET], (t + 2) * KT);
-    } else {
+    } else if constexpr ((VAR & 16384) == 0) {
       if (t + 1 < ntiles && (VAR & 128) == 0) load_tile((t + 1) * KT);
     }
 #pragma unroll
@@ -795,6 +839,13 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
     } else {
       if (t + 1 < ntiles && (VAR & 128) == 0) store_tile((t + 1) & 1);
     }
+    // VAR & 16384 (with 8192): issue the next tile's DMA after this tile's last LDS read -- the
+    // compiler orders every LDS read after any in-flight LDS-DMA (vmcnt(0)), so an early issue
+    // makes the V reads wait for it
+    if constexpr ((VAR & 16384) != 0) {
+      if (t + 1 < ntiles) load_tile((t + 1) * KT);
+    }
+    if constexpr (kDMA) __builtin_amdgcn_s_waitcnt(0x0f70);   // this wave's DMA pieces landed
     if constexpr ((VAR & 256) == 0) __syncthreads();
     };
   if constexpr (kPF2) {
@@ -1764,6 +1815,11 @@ extern "C" int gp_dilated_attn_fwd_ex(const uint16_t* q, int64_t q_row_stride, i
       case 1538: dilated_attn32_kernel<48, true, 8, 1538><<<(unsigned)items, 512, 0, s>>>(a); break;
       case 1026: dilated_attn32_kernel<48, true, 4, 1026><<<(unsigned)items, 256, 0, s>>>(a); break;
       case 2050: dilated_attn32_kernel<48, true, 4, 2050><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 10242: dilated_attn32_kernel<48, true, 4, 10242><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 10243: dilated_attn32_kernel<48, true, 4, 10242, 5><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 26626: dilated_attn32_kernel<48, true, 4, 26626><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 26627: dilated_attn32_kernel<48, true, 4, 26626, 5><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 14338: dilated_attn32_kernel<48, true, 4, 14338><<<(unsigned)items, 256, 0, s>>>(a); break;
       case 6146: dilated_attn32_kernel<48, true, 4, 6146><<<(unsigned)items, 256, 0, s>>>(a); break;
       case 6150: dilated_attn32_kernel<48, true, 4, 6150><<<(unsigned)items, 256, 0, s>>>(a); break;
       case 2562: dilated_attn32_kernel<48, true, 8, 2562><<<(unsigned)items, 512, 0, s>>>(a); break;
