@@ -200,6 +200,11 @@ int gp_dilated_attn_fwd_varlen(const void* plan_host, const void* plan_dev, int 
 int gp_branch_merge_ln_varlen(const void* plan_host, const void* plan_dev, const float* ln_w,
                               const float* ln_b, float eps, uint16_t* out, void* stream);
 
+/* Diagnostics: per-segment in-kernel cycle sums (s_memtime stamps) of the attention kernel's
+ * stamped build (GP_ATTN_VAR=34818), summed over waves: [S MFMAs, softmax, PV, stage store,
+ * barrier, whole wave, tiles, waves].  reset != 0 zeroes them.  Not used by the forward. */
+int gp_debug_attn_stamps(int64_t* out8, int reset);
+
 /* Residual add fused with the next pre-LN (encoder.py:141,147 / :159,126):
  *   x += y + bias (fp32 residual stream, in place);  ln_out = LayerNorm(x) (skipped if ln_w == NULL).
  * x: [rows, cols] fp32; y: [rows, cols] bf16 (GEMM output without bias); bias: [cols] fp32 or NULL;

@@ -364,6 +364,17 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 GP_DEV float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// Diagnostic in-kernel cycle stamps (VAR & 32768 builds only; read with gp_debug_attn_stamps):
+// per wave, cycles spent between fixed points of each tile, summed over all waves.
+__device__ unsigned long long g_attn_stamps[8];
+GP_DEV unsigned long long stamp_now() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+
 // VAR bits (A/B variants, all numerically identical): 1 = S's first k-step takes its C operand
 // from a persistent -m_run block (no per-tile accumulator init), 2 = staging addresses computed
 // once (no per-tile 64-bit index math, no bound checks on full tiles), 4 = all K fragments read
@@ -644,9 +655,21 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
   // prefetch -- before the first MFMA of every tile
   __builtin_amdgcn_s_waitcnt(0x0f70);
 
+  constexpr bool kStamp = (VAR & 32768) != 0;
+  unsigned long long sacc_t[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long t_prev = 0;
+  auto mark = [&](int seg) {
+    if constexpr (kStamp) {
+      const unsigned long long now = stamp_now();
+      if (seg >= 0) sacc_t[seg] += now - t_prev;
+      t_prev = now;
+    }
+  };
+  const unsigned long long t_kernel0 = kStamp ? stamp_now() : 0;
   auto tile_step = [&](int t, auto setc) {
     constexpr int SET = decltype(setc)::value;
     (void)SET;
+    mark(-1);
     // VAR 128/256/64: timing-only ablations (wrong results): no K/V streaming after tile 0 /
     // no barrier / no exp
     if constexpr (kPF2) {
@@ -708,6 +731,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
         sacc[u] = acc;
       }
       if constexpr ((VAR & 32) != 0) __builtin_amdgcn_s_setprio(0);
+      mark(0);                 // S MFMAs issued (K fragment reads waited)
       if (kv0 + 64 > c) {      // keys >= c are zero pads (added analytically at the end)
         // (the -inf below also holds for the kPre accumulator offset)
   #pragma unroll
@@ -813,6 +837,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
             }
       }
 
+      mark(1);                 // max, rescale, exp2, cvt (waits on the S results)
       // ---- O^T += V^T . P^T  (2 sub-tiles x 2 k-steps x 2 d-tiles)
       if constexpr ((VAR & 32) != 0) __builtin_amdgcn_s_setprio(1);   // MFMA-issuing wave first
   #pragma unroll
@@ -834,6 +859,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
       if constexpr ((VAR & 32) != 0) __builtin_amdgcn_s_setprio(0);
     }
 
+    mark(2);                   // PV MFMAs issued (V fragment reads waited)
     if constexpr (kPF2) {
       if (t + 1 < ntiles) store_from(stage2[1 - SET], (t + 1) & 1);
     } else {
@@ -846,7 +872,9 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
       if (t + 1 < ntiles) load_tile((t + 1) * KT);
     }
     if constexpr (kDMA) __builtin_amdgcn_s_waitcnt(0x0f70);   // this wave's DMA pieces landed
+    mark(3);                   // next tile's stage stored to LDS (waits on its loads)
     if constexpr ((VAR & 256) == 0) __syncthreads();
+    mark(4);                   // barrier
     };
   if constexpr (kPF2) {
     for (int t = 0; t < ntiles; t += 2) {
@@ -857,6 +885,16 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
     for (int t = 0; t < ntiles; ++t) tile_step(t, std::integral_constant<int, 0>());
   }
 
+  if constexpr (kStamp) {
+    const unsigned long long t_end = stamp_now();
+    sacc_t[5] = t_end - t_kernel0;
+    if (lane == 0) {
+#pragma unroll
+      for (int i2 = 0; i2 < 6; ++i2) atomicAdd(&g_attn_stamps[i2], sacc_t[i2]);
+      atomicAdd(&g_attn_stamps[6], (unsigned long long)ntiles);
+      atomicAdd(&g_attn_stamps[7], 1ull);
+    }
+  }
   // ---- epilogue
   float l;
   if constexpr (kOnes) {
@@ -1815,6 +1853,7 @@ extern "C" int gp_dilated_attn_fwd_ex(const uint16_t* q, int64_t q_row_stride, i
       case 1538: dilated_attn32_kernel<48, true, 8, 1538><<<(unsigned)items, 512, 0, s>>>(a); break;
       case 1026: dilated_attn32_kernel<48, true, 4, 1026><<<(unsigned)items, 256, 0, s>>>(a); break;
       case 2050: dilated_attn32_kernel<48, true, 4, 2050><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 34818: dilated_attn32_kernel<48, true, 4, 34818><<<(unsigned)items, 256, 0, s>>>(a); break;
       case 10242: dilated_attn32_kernel<48, true, 4, 10242><<<(unsigned)items, 256, 0, s>>>(a); break;
       case 10243: dilated_attn32_kernel<48, true, 4, 10242, 5><<<(unsigned)items, 256, 0, s>>>(a); break;
       case 26626: dilated_attn32_kernel<48, true, 4, 26626><<<(unsigned)items, 256, 0, s>>>(a); break;
@@ -2198,4 +2237,19 @@ extern "C" int gp_dilated_sparsify(const uint16_t* src, int64_t src_row_stride, 
   }
   return gp_dilated_sparsify_dests(src, src_row_stride, k_col, v_col, tok_lo, n_tok, L, H, D, seg_len, ratios,
                                    nbranch, dests, nd, stream);
+}
+
+// Diagnostics: the per-segment cycle sums of the last VAR & 32768 launches (see stamp_now).
+extern "C" int gp_debug_attn_stamps(int64_t* out8, int reset) {
+  GP_REQUIRE(out8 != nullptr, "gp_debug_attn_stamps: null output");
+  unsigned long long h[8];
+  hipError_t e = hipMemcpyFromSymbol(h, HIP_SYMBOL(g_attn_stamps), sizeof(h), 0, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return gp_set_error("gp_debug_attn_stamps: %s", hipGetErrorString(e)), (int)e;
+  for (int i = 0; i < 8; ++i) out8[i] = (int64_t)h[i];
+  if (reset) {
+    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_attn_stamps), z, sizeof(z), 0, hipMemcpyHostToDevice);
+    if (e != hipSuccess) return gp_set_error("gp_debug_attn_stamps: %s", hipGetErrorString(e)), (int)e;
+  }
+  return 0;
 }

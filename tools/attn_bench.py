@@ -56,6 +56,12 @@ for impl, (outs, lses) in first.items():
              float((a.float().isnan() != b.float().isnan()).sum()) for a, b in zip(outs, first[ref_impl][0]))
     dl = max(float((a - b).abs().max()) for a, b in zip(lses, first[ref_impl][1]))
     print("impl %s vs %s: max|d out| %.3g  max|d lse| %.3g" % (impl, ref_impl, do, dl))
+if any(i.endswith("@34818") for i in res):      # stamped build: cycles per segment per tile
+    st = _hip.debug_attn_stamps(reset=True)
+    names = ["S MFMAs", "softmax", "PV", "stage store", "barrier"]
+    tiles = max(st[6], 1)
+    print("stamps: %d waves, %d tiles, %.0f wave-cycles/tile; per tile: %s" % (
+        st[7], st[6], st[5] / tiles, ", ".join("%s %.0f" % (n, v / tiles) for n, v in zip(names, st[:5]))))
 for impl, ts in res.items():
     ts.sort()
     med = ts[len(ts) // 2]
