@@ -1854,6 +1854,8 @@ extern "C" int gp_dilated_attn_fwd_ex(const uint16_t* q, int64_t q_row_stride, i
       case 1026: dilated_attn32_kernel<48, true, 4, 1026><<<(unsigned)items, 256, 0, s>>>(a); break;
       case 2050: dilated_attn32_kernel<48, true, 4, 2050><<<(unsigned)items, 256, 0, s>>>(a); break;
       case 34818: dilated_attn32_kernel<48, true, 4, 34818><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 2054: dilated_attn32_kernel<48, true, 4, 2054><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 10246: dilated_attn32_kernel<48, true, 4, 10246><<<(unsigned)items, 256, 0, s>>>(a); break;
       case 10242: dilated_attn32_kernel<48, true, 4, 10242><<<(unsigned)items, 256, 0, s>>>(a); break;
       case 10243: dilated_attn32_kernel<48, true, 4, 10242, 5><<<(unsigned)items, 256, 0, s>>>(a); break;
       case 26626: dilated_attn32_kernel<48, true, 4, 26626><<<(unsigned)items, 256, 0, s>>>(a); break;
