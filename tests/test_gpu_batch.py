@@ -169,3 +169,19 @@ def test_packed_graph_replay_and_encode_slides():
         for (x, c), o in zip(slides, out):
             ref = model(x[None], c[None], all_layer_embed=True)
             _close(torch.stack(o), torch.stack(ref))
+
+
+def test_forward_packed_edge_cases():
+    """One-tile slides (L = 2: every branch a single short segment), a single slide, slides
+    straddling the 1024-token segment edge, and the empty list."""
+    model = _model()
+    assert model.forward_packed([], all_layer_embed=True) == []
+    slides = _slides([1, 1023, 1, 1024, 2047], seed=130)
+    with torch.no_grad():
+        got = model.forward_packed(slides, all_layer_embed=True)
+        for (x, c), outs in zip(slides, got):
+            ref = model(x[None], c[None], all_layer_embed=True)
+            for o, r in zip(outs, ref):
+                _close(o, r)
+        one = model.forward_packed(slides[1:2], all_layer_embed=False)
+        _close(one[0][0], model(slides[1][0][None], slides[1][1][None])[0])
