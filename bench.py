@@ -254,6 +254,18 @@ def main():
     }
     if sp:
         result["sp_exchange_mb_per_layer_rank0"] = round(model._sp.plan.exchange_bytes(0) / 1e6, 1)
+        # the SP gather (gp_dilated_sparsify_dests): per branch, read the K and V head-group columns
+        # of this rank's tokens (2*C_b bf16 each) and write one row per destination chunk
+        plan = model._sp.plan
+        a_w, b_w = plan.bounds[rank]
+        sp_bytes = sum((b_w - a_w) * 2 * plan.C[b] * 2 + sum(plan.send_splits(rank, b)) * 2 * plan.C[b] * 2
+                       for b in range(len(plan.C)))
+        n_sp, ms_sp = kt.get("sparsify", (0, 0.0))
+        sp_gbs = sp_bytes / (ms_sp / max(n_sp, 1) / 1e3) / 1e9 if ms_sp > 0 else 0.0
+        result["sparsify_roofline"] = {"bound": "hbm", "kernel": "gp_dilated_sparsify_dests",
+                                       "achieved": round(sp_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                                       "frac": round(sp_gbs / PEAK_HBM_GBS, 4), "traffic": None,
+                                       "bytes_per_launch": sp_bytes}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not mixed:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         result["cpu_baseline"] = cpu_baseline(args.tiles, threads)
