@@ -1523,11 +1523,38 @@ __global__ __launch_bounds__(256, 2) void dilated_attn_pp_kernel(const AttnArgs 
 }
 
 // ---------------------------------------------------------------------------------------
+// Exact unsigned division by a launch constant d < 2^31 via a multiply-high (the libdivide
+// "branchfree" form): the merge kernel's per-token divisions are wave-uniform, so they run on the
+// scalar unit instead of ~25 VALU instructions each.
+struct DivMagic {
+  uint32_t m;
+  int32_t l;     // 0: d == 1
+};
+inline DivMagic make_div_magic(uint32_t d) {
+  DivMagic r{0, 0};
+  if (d <= 1) return r;
+  int l = 0;
+  while ((1ull << l) < d) ++l;                                   // ceil(log2 d)
+  r.m = (uint32_t)(((((uint64_t)1 << l) - d) << 32) / d + 1);
+  r.l = l;
+  return r;
+}
+GP_DEV uint32_t div_magic(uint32_t n, DivMagic mg) {
+  if (mg.l == 0) return n;
+  const uint32_t t = __umulhi(n, mg.m);
+  return (t + ((n - t) >> 1)) >> (mg.l - 1);
+}
+
 struct MergeBranch {
   GpBranch g;
   const uint16_t* o;
   const float* lse;
+  DivMagic dg, dr;   // division by g.g and by g.r
 };
+inline void merge_branch_magic(MergeBranch& m) {
+  m.dg = make_div_magic((uint32_t)m.g.g);
+  m.dr = make_div_magic((uint32_t)m.g.r);
+}
 
 struct MergeArgs {
   int64_t B, L;
@@ -1543,6 +1570,7 @@ struct MergeArgs {
   const MergeBranch* mtab;
   const int64_t* tok_off;
   int32_t nslide;
+  DivMagic dnt;        // division by ntok (the batch index of a row)
 };
 
 // One wave per run of kTPW consecutive tokens; lane l owns the EPL = E/64 contiguous elements
@@ -1589,17 +1617,17 @@ __global__ __launch_bounds__(256) void branch_merge_kernel(const MergeArgs a) {
         bidx = 0;
         p = (int)(row - slide_tok0);
       } else {
-        bidx = row / nt;
+        bidx = (int)div_magic((uint32_t)row, a.dnt);
         p = (int)a.tok_lo + (row - bidx * nt);
       }
 #pragma unroll
       for (int b = 0; b < GP_MAX_BRANCHES; ++b)
         if (b < a.nbranch) {
-          const GpBranch& g = (kTab ? tb[b] : a.br[b]).g;
-          pn[b] = p / g.g;
-          pt[b] = p - pn[b] * g.g;
-          pi[b] = pt[b] / g.r;
-          pj[b] = pt[b] - pi[b] * g.r;
+          const MergeBranch& mb = kTab ? tb[b] : a.br[b];
+          pn[b] = (int)div_magic((uint32_t)p, mb.dg);
+          pt[b] = p - pn[b] * mb.g.g;
+          pi[b] = (int)div_magic((uint32_t)pt[b], mb.dr);
+          pj[b] = pt[b] - pi[b] * mb.g.r;
         }
     } else {
       ++p;
@@ -1938,11 +1966,13 @@ extern "C" int gp_branch_merge_ln_window(const uint16_t* const* o_in, const floa
   MergeArgs a;
   a.B = B; a.L = L; a.H = H; a.D = D; a.E = E; a.nbranch = nbranch;
   a.tok_lo = tok_lo; a.ntok = n_tok;
+  a.dnt = make_div_magic((uint32_t)n_tok);
   for (int b = 0; b < nbranch; ++b) {
     GP_REQUIRE(seg_len[b] > 0 && ratios[b] > 0 && o_in[b] && lse_in[b], "gp_branch_merge_ln: bad branch %d", b);
     a.br[b].g = gp_make_branch(L, seg_len[b], ratios[b], H);
     a.br[b].o = o_in[b];
     a.br[b].lse = lse_in[b];
+    merge_branch_magic(a.br[b]);
   }
   for (int b = nbranch; b < GP_MAX_BRANCHES; ++b) a.br[b] = a.br[nbranch - 1];
   a.ln_w = ln_w; a.ln_b = ln_b; a.eps = eps; a.out = out;
@@ -2071,6 +2101,7 @@ extern "C" int gp_varlen_plan(const int64_t* L, int nslide, int H, int D, const 
       m.g = geo[(size_t)i * nbranch + b];
       m.o = o_out[b] + ooff[(size_t)i * nbranch + b];
       m.lse = lse_out[b] + loff[(size_t)i * nbranch + b];
+      merge_branch_magic(m);
     }
   GP_REQUIRE(items < (int64_t)0x7fffffff, "gp_varlen_plan: too many work items");
   VarlenHdr* hp = reinterpret_cast<VarlenHdr*>(base);
