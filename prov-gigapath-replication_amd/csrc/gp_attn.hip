@@ -30,6 +30,29 @@ namespace {
 
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
+// Exact unsigned division by a launch constant d < 2^31 via a multiply-high (the libdivide
+// "branchfree" form): the merge kernel's per-token divisions are wave-uniform, so they run on the
+// scalar unit instead of ~25 VALU instructions each.
+struct DivMagic {
+  uint32_t m;
+  int32_t l;     // 0: d == 1
+};
+inline DivMagic make_div_magic(uint32_t d) {
+  DivMagic r{0, 0};
+  if (d <= 1) return r;
+  int l = 0;
+  while ((1ull << l) < d) ++l;                                   // ceil(log2 d)
+  r.m = (uint32_t)(((((uint64_t)1 << l) - d) << 32) / d + 1);
+  r.l = l;
+  return r;
+}
+GP_DEV uint32_t div_magic(uint32_t n, DivMagic mg) {
+  if (mg.l == 0) return n;
+  const uint32_t t = __umulhi(n, mg.m);
+  return (t + ((n - t) >> 1)) >> (mg.l - 1);
+}
+
+
 struct AttnBranch {
   GpBranch g;
   int32_t nqb;          // q-blocks per (batch-segment, head)
@@ -46,7 +69,14 @@ struct AttnBranch {
   // varlen table entries only (one per (slide, branch); B = 1, window = the whole slide)
   const uint16_t* q;    // the slide's first query row
   int64_t L;            // the slide's length (CLS + tiles)
+  DivMagic d_nqb, d_nsegw, d_hpg, d_r;   // the work-item decode's divisors (scalar multiply-high)
 };
+inline void attn_branch_magic(AttnBranch& e) {
+  e.d_nqb = make_div_magic((uint32_t)e.nqb);
+  e.d_nsegw = make_div_magic((uint32_t)e.nseg_w);
+  e.d_hpg = make_div_magic((uint32_t)e.g.hpg);
+  e.d_r = make_div_magic((uint32_t)e.g.r);
+}
 
 struct AttnArgs {
   const uint16_t* q;    // query rows: token t of batch b at row (b*L + t - q_tok_base)
@@ -61,6 +91,7 @@ struct AttnArgs {
   AttnBranch br[GP_MAX_BRANCHES];   // work order (heaviest first)
   const AttnBranch* tab;            // varlen: ntab (slide, branch) entries in device memory
   int32_t ntab;
+  DivMagic d_H;
 };
 
 // Work item -> (branch, batch, segment, head, query-row range).  Rows [i_lo, i_hi) of
@@ -72,28 +103,36 @@ struct WorkItem {
 
 GP_DEV int ceil_div_pos(int64_t a, int r) { return a > 0 ? (int)((a + r - 1) / r) : 0; }
 
+// The decode's divisions are wave-uniform: multiply-high by host-computed magic numbers (32-bit
+// operands: every quantity here is below 2^31) instead of VALU integer-division emulation.
+GP_DEV void decode_core(const AttnBranch& br, int local, int H, DivMagic dH, int64_t L, int64_t win_lo,
+                        int64_t win_hi, WorkItem& w) {
+  const GpBranch& g = br.g;
+  const int q1 = (int)div_magic((uint32_t)local, br.d_nqb);
+  w.qb = local - q1 * br.nqb;
+  const int bnw = (int)div_magic((uint32_t)q1, dH);
+  w.hh = q1 - bnw * H;
+  w.bidx = (int)div_magic((uint32_t)bnw, br.d_nsegw);
+  w.n = br.n_lo + (bnw - w.bidx * br.nseg_w);
+  w.bn = w.bidx * g.nseg + w.n;
+  w.j = (int)div_magic((uint32_t)w.hh, br.d_hpg);
+  const int rem = (int)(L - (int64_t)w.n * g.s);
+  const int lim = (rem < g.s ? rem : g.s) - w.j;
+  w.c = lim > 0 ? (int)div_magic((uint32_t)(lim + g.r - 1), br.d_r) : 0;
+  const int base = w.n * g.g + w.j;
+  const int alo = (int)(win_lo - base), ahi = (int)(win_hi - base);
+  w.i_lo = alo > 0 ? (int)div_magic((uint32_t)(alo + g.r - 1), br.d_r) : 0;
+  const int hi = ahi > 0 ? (int)div_magic((uint32_t)(ahi + g.r - 1), br.d_r) : 0;
+  w.i_hi = hi < g.m ? hi : g.m;
+}
+
 GP_DEV void decode_item(const AttnArgs& a, int item, WorkItem& w) {
   int bi = 0;
 #pragma unroll
   for (int t = 1; t < GP_MAX_BRANCHES; ++t)
     if (t < a.nbranch && item >= (int)a.br[t].item_begin) bi = t;
-  const AttnBranch& br = a.br[bi];
-  const GpBranch& g = br.g;
-  int local = item - (int)br.item_begin;
   w.bi = bi;
-  w.qb = local % br.nqb;
-  local /= br.nqb;
-  w.hh = local % a.H;
-  const int bnw = local / a.H;
-  w.bidx = bnw / br.nseg_w;
-  w.n = br.n_lo + (bnw - w.bidx * br.nseg_w);
-  w.bn = w.bidx * g.nseg + w.n;
-  w.j = w.hh / g.hpg;
-  w.c = gp_valid_rows(g, a.L, w.n, w.j);
-  const int64_t base = (int64_t)w.n * g.g + w.j;
-  w.i_lo = ceil_div_pos(a.win_lo - base, g.r);
-  const int hi = ceil_div_pos(a.win_hi - base, g.r);
-  w.i_hi = hi < g.m ? hi : g.m;
+  decode_core(a.br[bi], item - (int)a.br[bi].item_begin, a.H, a.d_H, a.L, a.win_lo, a.win_hi, w);
 }
 
 // Varlen (packed slides): entry = (slide, branch), items ordered by entry (heaviest first);
@@ -105,21 +144,8 @@ GP_DEV void decode_item_tab(const AttnArgs& a, int item, WorkItem& w, AttnBranch
     if ((int64_t)item >= a.tab[mid].item_begin) lo = mid; else hi = mid - 1;
   }
   e = a.tab[lo];
-  const GpBranch& g = e.g;
-  int local = item - (int)e.item_begin;
   w.bi = lo;
-  w.qb = local % e.nqb;
-  local /= e.nqb;
-  w.hh = local % a.H;
-  w.n = local / a.H;
-  w.bidx = 0;
-  w.bn = w.n;
-  w.j = w.hh / g.hpg;
-  w.c = gp_valid_rows(g, e.L, w.n, w.j);
-  const int64_t base = (int64_t)w.n * g.g + w.j;
-  w.i_lo = 0;
-  const int hi2 = ceil_div_pos(e.L - base, g.r);
-  w.i_hi = hi2 < g.m ? hi2 : g.m;
+  decode_core(e, item - (int)e.item_begin, a.H, a.d_H, e.L, 0, e.L, w);
 }
 
 constexpr int kWaves = 4;
@@ -1523,28 +1549,6 @@ __global__ __launch_bounds__(256, 2) void dilated_attn_pp_kernel(const AttnArgs 
 }
 
 // ---------------------------------------------------------------------------------------
-// Exact unsigned division by a launch constant d < 2^31 via a multiply-high (the libdivide
-// "branchfree" form): the merge kernel's per-token divisions are wave-uniform, so they run on the
-// scalar unit instead of ~25 VALU instructions each.
-struct DivMagic {
-  uint32_t m;
-  int32_t l;     // 0: d == 1
-};
-inline DivMagic make_div_magic(uint32_t d) {
-  DivMagic r{0, 0};
-  if (d <= 1) return r;
-  int l = 0;
-  while ((1ull << l) < d) ++l;                                   // ceil(log2 d)
-  r.m = (uint32_t)(((((uint64_t)1 << l) - d) << 32) / d + 1);
-  r.l = l;
-  return r;
-}
-GP_DEV uint32_t div_magic(uint32_t n, DivMagic mg) {
-  if (mg.l == 0) return n;
-  const uint32_t t = __umulhi(n, mg.m);
-  return (t + ((n - t) >> 1)) >> (mg.l - 1);
-}
-
 struct MergeBranch {
   GpBranch g;
   const uint16_t* o;
@@ -1834,10 +1838,14 @@ extern "C" int gp_dilated_attn_fwd_ex(const uint16_t* q, int64_t q_row_stride, i
     e.kv_sparse = d.kv_sparse_cols ? 1 : 0;
     e.o = d.o;
     e.lse = d.lse;
+    attn_branch_magic(e);
     items += B * (int64_t)e.nseg_w * H * e.nqb;
   }
   for (int x = nbranch; x < GP_MAX_BRANCHES; ++x) a.br[x] = a.br[nbranch - 1];
   a.total_items = items;
+  a.d_H = make_div_magic((uint32_t)H);
+  a.tab = nullptr;
+  a.ntab = 0;
   GP_REQUIRE(items < (int64_t)0x7fffffff, "gp_dilated_attn_fwd: too many work items");
   hipStream_t s = gp_stream(stream);
   if (impl == 1) {
@@ -1898,9 +1906,10 @@ extern "C" int gp_dilated_attn_fwd_ex(const uint16_t* q, int64_t q_row_stride, i
       default: return gp_set_error("gp_dilated_attn_fwd: GP_ATTN_VAR=%d unknown", var), GP_EARG;
     }
   } else if (q_log2_prescaled) {
-    // default: VAR 2050 (staging addresses hoisted, K/V staged by buffer loads through a bounded
-    // descriptor: +5-7 % over VAR 2); VAR 2 where the descriptor layout does not fit
-    if (D == 48 && kv_desc_ok) dilated_attn32_kernel<48, true, 4, 2050><<<(unsigned)items, 256, 0, s>>>(a);
+    // default: VAR 10242 -- K/V tiles by LDS-DMA (buffer_load ... lds) through a bounded descriptor
+    // straight into the tile images (+2-3 % over VAR 2050's buffer loads into registers, itself
+    // +5-7 % over VAR 2); VAR 2 where the descriptor layout does not fit
+    if (D == 48 && kv_desc_ok) dilated_attn32_kernel<48, true, 4, 10242><<<(unsigned)items, 256, 0, s>>>(a);
     else if (D == 48) dilated_attn32_kernel<48, true, 4, 2><<<(unsigned)items, 256, 0, s>>>(a);
     else dilated_attn32_kernel<64, true, 4><<<(unsigned)items, 256, 0, s>>>(a);
   } else {
@@ -2093,6 +2102,7 @@ extern "C" int gp_varlen_plan(const int64_t* L, int nslide, int H, int D, const 
     e.o = o_out[b] + ooff[id];
     e.lse = lse_out[b] + loff[id];
     e.L = L[i];
+    attn_branch_magic(e);
     items += (int64_t)g.nseg * H * e.nqb;
   }
   for (int i = 0; i < nslide; ++i)
@@ -2140,6 +2150,7 @@ extern "C" int gp_dilated_attn_fwd_varlen(const void* plan_host, const void* pla
   a.total_items = h.total_items;
   a.tab = reinterpret_cast<const AttnBranch*>(static_cast<const char*>(plan_dev) + h.tab_off);
   a.ntab = h.ntab;
+  a.d_H = make_div_magic((uint32_t)h.H);
   dilated_attn32_kernel<48, true, 4, 2050, 2, true><<<(unsigned)h.total_items, 256, 0, gp_stream(stream)>>>(a);
   return gp_check_launch("gp_dilated_attn_fwd_varlen");
 }
