@@ -627,7 +627,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
 
   bf16x8 onesA = {}, mqB = {};    // kMI operands
   if constexpr (kMI) {
-    if (h == 0) onesA[0] = (__bf16)1.0f;
+    if (h == 0) { onesA[0] = (__bf16)1.0f; onesA[1] = (__bf16)1.0f; }
   }
   float m_run = -INFINITY;   // running max, log2 domain, of query l32
   float lsum = 0.f;          // row sum (VALU path, D % 32 == 0 only)
@@ -789,7 +789,19 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
             // m stays exactly representable in bf16 (it enters the MFMA through q); the shift
             // applied is the rounded one, so numerator and denominator stay consistent
             const float m_old = (sub == 0) ? 0.f : m_run;
-            const float m_new = need ? (float)(__bf16)(m_old + mx) : m_old;
+            // kMK: m kept bf16-exact; kMI: m kept as an exact hi + lo pair of bf16 values (two rows of
+            // the init MFMA), so it tracks the max to ~2^-16 relative and the bookkeeping stays exact
+            float m_new = m_old;
+            if (need) {
+              if constexpr (kMI) {
+                const float tt = -(m_old + mx);
+                const __bf16 hi = (__bf16)tt;
+                const __bf16 lo = (__bf16)(tt - (float)hi);
+                m_new = -((float)hi + (float)lo);
+              } else {
+                m_new = (float)(__bf16)(m_old + mx);
+              }
+            }
             const float d = m_new - m_old;
             if (sub > 0) {
               const float alpha = fast_exp2(-d);
@@ -807,7 +819,11 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
             if constexpr (kMK) {
               if (h == 0) qf[KS][0] = (__bf16)(-m_run);
             } else {
-              if (h == 0) mqB[0] = (__bf16)(-m_run);
+              if (h == 0) {
+                const __bf16 hi = (__bf16)(-m_run);
+                mqB[0] = hi;
+                mqB[1] = (__bf16)(-m_run - (float)hi);
+              }
             }
           } else {
             const float delta = need ? mx : 0.f;
@@ -1906,10 +1922,11 @@ extern "C" int gp_dilated_attn_fwd_ex(const uint16_t* q, int64_t q_row_stride, i
       default: return gp_set_error("gp_dilated_attn_fwd: GP_ATTN_VAR=%d unknown", var), GP_EARG;
     }
   } else if (q_log2_prescaled) {
-    // default: VAR 10242 -- K/V tiles by LDS-DMA (buffer_load ... lds) through a bounded descriptor
-    // straight into the tile images (+2-3 % over VAR 2050's buffer loads into registers, itself
-    // +5-7 % over VAR 2); VAR 2 where the descriptor layout does not fit
-    if (D == 48 && kv_desc_ok) dilated_attn32_kernel<48, true, 4, 10242><<<(unsigned)items, 256, 0, s>>>(a);
+    // default: VAR 14338 -- K/V tiles by LDS-DMA (buffer_load ... lds) through a bounded descriptor
+    // straight into the tile images (VAR 10242: +2-3 % over VAR 2050's buffer loads into registers,
+    // itself +5-7 % over VAR 2) and the -m start block of S from one MFMA of an exact hi + lo bf16
+    // pair instead of 16 v_mov (VAR 4096: +1.5 %); VAR 2 where the descriptor layout does not fit
+    if (D == 48 && kv_desc_ok) dilated_attn32_kernel<48, true, 4, 14338><<<(unsigned)items, 256, 0, s>>>(a);
     else if (D == 48) dilated_attn32_kernel<48, true, 4, 2><<<(unsigned)items, 256, 0, s>>>(a);
     else dilated_attn32_kernel<64, true, 4><<<(unsigned)items, 256, 0, s>>>(a);
   } else {
@@ -2151,7 +2168,8 @@ extern "C" int gp_dilated_attn_fwd_varlen(const void* plan_host, const void* pla
   a.tab = reinterpret_cast<const AttnBranch*>(static_cast<const char*>(plan_dev) + h.tab_off);
   a.ntab = h.ntab;
   a.d_H = make_div_magic((uint32_t)h.H);
-  dilated_attn32_kernel<48, true, 4, 2050, 2, true><<<(unsigned)h.total_items, 256, 0, gp_stream(stream)>>>(a);
+  // the single-slide default's variant, so each packed slide's outputs equal its own launch's
+  dilated_attn32_kernel<48, true, 4, 14338, 2, true><<<(unsigned)h.total_items, 256, 0, gp_stream(stream)>>>(a);
   return gp_check_launch("gp_dilated_attn_fwd_varlen");
 }
 

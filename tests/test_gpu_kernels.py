@@ -183,11 +183,12 @@ def test_dilated_attention_vs_oracle(name, B, L, segs, ratios, attn_impl):
 LSE_ATOL = 2.5e-3
 
 
-@pytest.mark.parametrize("impl", ["2", "3", "2@2", "2@10242", "4@7"])
+@pytest.mark.parametrize("impl", ["2", "3", "2@2", "2@2050", "2@10242", "4@7"])
 @pytest.mark.parametrize("name,B,L,segs,ratios", ATTN_CASES)
 def test_dilated_attention_prescaled_q(name, B, L, segs, ratios, impl, monkeypatch):
-    # "2": the default (buffer-descriptor staging); "2@2": global-load staging; "2@10242": LDS-DMA
-    # staging; "4@7": two query blocks per wave; "3": software-pipelined
+    # "2": the default (LDS-DMA staging, MFMA-initialised running-max block); "2@2": global-load
+    # staging; "2@2050": buffer loads into registers; "2@10242": LDS-DMA with v_mov-initialised
+    # running max; "4@7": two query blocks per wave; "3": software-pipelined
     base, _, var = impl.partition("@")
     monkeypatch.setenv("GP_ATTN_IMPL", base)
     if var:
