@@ -183,7 +183,7 @@ def test_dilated_attention_vs_oracle(name, B, L, segs, ratios, attn_impl):
 LSE_ATOL = 2.5e-3
 
 
-@pytest.mark.parametrize("impl", ["2", "3", "2@2", "2@2050", "2@10242", "4@7"])
+@pytest.mark.parametrize("impl", ["2", "3", "2@2", "2@2050", "2@10242", "2@14338", "4@7"])
 @pytest.mark.parametrize("name,B,L,segs,ratios", ATTN_CASES)
 def test_dilated_attention_prescaled_q(name, B, L, segs, ratios, impl, monkeypatch):
     # "2": the default (LDS-DMA staging, MFMA-initialised running-max block); "2@2": global-load
