@@ -401,6 +401,9 @@ GP_DEV unsigned long long stamp_now() {
   return t;
 }
 
+// lse bit pattern (a quiet NaN no real row produces) that flags a row for the fixup pass
+constexpr uint32_t kLseRedo = 0x7fc0dead;
+
 // VAR bits (A/B variants, all numerically identical): 1 = S's first k-step takes its C operand
 // from a persistent -m_run block (no per-tile accumulator init), 2 = staging addresses computed
 // once (no per-tile 64-bit index math, no bound checks on full tiles), 4 = all K fragments read
@@ -409,7 +412,7 @@ GP_DEV unsigned long long stamp_now() {
 // with no per-tile accumulator initialisation and no extra registers (2 more MFMAs per tile,
 // ~17 fewer VALU).  OCC = waves per SIMD the register budget must allow.
 template <int D, bool kPre, int NW, int VAR = 0, int OCC = 2, bool kTab = false>
-__global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const AttnArgs a) {
+__device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_idx) {
   static_assert(D == 48 || D == 64, "v2 kernel covers D = 48 and 64");
   static_assert(NW == 4 || NW == 8, "");
   constexpr int NT = NW * 64;                // threads
@@ -426,6 +429,17 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
   // [1, 0 ...] (A) x [-m_run, 0 ...] (B) with C = 0, instead of 16 v_mov per sub-tile (the loop
   // is VALU-issue bound; the MFMA pipe has slack); m_run kept bf16-exact as with VAR 8
   constexpr bool kMI = (VAR & 4096) != 0;
+  // VAR & 262144: no per-tile row max after the first 64 keys.  Tile 0 sets m_run to its exact max;
+  // later tiles only watch the running row sum l (the ones row of O, exact bookkeeping of
+  // sum exp2(s - m_run)) and renormalise when l > 2^24 (m_run += log2 l, so m_run stays within
+  // log2(c) of the true running max and no p can underflow against it).  A later key more than
+  // ~127 log2 units above the running max would overflow exp2: every query's final l is checked,
+  // a query whose l is not finite gets an lse marker (kLseRedo) and the fixup launch (VAR &
+  // 524288, the exact per-tile-max kernel, run right after on the same stream) recomputes every
+  // block holding a marker and exits at once elsewhere.
+  constexpr bool kNM = (VAR & 262144) != 0;
+  constexpr bool kFix = (VAR & 524288) != 0;
+  static_assert(!(kNM && kFix), "the fixup pass is the exact kernel");
   static_assert(!kMI || (D == 48 && kPre && !kMK && (VAR & 1) == 0), "VAR 4096 needs D = 48, kPre, no VAR 8/1");
   constexpr int KROWB = (kMK ? 64 : D) * 2 + 16;   // K image row bytes (padded)
   constexpr int VROWB = 128;                 // V image row bytes (64 bf16, swizzled 32-B blocks)
@@ -437,13 +451,22 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
   constexpr int LPT = (TOT + NT - 1) / NT;
   static_assert(TOT % NT == 0 || (VAR & 2) != 0, "uneven chunk split needs VAR & 2");
   constexpr float kThr = 8.0f;               // lazy-rescale threshold (log2 units)
-  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  // VAR & 131072: the two tile buffers are two distinct LDS objects (each selected at compile time
+  // by the unrolled loop), so the LDS lowering gives them distinct alias scopes and the wait
+  // insertion no longer orders this tile's LDS reads after the next tile's in-flight LDS-DMA
+  constexpr bool kTwo = (VAR & 131072) != 0;
+  __shared__ __attribute__((aligned(16))) char smem[kTwo ? BUF : 2 * BUF];
+  __shared__ __attribute__((aligned(16))) char smem_b[kTwo ? BUF : 16];
+  auto bufp_of = [&](int b) -> char* {
+    if constexpr (kTwo) return b ? smem_b : smem;
+    else return smem + b * BUF;
+  };
 
   // ---- work item (32-bit index math: items < 2^31, checked on the host)
   WorkItem wi;
   AttnBranch te;                             // kTab: this item's table entry
-  if constexpr (kTab) decode_item_tab(a, (int)xcd_group(blockIdx.x, gridDim.x), wi, te);
-  else decode_item(a, (int)xcd_group(blockIdx.x, gridDim.x), wi);
+  if constexpr (kTab) decode_item_tab(a, item_idx, wi, te);
+  else decode_item(a, item_idx, wi);
   const AttnBranch& brr = kTab ? te : a.br[wi.bi];
   const GpBranch g = brr.g;
   const int hh = wi.hh, c = wi.c, bn = wi.bn;
@@ -451,6 +474,13 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
   const int q0 = wi.i_lo + wi.qb * QB;
   if (q0 >= rows_needed) return;
   const int qvalid = c < rows_needed ? c : rows_needed;   // see dilated_attn_kernel
+  if constexpr (kFix) {      // fixup pass: only blocks the kNM kernel flagged are recomputed
+    const int i = q0 + (int)threadIdx.x;
+    bool flagged = false;
+    if (threadIdx.x < QB && i < rows_needed)
+      flagged = __float_as_uint(brr.lse[((int64_t)wi.bn * a.H + wi.hh) * g.m + i]) == kLseRedo;
+    if (!__syncthreads_or(flagged)) return;
+  }
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int l32 = lane & 31, h = lane >> 5;
@@ -467,7 +497,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
     for (int idx = threadIdx.x; idx < 2 * KT * 2; idx += NT) {   // 2 bufs x KT rows x 2 chunks
       const int buf = idx / (2 * KT), rem = idx % (2 * KT), row = rem >> 1, half = rem & 1;
       const uint4 col = half ? make_uint4(0, 0, 0, 0) : make_uint4(0x3F80u, 0, 0, 0);
-      *reinterpret_cast<uint4*>(smem + buf * BUF + row * KROWB + 96 + 16 * half) = col;
+      *reinterpret_cast<uint4*>(bufp_of(buf) + row * KROWB + 96 + 16 * half) = col;
     }
   }
   // V images: the d-columns >= D of every row (block 3 for D = 48) hold bf16 1.0
@@ -475,7 +505,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
     for (int idx = threadIdx.x; idx < 2 * KT * 2; idx += NT) {   // 2 bufs x KT rows x 2 chunks
       const int buf = idx / (2 * KT), rem = idx % (2 * KT), row = rem >> 1, half = rem & 1;
       const uint4 ones = make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
-      *reinterpret_cast<uint4*>(smem + buf * BUF + KTILE + row * VROWB + 32 * (3 ^ (row & 3)) + 16 * half) = ones;
+      *reinterpret_cast<uint4*>(bufp_of(buf) + KTILE + row * VROWB + 32 * (3 ^ (row & 3)) + 16 * half) = ones;
     }
   }
 
@@ -527,6 +557,8 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
   // rows, swizzled 32-B blocks; the lanes of the bf16-ones block are off, the prologue wrote
   // it).  Piece p of the 15 goes to wave p % 4.
   constexpr bool kDMA = (VAR & 8192) != 0;
+  static_assert(!kNM || (kMI && kOnes), "VAR 262144 needs VAR 4096 (D = 48)");
+  static_assert(!kTwo || (kDMA && (VAR & 65536) != 0), "VAR 131072 needs VAR 8192 + 65536");
   static_assert(!kDMA || (D == 48 && NW == 4 && KT == 64 && (VAR & 2048) != 0 && !kMK),
                 "VAR 8192 needs D = 48, 4 waves, 64-key tiles and VAR 2048");
   constexpr int kPieces = (KT * KROWB + KT * VROWB) / 1024;      // 15
@@ -550,13 +582,13 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
       }
     }
   }
-  auto load_tile = [&](int kv0) {
+  auto load_tile = [&](int kv0, int nbuf = -1) {
     if constexpr (kDMA) {
       const int64_t tb = (int64_t)kv0 * kvstride * 2;
       const int64_t nrec = (int64_t)(c - kv0 - 1) * kvstride * 2 + kv_dv + 2 * D;
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
           (void*)((const char*)kbase + tb), (short)0, (int)(nrec < 0x7fffffff ? nrec : 0x7fffffff), 0x00020000);
-      char* bufp = smem + ((kv0 / KT) & 1) * BUF;
+      char* bufp = (kTwo && nbuf >= 0) ? bufp_of(nbuf) : bufp_of((kv0 / KT) & 1);
 #pragma unroll
       for (int sl = 0; sl < 4; ++sl) {
         const int pc = w + 4 * sl;
@@ -621,7 +653,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
         const int row = rem / CH, ch = rem % CH;
         off = tsel ? KTILE + row * VROWB + 32 * ((ch >> 1) ^ (row & 3)) + 16 * (ch & 1) : row * KROWB + ch * 16;
       }
-      *reinterpret_cast<uint4*>(smem + buf * BUF + off) = stage[u];
+      *reinterpret_cast<uint4*>(bufp_of(buf) + off) = stage[u];
     }
   };
 
@@ -641,6 +673,16 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
     for (int r = 0; r < 16; ++r) oacc[mt][r] = 0.f;
 
   const int ntiles = (c + KT - 1) / KT;
+  // kTwo: the lane part of each V^T fragment offset (row & 3 does not depend on the sub-tile),
+  // made opaque so the reads stay one GEP from their LDS object -- the LDS lowering tags an access
+  // with its object's alias scope only a few GEPs deep, and an untagged read waits on every DMA
+  int vlane[2];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+    const int rl = 4 * (lane >> 5) + ((lane >> 2) & 3);
+    vlane[mt] = rl * VROWB + 32 * ((2 * mt + ((lane >> 4) & 1)) ^ (rl & 3)) + 8 * (lane & 3);
+    if constexpr (kTwo) asm volatile("" : "+v"(vlane[mt]));
+  }
   // VAR & 1024: prefetch distance 2 -- two register stage sets (tile t+2 loads while tile t+1
   // waits in the other set), the loop unrolled by 2 so each set is a compile-time choice
   constexpr bool kPF2 = (VAR & 1024) != 0;
@@ -661,7 +703,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
 #pragma unroll
     for (int u = 0; u < LPT; ++u) {
       if (TOT % NT != 0 && threadIdx.x + NT * u >= TOT) continue;
-      *reinterpret_cast<uint4*>(smem + buf * BUF + loff[u]) = st[u];
+      *reinterpret_cast<uint4*>(bufp_of(buf) + loff[u]) = st[u];
     }
   };
   if (ntiles > 0) {
@@ -701,7 +743,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
     if constexpr (kPF2) {
       if (t + 2 < ntiles) load_into(stage2[SET], (t + 2) * KT);
     } else if constexpr ((VAR & 16384) == 0) {
-      if (t + 1 < ntiles && (VAR & 128) == 0) load_tile((t + 1) * KT);
+      if (t + 1 < ntiles && (VAR & 128) == 0) load_tile((t + 1) * KT, 1 - SET);
     }
 #pragma unroll
     for (int hf = 0; hf < KT / 64; ++hf) {
@@ -712,8 +754,8 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
       // into the ds_read immediates instead of a per-tile v_add)
       constexpr bool kU2 = (VAR & 65536) != 0;
       const int bsel = ((VAR & 128) != 0) ? 0 : (kU2 ? SET : (t & 1));
-      const char* Kb = smem + bsel * BUF + hf * 64 * KROWB;
-      const char* Vb = smem + bsel * BUF + KTILE + hf * 64 * VROWB;
+      const char* Kb = bufp_of(bsel) + hf * 64 * KROWB;
+      const char* Vb = bufp_of(bsel) + KTILE + hf * 64 * VROWB;
       // ---- S^T for two 32-key sub-tiles.  kPre (q pre-multiplied by scale*log2 e): the
       // accumulator starts at -m_run, so it already holds log2-domain scores minus the max.
       f32x16 sacc[2];
@@ -772,22 +814,58 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
       }
 
       // ---- online softmax with deferred rescale (two independent max chains)
+      const bool do_max = !kNM || sub == 0;
+      float mx = 0.f;
+      if (do_max) {
       float mxa = sacc[0][0], mxb = sacc[1][0];
   #pragma unroll
       for (int r = 1; r < 16; ++r) {
         mxa = fmaxf(mxa, sacc[0][r]);
         mxb = fmaxf(mxb, sacc[1][r]);
       }
-      float mx = fmaxf(mxa, mxb);
+      mx = fmaxf(mxa, mxb);
       {
         const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
         mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
       }
+      }
       bf16x8 pf[2][2];
+      if constexpr (kNM) {
+        if (!do_max) {
+          // l of the tiles so far (the ones row); renormalise when it grew past 2^24
+          const float lc = oacc[1][8];
+          const bool big = lc > 0x1p24f && (__float_as_uint(lc) & 0x7f800000u) != 0x7f800000u;
+          if (__builtin_amdgcn_ballot_w64(big)) {
+            float m_new = m_run;
+            if (big) {
+              const float tt = -(m_run + __builtin_amdgcn_logf(lc));
+              const __bf16 hi = (__bf16)tt;
+              const __bf16 lo = (__bf16)(tt - (float)hi);
+              m_new = -((float)hi + (float)lo);
+            }
+            const float d = m_new - m_run;
+            const float alpha = fast_exp2(-d);
+  #pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+  #pragma unroll
+              for (int r = 0; r < 16; ++r) oacc[mt][r] *= alpha;
+            m_run = m_new;
+  #pragma unroll
+            for (int u = 0; u < 2; ++u)
+  #pragma unroll
+              for (int r = 0; r < 16; ++r) sacc[u][r] -= d;
+            if (h == 0) {
+              const __bf16 hi = (__bf16)(-m_run);
+              mqB[0] = hi;
+              mqB[1] = (__bf16)(-m_run - (float)hi);
+            }
+          }
+        }
+      }
       if constexpr (kPre) {
         // scores are s*c - m_run; rescale only when a query's max moved up by > kThr
         // (tile 0: always, which sets m_run to that tile's exact max)
-        const bool need = (sub == 0) || (mx > kThr);
+        const bool need = do_max && ((sub == 0) || (mx > kThr));
         if (__builtin_amdgcn_ballot_w64(need)) {
           if constexpr (kMK || kMI) {
             // m stays exactly representable in bf16 (it enters the MFMA through q); the shift
@@ -894,7 +972,12 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
   #pragma unroll
           for (int mt = 0; mt < 2; ++mt) {
             const int blk = 2 * mt + ((lane >> 4) & 1);
-            const char* p0 = Vb + row * VROWB + 32 * (blk ^ (row & 3)) + 8 * (lane & 3);
+            const char* p0;
+            if constexpr (kTwo) {
+              p0 = Vb + (vlane[mt] + (32 * u + 16 * s) * VROWB);
+            } else {
+              p0 = Vb + row * VROWB + 32 * (blk ^ (row & 3)) + 8 * (lane & 3);
+            }
             const char* p1 = p0 + 8 * VROWB;   // rows + 8 keep (row & 3)
             const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
             const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p1);
@@ -980,7 +1063,62 @@ __global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const Attn
           store_bf16<4>(orow + d0, vv);
         }
       }
-    if (h == 0) br.lse[((int64_t)bn * a.H + hh) * g.m + i] = (mr + __builtin_amdgcn_logf(l)) * 0.69314718055994530942f;
+    float lse = (mr + __builtin_amdgcn_logf(l)) * 0.69314718055994530942f;
+    if constexpr (kNM) {     // overflowed (some p = inf): flag the row for the fixup pass
+      if ((__float_as_uint(l) & 0x7f800000u) == 0x7f800000u || !(l > 0.f)) lse = __uint_as_float(kLseRedo);
+    }
+    if (h == 0) br.lse[((int64_t)bn * a.H + hh) * g.m + i] = lse;
+  }
+}
+
+// The kernel: one work item per block, or (VAR & 524288, the fixup pass after a VAR & 262144
+// launch) kFixItems consecutive items per block -- the block reads the lse of every needed row of
+// all of them at once (wave w: items 8w .. 8w + 7; 16 independent loads per lane) and exits unless
+// some row holds the kLseRedo marker, so the pass costs about one load latency per 32 items when
+// nothing overflowed.
+constexpr int kFixItems = 32;
+
+template <int D, bool kPre, int NW, int VAR = 0, int OCC = 2, bool kTab = false>
+__global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const AttnArgs a) {
+  if constexpr ((VAR & 524288) != 0) {
+    static_assert(NW == 4 && kFixItems % NW == 0, "fixup scan: 4 waves x kFixItems / 4 items");
+    constexpr int QB = NW * 32;
+    const int it0 = (int)blockIdx.x * kFixItems;
+    // wave index made provably uniform: the item decode then runs on the scalar unit (s_load from
+    // the kernel arguments), not as a chain of dependent per-lane global loads
+    const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), lane = (int)threadIdx.x & 63;
+    // every load is issued before any is compared (clamped in-bounds indices, masked after), so the
+    // 16 loads of a lane are in flight together
+    constexpr int NV = (kFixItems / NW) * (QB / 64);
+    uint32_t vals[NV];
+    bool use[NV];
+#pragma unroll
+    for (int k = 0; k < kFixItems / NW; ++k) {
+      const int it = it0 + (kFixItems / NW) * w + k;
+      const bool live = it < a.total_items;
+      WorkItem wi;
+      AttnBranch te;
+      const int itc = live ? it : (int)a.total_items - 1;
+      if constexpr (kTab) decode_item_tab(a, itc, wi, te);
+      else decode_item(a, itc, wi);
+      const AttnBranch& brr = kTab ? te : a.br[wi.bi];
+      const int q0 = wi.i_lo + wi.qb * QB;
+      const float* lrow = brr.lse + ((int64_t)wi.bn * a.H + wi.hh) * brr.g.m;
+#pragma unroll
+      for (int hf = 0; hf < QB / 64; ++hf) {
+        const int i = q0 + 64 * hf + lane;
+        const int n = k * (QB / 64) + hf;
+        use[n] = live && i < wi.i_hi;
+        vals[n] = __float_as_uint(lrow[use[n] ? i : 0]);
+      }
+    }
+    bool flagged = false;
+#pragma unroll
+    for (int n = 0; n < NV; ++n) flagged |= use[n] && vals[n] == kLseRedo;
+    if (!__syncthreads_or(flagged)) return;
+    for (int k = 0; k < kFixItems && it0 + k < a.total_items; ++k) attn32_item<D, kPre, NW, VAR, OCC, kTab>(a, it0 + k);
+  } else {
+    attn32_item<D, kPre, NW, VAR, OCC, kTab>(a, (int)xcd_group(blockIdx.x, gridDim.x));
   }
 }
 
@@ -1922,6 +2060,14 @@ extern "C" int gp_dilated_attn_fwd_ex(const uint16_t* q, int64_t q_row_stride, i
       case 10242: dilated_attn32_kernel<48, true, 4, 10242><<<(unsigned)items, 256, 0, s>>>(a); break;
       case 10243: dilated_attn32_kernel<48, true, 4, 10242, 5><<<(unsigned)items, 256, 0, s>>>(a); break;
       case 79874: dilated_attn32_kernel<48, true, 4, 79874><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 210946: dilated_attn32_kernel<48, true, 4, 210946><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 342019:   // test hook: 342018 WITHOUT the fixup pass (overflowed rows keep the lse marker)
+        dilated_attn32_kernel<48, true, 4, 342018><<<(unsigned)items, 256, 0, s>>>(a);
+        break;
+      case 342018:   // no per-tile max after tile 0, then the fixup pass for flagged blocks
+        dilated_attn32_kernel<48, true, 4, 342018><<<(unsigned)items, 256, 0, s>>>(a);
+        dilated_attn32_kernel<48, true, 4, 79874 + 524288><<<(unsigned)((items + kFixItems - 1) / kFixItems), 256, 0, s>>>(a);
+        break;
       case 26626: dilated_attn32_kernel<48, true, 4, 26626><<<(unsigned)items, 256, 0, s>>>(a); break;
       case 26627: dilated_attn32_kernel<48, true, 4, 26626, 5><<<(unsigned)items, 256, 0, s>>>(a); break;
       case 14338: dilated_attn32_kernel<48, true, 4, 14338><<<(unsigned)items, 256, 0, s>>>(a); break;
@@ -1938,7 +2084,12 @@ extern "C" int gp_dilated_attn_fwd_ex(const uint16_t* q, int64_t q_row_stride, i
     // straight into the tile images (VAR 10242: +2-3 % over VAR 2050's buffer loads into registers,
     // itself +5-7 % over VAR 2) and the -m start block of S from one MFMA of an exact hi + lo bf16
     // pair instead of 16 v_mov (VAR 4096: +1.5 %); VAR 2 where the descriptor layout does not fit
-    if (D == 48 && kv_desc_ok) dilated_attn32_kernel<48, true, 4, 79874><<<(unsigned)items, 256, 0, s>>>(a);
+    if (D == 48 && kv_desc_ok) {
+      // VAR 342018 = 79874 without the per-tile row max after tile 0 (+2.7 %), then the fixup pass
+      // (exact kernel, exits at once unless a block overflowed)
+      dilated_attn32_kernel<48, true, 4, 342018><<<(unsigned)items, 256, 0, s>>>(a);
+      dilated_attn32_kernel<48, true, 4, 79874 + 524288><<<(unsigned)((items + kFixItems - 1) / kFixItems), 256, 0, s>>>(a);
+    }
     else if (D == 48) dilated_attn32_kernel<48, true, 4, 2><<<(unsigned)items, 256, 0, s>>>(a);
     else dilated_attn32_kernel<64, true, 4><<<(unsigned)items, 256, 0, s>>>(a);
   } else {
@@ -2181,7 +2332,8 @@ extern "C" int gp_dilated_attn_fwd_varlen(const void* plan_host, const void* pla
   a.ntab = h.ntab;
   a.d_H = make_div_magic((uint32_t)h.H);
   // the single-slide default's variant, so each packed slide's outputs equal its own launch's
-  dilated_attn32_kernel<48, true, 4, 79874, 2, true><<<(unsigned)h.total_items, 256, 0, gp_stream(stream)>>>(a);
+  dilated_attn32_kernel<48, true, 4, 342018, 2, true><<<(unsigned)h.total_items, 256, 0, gp_stream(stream)>>>(a);
+  dilated_attn32_kernel<48, true, 4, 79874 + 524288, 2, true><<<(unsigned)((h.total_items + kFixItems - 1) / kFixItems), 256, 0, gp_stream(stream)>>>(a);
   return gp_check_launch("gp_dilated_attn_fwd_varlen");
 }
 

@@ -183,7 +183,7 @@ def test_dilated_attention_vs_oracle(name, B, L, segs, ratios, attn_impl):
 LSE_ATOL = 2.5e-3
 
 
-@pytest.mark.parametrize("impl", ["2", "3", "2@2", "2@2050", "2@10242", "2@14338", "4@7"])
+@pytest.mark.parametrize("impl", ["2", "3", "2@2", "2@2050", "2@10242", "2@14338", "2@79874", "2@210946", "4@7"])
 @pytest.mark.parametrize("name,B,L,segs,ratios", ATTN_CASES)
 def test_dilated_attention_prescaled_q(name, B, L, segs, ratios, impl, monkeypatch):
     # "2": the default (LDS-DMA staging, MFMA-initialised running-max block); "2@2": global-load
@@ -213,6 +213,48 @@ def test_dilated_attention_prescaled_q(name, B, L, segs, ratios, impl, monkeypat
         assert torch.isfinite(o[mask]).all() and torch.isfinite(l[mask]).all(), (name, b)
         assert (o - o_ref).abs()[mask].max().item() <= 1.2e-2 * max(1.0, o_ref.abs().max().item()), (name, b)
         assert (l - l_ref).abs()[mask].max().item() <= LSE_ATOL, (name, b)
+
+
+@pytest.mark.parametrize("impl", ["2", "2@342018"])
+def test_attention_no_max_overflow_fixup_and_renormalise(impl, monkeypatch):
+    """Default kernel (no per-tile row max after the first 64 keys): head 0 has one key whose
+    log2-domain score (200) is > 127 above every earlier key, so exp2 overflows and the block must
+    be recomputed by the exact fixup pass; head 1's scores climb 30 log2 units per 64-key tile, so
+    the running sum passes 2^24 and is renormalised mid-row.  Both must match the oracle."""
+    base, _, var = impl.partition("@")
+    monkeypatch.setenv("GP_ATTN_IMPL", base)
+    if var:
+        monkeypatch.setenv("GP_ATTN_VAR", var)
+    h = _hip()
+    B, L, H, D = 1, 300, 16, 48
+    E = H * D
+    qkv = _rand_qkv(B, L, E, seed=21).float() * 0.3
+    qkv[:, 0 * D:2 * D] = 0.0                    # q heads 0, 1: [8, 0, ...]
+    qkv[:, 0 * D] = 8.0
+    qkv[:, 1 * D] = 8.0
+    qkv[:, E:E + 2 * D] = 0.0                    # k heads 0, 1
+    qkv[150, E] = 25.0                           # head 0: score 200 at key 150 only
+    qkv[:, E + D] = torch.from_numpy((np.arange(L) // 64) * 3.75).float()   # head 1: 30 per tile
+    qkv = qkv.bfloat16()
+    segs, ratios = [300], [1]
+    outs, lses = _run_attn(h, qkv, B, L, H, D, segs, ratios, prescaled=True)
+    q, k, v = (qkv[:, i * E:(i + 1) * E].float().view(B, L, H, D) for i in range(3))
+    o_ref, l_ref = orc.branch_attention(q, k, v, 300, 1, scale=0.6931471805599453)
+    o = outs[0].float().cpu().view(B, 1, L, H, D).permute(0, 1, 3, 2, 4)
+    l = lses[0].cpu().view(B, 1, H, L)
+    assert torch.isfinite(o).all() and torch.isfinite(l).all()
+    assert (o - o_ref).abs().max().item() <= 1.2e-2 * max(1.0, o_ref.abs().max().item())
+    assert (l - l_ref).abs().max().item() <= LSE_ATOL + 1e-5 * l_ref.abs().max().item()
+    # head 0 is dominated by key 150, head 1 by the last tile's keys
+    assert (o[0, 0, 0] - v[0, 150, 0]).abs().max().item() <= 1e-2 * max(1.0, v[0, 150, 0].abs().max().item())
+    # the input does overflow the no-max kernel: without the fixup pass (test hook VAR 342019)
+    # head 0's rows carry the lse marker, head 1's (renormalised) rows are already right
+    monkeypatch.setenv("GP_ATTN_IMPL", "2")
+    monkeypatch.setenv("GP_ATTN_VAR", "342019")
+    outs2, lses2 = _run_attn(h, qkv, B, L, H, D, segs, ratios, prescaled=True)
+    l2 = lses2[0].cpu().view(B, 1, H, L)
+    assert (l2[0, 0, 0].view(torch.int32) == 0x7FC0DEAD).any()
+    assert (l2[0, 0, 1] - l_ref[0, 0, 1]).abs().max().item() <= LSE_ATOL + 1e-5 * l_ref.abs().max().item()
 
 
 def test_attention_large_scores_and_empty_heads(attn_impl):
