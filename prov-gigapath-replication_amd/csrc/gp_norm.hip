@@ -326,6 +326,103 @@ __global__ __launch_bounds__(256) void gelu_ln_wave2_kernel(const uint16_t* h, c
 }
 
 // ---------------------------------------------------------------------------------------
+// GELU+LN through a lookup table (default for F = 3072 / 4096): the input is bf16 and the GELU output
+// is rounded to bf16 before the LN, so GELU is a function of the 16 input bits.  Each block first
+// fills a 65536-entry table in LDS with exactly bf16(gelu_erf(x)) (the v2 arithmetic, so the output is
+// bit-identical to gelu_ln_wave2_kernel), then its 16 waves walk rows grid-stride with the v2 LN
+// arithmetic, one ds_read_u16 per element instead of ~13 VALU operations with a v_rcp and a v_exp
+// (v2 is VALU-issue bound at ~1130 instructions per row per wave).  128 KiB table + the LN weights:
+// one block per CU, launched once per CU; 8 waves (16 waves and deeper row prefetch measured slower).
+template <int EPL, int NW = 8>
+__global__ __launch_bounds__(NW * 64) void gelu_ln_lut_kernel(const uint16_t* h, const float* __restrict__ ln_w,
+                                                          const float* __restrict__ ln_b, float eps,
+                                                          uint16_t* out, int64_t rows) {
+  constexpr int C = 64 * EPL, NK = EPL / 8;
+  __shared__ __attribute__((aligned(16))) uint16_t tab[65536];
+  __shared__ __attribute__((aligned(16))) float sw[C], sb[C];
+  for (int g = threadIdx.x; g < 65536 / 8; g += NW * 64) {   // 8 consecutive entries per step
+    float v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = gelu_erf(__uint_as_float((uint32_t)(8 * g + i) << 16));
+    *reinterpret_cast<uint4*>(tab + 8 * g) = pack8(v);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  for (int i = threadIdx.x * 4; i < C; i += NW * 64 * 4) {
+    *reinterpret_cast<float4*>(sw + i) = *reinterpret_cast<const float4*>(ln_w + i);
+    *reinterpret_cast<float4*>(sb + i) = *reinterpret_cast<const float4*>(ln_b + i);
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int64_t stride = (int64_t)gridDim.x * NW;
+  int64_t row = (int64_t)blockIdx.x * NW + (threadIdx.x >> 6);
+  uint4 cur[NK], nxt[NK];
+  if (row < rows) {
+#pragma unroll
+    for (int k = 0; k < NK; ++k) cur[k] = *reinterpret_cast<const uint4*>(h + row * C + k * 512 + 8 * lane);
+  }
+  auto look2 = [&](uint32_t w) -> uint32_t {   // two bf16 inputs -> two bf16 GELU outputs
+    return (uint32_t)tab[w & 0xffffu] | ((uint32_t)tab[w >> 16] << 16);
+  };
+  for (; row < rows; row += stride) {
+    if (row + stride < rows) {
+#pragma unroll
+      for (int k = 0; k < NK; ++k)
+        nxt[k] = *reinterpret_cast<const uint4*>(h + (row + stride) * C + k * 512 + 8 * lane);
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      cur[k] = make_uint4(look2(cur[k].x), look2(cur[k].y), look2(cur[k].z), look2(cur[k].w));
+      float v[8];
+      unpack8(cur[k], v);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s += v[i];
+      __builtin_amdgcn_sched_barrier(0);   // bounds the lookups in flight (registers: 1024-thread block)
+    }
+    const float mean = wave_sum(s) / (float)C;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      float v[8];
+      unpack8(cur[k], v);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float d = v[i] - mean;
+        q += d * d;
+      }
+    }
+    const float rstd = rsqrtf(wave_sum(q) / (float)C + eps);
+    const int wo = 8 * lane;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      float v[8], wv[8], bv[8];
+      unpack8(cur[k], v);
+      *reinterpret_cast<float4*>(wv) = *reinterpret_cast<const float4*>(sw + k * 512 + wo);
+      *reinterpret_cast<float4*>(wv + 4) = *reinterpret_cast<const float4*>(sw + k * 512 + wo + 4);
+      *reinterpret_cast<float4*>(bv) = *reinterpret_cast<const float4*>(sb + k * 512 + wo);
+      *reinterpret_cast<float4*>(bv + 4) = *reinterpret_cast<const float4*>(sb + k * 512 + wo + 4);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = (v[i] - mean) * rstd * wv[i] + bv[i];
+      *reinterpret_cast<uint4*>(out + row * C + k * 512 + 8 * lane) = pack8(v);
+    }
+#pragma unroll
+    for (int k = 0; k < NK; ++k) cur[k] = nxt[k];
+  }
+}
+
+static int gp_num_cus() {       // per-device cache of the CU count (LUT kernel: one block per CU)
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cache[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cache[dev] = n;
+  }
+  return cache[dev];
+}
+
+// ---------------------------------------------------------------------------------------
 template <int EPL>
 __global__ __launch_bounds__(256) void layernorm_f32_kernel(const float* __restrict__ x, int64_t row_stride,
                                                             const float* __restrict__ ln_w,
@@ -432,9 +529,18 @@ extern "C" int gp_gelu_layernorm(const uint16_t* h, const float* ln_w, const flo
   GP_REQUIRE(h && ln_w && ln_b && out, "gp_gelu_layernorm: null pointer");
   hipStream_t s = gp_stream(stream);
   GP_REQUIRE(rows < (int64_t)0x7fffffff, "gp_gelu_layernorm: too many rows");
-  const char* impl_env = getenv("GP_GELU_IMPL");    // A/B: 1 = block per row, 2 = wave per row (v1)
-  const int impl = impl_env ? atoi(impl_env) : 3;
-  if (impl == 3) {     // default: wave per row, grid-stride with next-row prefetch, bf16-rounded GELU
+  const char* impl_env = getenv("GP_GELU_IMPL");    // A/B: 1 = block per row, 2 = wave per row (v1), 3 = v2, 5 = table
+  const int impl = impl_env ? atoi(impl_env) : ((cols == 3072 || cols == 4096) ? 5 : 3);
+  if (impl == 5) {     // default where the table + LN weights fit in LDS: GELU by lookup table
+    GP_REQUIRE(cols == 3072 || cols == 4096, "gp_gelu_layernorm: GP_GELU_IMPL=5 needs cols 3072 or 4096");
+    const int64_t want = (rows + 7) / 8;
+    const int cus = gp_num_cus();
+    const unsigned nb = (unsigned)(want < cus ? want : cus);
+    if (cols == 3072) gelu_ln_lut_kernel<48><<<nb, 512, 0, s>>>(h, ln_w, ln_b, eps, out, rows);
+    else gelu_ln_lut_kernel<64><<<nb, 512, 0, s>>>(h, ln_w, ln_b, eps, out, rows);
+    return gp_check_launch("gp_gelu_layernorm");
+  }
+  if (impl == 3) {     // v2 (default for F = 6144): wave per row, grid-stride with next-row prefetch, bf16-rounded GELU
     const int64_t want = (rows + 3) / 4;
     const unsigned nb = (unsigned)(want < 1024 ? want : 1024);
     switch (cols / 64) {

@@ -17,7 +17,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--rows", type=int, default=70001)
 ap.add_argument("--cols", type=int, default=3072)
 ap.add_argument("--iters", type=int, default=20)
-ap.add_argument("--impls", default="3,2")
+ap.add_argument("--impls", default="3,5")
 args = ap.parse_args()
 M, F = args.rows, args.cols
 g = torch.Generator(device="cuda").manual_seed(0)
