@@ -1751,8 +1751,12 @@ struct MergeArgs {
 // branch-order accumulation) followed by inner_attn_ln.
 constexpr int kTPW = 1;
 
-template <int EPL, int D, bool kTab = false>
+// NBR < GP_MAX_BRANCHES: the launch guarantees a.nbranch == NBR, so the branch loops have a
+// compile-time trip count (the 5-branch schedule of every registered arch: 3 dead branches of
+// position stepping, address math and exp fewer per token)
+template <int EPL, int D, bool kTab = false, int NBR = GP_MAX_BRANCHES>
 __global__ __launch_bounds__(256) void branch_merge_kernel(const MergeArgs a) {
+  const int nbr = NBR < GP_MAX_BRANCHES ? NBR : a.nbranch;
   const int lane = threadIdx.x & 63;
   const int run = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + (int)(threadIdx.x >> 6));
   const int total = (int)(a.B * a.ntok);
@@ -1769,8 +1773,8 @@ __global__ __launch_bounds__(256) void branch_merge_kernel(const MergeArgs a) {
     }
     slide_tok0 = a.tok_off[lo];
 #pragma unroll
-    for (int b = 0; b < GP_MAX_BRANCHES; ++b)
-      if (b < a.nbranch) tb[b] = a.mtab[lo * a.nbranch + b];
+    for (int b = 0; b < NBR; ++b)
+      if (b < nbr) tb[b] = a.mtab[lo * a.nbranch + b];
   }
   const int nt = (int)a.ntok;
   const int E = 64 * EPL;
@@ -1790,8 +1794,8 @@ __global__ __launch_bounds__(256) void branch_merge_kernel(const MergeArgs a) {
         p = (int)a.tok_lo + (row - bidx * nt);
       }
 #pragma unroll
-      for (int b = 0; b < GP_MAX_BRANCHES; ++b)
-        if (b < a.nbranch) {
+      for (int b = 0; b < NBR; ++b)
+        if (b < nbr) {
           const MergeBranch& mb = kTab ? tb[b] : a.br[b];
           pn[b] = (int)div_magic((uint32_t)p, mb.dg);
           pt[b] = p - pn[b] * mb.g.g;
@@ -1801,8 +1805,8 @@ __global__ __launch_bounds__(256) void branch_merge_kernel(const MergeArgs a) {
     } else {
       ++p;
 #pragma unroll
-      for (int b = 0; b < GP_MAX_BRANCHES; ++b)
-        if (b < a.nbranch) {
+      for (int b = 0; b < NBR; ++b)
+        if (b < nbr) {
           const GpBranch& g = (kTab ? tb[b] : a.br[b]).g;
           if (++pt[b] == g.g) { pt[b] = 0; ++pn[b]; pi[b] = 0; pj[b] = 0; }
           else if (++pj[b] == g.r) { pj[b] = 0; ++pi[b]; }
@@ -1813,10 +1817,10 @@ __global__ __launch_bounds__(256) void branch_merge_kernel(const MergeArgs a) {
     bool cov[GP_MAX_BRANCHES];
     uint2 ob[GP_MAX_BRANCHES][EPL / 4];
 #pragma unroll
-    for (int b = 0; b < GP_MAX_BRANCHES; ++b) {
+    for (int b = 0; b < NBR; ++b) {
       lse[b] = -1e8f;
       cov[b] = false;
-      if (b < a.nbranch) {
+      if (b < nbr) {
         const GpBranch& g = (kTab ? tb[b] : a.br[b]).g;
         const int lph = g.hpg * (D / EPL);        // lanes per head group
         cov[b] = lane >= pj[b] * lph && lane < (pj[b] + 1) * lph;
@@ -1831,15 +1835,15 @@ __global__ __launch_bounds__(256) void branch_merge_kernel(const MergeArgs a) {
     }
     float mx = -INFINITY;
 #pragma unroll
-    for (int b = 0; b < GP_MAX_BRANCHES; ++b)
-      if (b < a.nbranch) {
+    for (int b = 0; b < NBR; ++b)
+      if (b < nbr) {
         if (cov[b] && lse[b] == 0.f) lse[b] = -1e8f;   // dilated_attention.py:46
         mx = fmaxf(mx, lse[b]);
       }
     float wsum = 0.f;
 #pragma unroll
-    for (int b = 0; b < GP_MAX_BRANCHES; ++b)
-      if (b < a.nbranch) {
+    for (int b = 0; b < NBR; ++b)
+      if (b < nbr) {
         lse[b] = expf(lse[b] - mx);
         wsum += lse[b];
       }
@@ -1848,8 +1852,8 @@ __global__ __launch_bounds__(256) void branch_merge_kernel(const MergeArgs a) {
 #pragma unroll
     for (int e = 0; e < EPL; ++e) acc[e] = 0.f;
 #pragma unroll
-    for (int b = 0; b < GP_MAX_BRANCHES; ++b) {
-      if (b < a.nbranch && cov[b]) {
+    for (int b = 0; b < NBR; ++b) {
+      if (b < nbr && cov[b]) {
         const float wb = lse[b] * inv;
 #pragma unroll
         for (int q = 0; q < EPL / 4; ++q) {
@@ -2169,7 +2173,8 @@ extern "C" int gp_branch_merge_ln_window(const uint16_t* const* o_in, const floa
   hipStream_t s = gp_stream(stream);
   switch (E) {
     case 768:
-      if (D == 48) branch_merge_kernel<12, 48><<<nb, 256, 0, s>>>(a);
+      if (D == 48 && nbranch == 5) branch_merge_kernel<12, 48, false, 5><<<nb, 256, 0, s>>>(a);
+      else if (D == 48) branch_merge_kernel<12, 48><<<nb, 256, 0, s>>>(a);
       else if (D == 96) branch_merge_kernel<12, 96><<<nb, 256, 0, s>>>(a);
       else branch_merge_kernel<12, 12><<<nb, 256, 0, s>>>(a);
       break;
