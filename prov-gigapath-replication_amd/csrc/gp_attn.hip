@@ -438,6 +438,14 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   // 524288, the exact per-tile-max kernel, run right after on the same stream) recomputes every
   // block holding a marker and exits at once elsewhere.
   constexpr bool kNM = (VAR & 262144) != 0;
+  // VAR & 1048576 (with 262144): no offset at all -- S starts from C = 0 (no init MFMA, m = 0), so
+  // p = exp2(s) of the pre-scaled log2-domain score; no max, no renormalisation.  Valid while the
+  // real-key row sum l stays in [2^-100, 2^100] (every p then keeps full bf16 precision relative to
+  // the largest); outside it (or non-finite) the row gets the lse marker and the exact fixup pass
+  // recomputes its block.  With zero-pad keys (npad > 0) a tiny l is not flagged: the pads (p = 1)
+  // then dominate exactly as in the reference.
+  constexpr bool kZM = (VAR & 1048576) != 0;
+  static_assert(!kZM || kNM, "VAR 1048576 builds on VAR 262144");
   constexpr bool kFix = (VAR & 524288) != 0;
   static_assert(!(kNM && kFix), "the fixup pass is the exact kernel");
   static_assert(!kMI || (D == 48 && kPre && !kMK && (VAR & 1) == 0), "VAR 4096 needs D = 48, kPre, no VAR 8/1");
@@ -763,7 +771,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
       // in its own registers, rewritten only on a rescale) instead of initialising per tile
       const float init = (kPre && sub > 0) ? -m_run : 0.f;
       f32x16 ini;
-      if constexpr (kMI) {
+      if constexpr (kMI && !kZM) {
         f32x16 zero;
   #pragma unroll
         for (int r = 0; r < 16; ++r) zero[r] = 0.f;
@@ -781,7 +789,10 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   #pragma unroll
       for (int u = 0; u < 2; ++u) {
         f32x16 acc;
-        if constexpr (kMI) {
+        if constexpr (kZM) {
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+        } else if constexpr (kMI) {
           acc = ini;
         } else if constexpr (kMK) {
   #pragma unroll
@@ -814,7 +825,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
       }
 
       // ---- online softmax with deferred rescale (two independent max chains)
-      const bool do_max = !kNM || sub == 0;
+      const bool do_max = !kZM && (!kNM || sub == 0);
       float mx = 0.f;
       if (do_max) {
       float mxa = sacc[0][0], mxb = sacc[1][0];
@@ -830,7 +841,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
       }
       }
       bf16x8 pf[2][2];
-      if constexpr (kNM) {
+      if constexpr (kNM && !kZM) {
         if (!do_max) {
           // l of the tiles so far (the ones row); renormalise when it grew past 2^24
           const float lc = oacc[1][8];
@@ -1040,6 +1051,12 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
     l = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
   }
   const int npad = g.m - c;
+  bool zm_bad = false;
+  if constexpr (kZM) {
+    m_run = 0.f;
+    const uint32_t eb = __float_as_uint(l) & 0x7f800000u;
+    zm_bad = eb == 0x7f800000u || !(l <= 0x1p100f) || (npad == 0 && !(l >= 0x1p-100f));
+  }
   float mr = m_run, so = 1.f;
   if (npad > 0) {
     const float mf = fmaxf(mr, 0.f);
@@ -1065,7 +1082,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
       }
     float lse = (mr + __builtin_amdgcn_logf(l)) * 0.69314718055994530942f;
     if constexpr (kNM) {     // overflowed (some p = inf): flag the row for the fixup pass
-      if ((__float_as_uint(l) & 0x7f800000u) == 0x7f800000u || !(l > 0.f)) lse = __uint_as_float(kLseRedo);
+      if ((__float_as_uint(l) & 0x7f800000u) == 0x7f800000u || !(l > 0.f) || zm_bad) lse = __uint_as_float(kLseRedo);
     }
     if (h == 0) br.lse[((int64_t)bn * a.H + hh) * g.m + i] = lse;
   }
@@ -2065,6 +2082,13 @@ extern "C" int gp_dilated_attn_fwd_ex(const uint16_t* q, int64_t q_row_stride, i
       case 10243: dilated_attn32_kernel<48, true, 4, 10242, 5><<<(unsigned)items, 256, 0, s>>>(a); break;
       case 79874: dilated_attn32_kernel<48, true, 4, 79874><<<(unsigned)items, 256, 0, s>>>(a); break;
       case 210946: dilated_attn32_kernel<48, true, 4, 210946><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 1390594:  // 342018 with no offset at all (S from C = 0), then the fixup pass
+        dilated_attn32_kernel<48, true, 4, 1390594><<<(unsigned)items, 256, 0, s>>>(a);
+        dilated_attn32_kernel<48, true, 4, 79874 + 524288><<<(unsigned)((items + kFixItems - 1) / kFixItems), 256, 0, s>>>(a);
+        break;
+      case 1390595:  // test hook: 1390594 WITHOUT the fixup pass
+        dilated_attn32_kernel<48, true, 4, 1390594><<<(unsigned)items, 256, 0, s>>>(a);
+        break;
       case 342019:   // test hook: 342018 WITHOUT the fixup pass (overflowed rows keep the lse marker)
         dilated_attn32_kernel<48, true, 4, 342018><<<(unsigned)items, 256, 0, s>>>(a);
         break;
@@ -2089,9 +2113,10 @@ extern "C" int gp_dilated_attn_fwd_ex(const uint16_t* q, int64_t q_row_stride, i
     // itself +5-7 % over VAR 2) and the -m start block of S from one MFMA of an exact hi + lo bf16
     // pair instead of 16 v_mov (VAR 4096: +1.5 %); VAR 2 where the descriptor layout does not fit
     if (D == 48 && kv_desc_ok) {
-      // VAR 342018 = 79874 without the per-tile row max after tile 0 (+2.7 %), then the fixup pass
-      // (exact kernel, exits at once unless a block overflowed)
-      dilated_attn32_kernel<48, true, 4, 342018><<<(unsigned)items, 256, 0, s>>>(a);
+      // VAR 1390594 = 79874 without any row max or offset (S from C = 0, p = exp2(s); 342018 keeps the
+      // first tile's max as the offset: +1 % in the forward for it, lse error up to ~2^-8 instead of
+      // ~2^-9), then the fixup pass (exact kernel, exits at once unless a block was flagged)
+      dilated_attn32_kernel<48, true, 4, 1390594><<<(unsigned)items, 256, 0, s>>>(a);
       dilated_attn32_kernel<48, true, 4, 79874 + 524288><<<(unsigned)((items + kFixItems - 1) / kFixItems), 256, 0, s>>>(a);
     }
     else if (D == 48) dilated_attn32_kernel<48, true, 4, 2><<<(unsigned)items, 256, 0, s>>>(a);
@@ -2337,7 +2362,7 @@ extern "C" int gp_dilated_attn_fwd_varlen(const void* plan_host, const void* pla
   a.ntab = h.ntab;
   a.d_H = make_div_magic((uint32_t)h.H);
   // the single-slide default's variant, so each packed slide's outputs equal its own launch's
-  dilated_attn32_kernel<48, true, 4, 342018, 2, true><<<(unsigned)h.total_items, 256, 0, gp_stream(stream)>>>(a);
+  dilated_attn32_kernel<48, true, 4, 1390594, 2, true><<<(unsigned)h.total_items, 256, 0, gp_stream(stream)>>>(a);
   dilated_attn32_kernel<48, true, 4, 79874 + 524288, 2, true><<<(unsigned)((h.total_items + kFixItems - 1) / kFixItems), 256, 0, gp_stream(stream)>>>(a);
   return gp_check_launch("gp_dilated_attn_fwd_varlen");
 }

@@ -176,14 +176,16 @@ def test_dilated_attention_vs_oracle(name, B, L, segs, ratios, attn_impl):
         dl = (l - l_ref).abs()[mask].max().item()
         assert do <= 1.2e-2 * max(1.0, o_ref.abs().max().item()), (name, b, do)
         # LSE: the softmax row sum is accumulated by the MFMA from the bf16-rounded P it also
-        # uses for P.V (relative error <= 2^-9 per term) -> |d lse| <= ~2e-3
+        # uses for P.V (RNE to 8 significant bits: relative error <= 2^-8 per term); the default
+        # kernel uses no max offset, so even a dominant term is rounded -> |d lse| <= ln(1 + 2^-8)
         assert dl <= LSE_ATOL, (name, b, dl)
 
 
-LSE_ATOL = 2.5e-3
+LSE_ATOL = 4e-3      # ln(1 + 2^-8) = 3.9e-3
 
 
-@pytest.mark.parametrize("impl", ["2", "3", "2@2", "2@2050", "2@10242", "2@14338", "2@79874", "2@210946", "4@7"])
+@pytest.mark.parametrize("impl", ["2", "3", "2@2", "2@2050", "2@10242", "2@14338", "2@79874", "2@210946", "2@342018",
+                                  "2@1390594", "4@7"])
 @pytest.mark.parametrize("name,B,L,segs,ratios", ATTN_CASES)
 def test_dilated_attention_prescaled_q(name, B, L, segs, ratios, impl, monkeypatch):
     # "2": the default (LDS-DMA staging, MFMA-initialised running-max block); "2@2": global-load
@@ -215,7 +217,7 @@ def test_dilated_attention_prescaled_q(name, B, L, segs, ratios, impl, monkeypat
         assert (l - l_ref).abs()[mask].max().item() <= LSE_ATOL, (name, b)
 
 
-@pytest.mark.parametrize("impl", ["2", "2@342018"])
+@pytest.mark.parametrize("impl", ["2", "2@342018", "2@1390594"])
 def test_attention_no_max_overflow_fixup_and_renormalise(impl, monkeypatch):
     """Default kernel (no per-tile row max after the first 64 keys): head 0 has one key whose
     log2-domain score (200) is > 127 above every earlier key, so exp2 overflows and the block must
