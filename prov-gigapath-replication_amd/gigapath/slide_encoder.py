@@ -240,7 +240,10 @@ class LongNetViT(nn.Module):
             self._graphs.pop(old)
             self._graph_ws.pop(old, None)
         stream = self.graph_stream()
-        sx, sc = x.detach().clone(), c.detach().clone().contiguous()
+        # the static input is kept in bf16 (the forward's first use converts to bf16 anyway): the
+        # per-replay sx.copy_(x) then converts while copying, instead of a full-precision copy plus
+        # a conversion pass inside the graph (one 0.86 GB HBM round trip fewer at 70k tiles)
+        sx, sc = x.detach().to(torch.bfloat16, copy=True).contiguous(), c.detach().clone().contiguous()
         cur = torch.cuda.current_stream()
         stream.wait_stream(cur)
         with torch.cuda.stream(stream):
