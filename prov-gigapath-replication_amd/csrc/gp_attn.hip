@@ -1861,10 +1861,12 @@ __global__ __launch_bounds__(256) void branch_merge_kernel(const MergeArgs a) {
 #pragma unroll
     for (int b = 0; b < NBR; ++b)
       if (b < nbr) {
-        lse[b] = expf(lse[b] - mx);
+        // v_exp_f32 / v_rcp_f32 (1 ulp) instead of the libm expf and the IEEE division sequence: the
+        // weights are fp32 (the reference rounds them to the activation dtype, dilated_attention.py:128)
+        lse[b] = fast_exp2((lse[b] - mx) * 1.44269504088896340736f);
         wsum += lse[b];
       }
-    const float inv = 1.0f / wsum;
+    const float inv = __builtin_amdgcn_rcpf(wsum);
     float acc[EPL];
 #pragma unroll
     for (int e = 0; e < EPL; ++e) acc[e] = 0.f;
