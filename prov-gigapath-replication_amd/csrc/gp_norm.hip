@@ -3,6 +3,8 @@
 // lane owning EPL = cols/64 contiguous values (16-byte fp32 / 8-byte bf16 accesses).
 #include <math.h>
 
+#include <atomic>
+
 #include <stdlib.h>
 
 #include "gp_api.h"
@@ -333,19 +335,37 @@ __global__ __launch_bounds__(256) void gelu_ln_wave2_kernel(const uint16_t* h, c
 // arithmetic, one ds_read_u16 per element instead of ~13 VALU operations with a v_rcp and a v_exp
 // (v2 is VALU-issue bound at ~1130 instructions per row per wave).  128 KiB table + the LN weights:
 // one block per CU, launched once per CU; 8 waves (16 waves and deeper row prefetch measured slower).
-template <int EPL, int NW = 8>
+// kCopy: the table is copied into LDS from g_gelu_tab (filled once per device by gelu_tab_fill_kernel,
+// the same arithmetic, so the entries are bit-identical) -- 128 KiB from L2 instead of 65,536 gelu_erf
+// evaluations per block (~8 % of the launch at 70k rows).  Without kCopy each block evaluates the table.
+__device__ __attribute__((aligned(16))) uint16_t g_gelu_tab[65536];
+
+__global__ __launch_bounds__(256) void gelu_tab_fill_kernel() {
+  const int g = (int)blockIdx.x * 256 + (int)threadIdx.x;   // 8192 groups of 8 consecutive entries
+  float v[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = gelu_erf(__uint_as_float((uint32_t)(8 * g + i) << 16));
+  *reinterpret_cast<uint4*>(g_gelu_tab + 8 * g) = pack8(v);
+}
+
+template <int EPL, int NW = 8, bool kCopy = false>
 __global__ __launch_bounds__(NW * 64) void gelu_ln_lut_kernel(const uint16_t* h, const float* __restrict__ ln_w,
                                                           const float* __restrict__ ln_b, float eps,
                                                           uint16_t* out, int64_t rows) {
   constexpr int C = 64 * EPL, NK = EPL / 8;
   __shared__ __attribute__((aligned(16))) uint16_t tab[65536];
   __shared__ __attribute__((aligned(16))) float sw[C], sb[C];
-  for (int g = threadIdx.x; g < 65536 / 8; g += NW * 64) {   // 8 consecutive entries per step
-    float v[8];
+  if constexpr (kCopy) {
+    for (int g = threadIdx.x; g < 65536 / 8; g += NW * 64)
+      *reinterpret_cast<uint4*>(tab + 8 * g) = *reinterpret_cast<const uint4*>(g_gelu_tab + 8 * g);
+  } else {
+    for (int g = threadIdx.x; g < 65536 / 8; g += NW * 64) {   // 8 consecutive entries per step
+      float v[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = gelu_erf(__uint_as_float((uint32_t)(8 * g + i) << 16));
-    *reinterpret_cast<uint4*>(tab + 8 * g) = pack8(v);
-    __builtin_amdgcn_sched_barrier(0);
+      for (int i = 0; i < 8; ++i) v[i] = gelu_erf(__uint_as_float((uint32_t)(8 * g + i) << 16));
+      *reinterpret_cast<uint4*>(tab + 8 * g) = pack8(v);
+      __builtin_amdgcn_sched_barrier(0);
+    }
   }
   for (int i = threadIdx.x * 4; i < C; i += NW * 64 * 4) {
     *reinterpret_cast<float4*>(sw + i) = *reinterpret_cast<const float4*>(ln_w + i);
@@ -420,6 +440,24 @@ static int gp_num_cus() {       // per-device cache of the CU count (LUT kernel:
     cache[dev] = n;
   }
   return cache[dev];
+}
+
+// g_gelu_tab of the current device is filled (once: a fill launch on the caller's stream, then a
+// synchronize of that stream, so no other stream can see the flag before the table is complete).  While
+// the stream is being captured into a graph the fill cannot be synchronised: the caller then takes the
+// self-filling kernel until an eager call has filled the table.  Two threads filling at once write the
+// same bytes.
+static bool gelu_tab_ready(hipStream_t s) {
+  static std::atomic<bool> ready[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
+  if (ready[dev].load(std::memory_order_acquire)) return true;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
+  gelu_tab_fill_kernel<<<65536 / 8 / 256, 256, 0, s>>>();
+  if (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess) return false;
+  ready[dev].store(true, std::memory_order_release);
+  return true;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -531,13 +569,20 @@ extern "C" int gp_gelu_layernorm(const uint16_t* h, const float* ln_w, const flo
   GP_REQUIRE(rows < (int64_t)0x7fffffff, "gp_gelu_layernorm: too many rows");
   const char* impl_env = getenv("GP_GELU_IMPL");    // A/B: 1 = block per row, 2 = wave per row (v1), 3 = v2, 5 = table
   const int impl = impl_env ? atoi(impl_env) : ((cols == 3072 || cols == 4096) ? 5 : 3);
-  if (impl == 5) {     // default where the table + LN weights fit in LDS: GELU by lookup table
-    GP_REQUIRE(cols == 3072 || cols == 4096, "gp_gelu_layernorm: GP_GELU_IMPL=5 needs cols 3072 or 4096");
+  if (impl == 5 || impl == 4) {     // default where the table + LN weights fit in LDS: GELU by lookup table
+    GP_REQUIRE(cols == 3072 || cols == 4096, "gp_gelu_layernorm: GP_GELU_IMPL=4/5 needs cols 3072 or 4096");
     const int64_t want = (rows + 7) / 8;
     const int cus = gp_num_cus();
     const unsigned nb = (unsigned)(want < cus ? want : cus);
-    if (cols == 3072) gelu_ln_lut_kernel<48><<<nb, 512, 0, s>>>(h, ln_w, ln_b, eps, out, rows);
-    else gelu_ln_lut_kernel<64><<<nb, 512, 0, s>>>(h, ln_w, ln_b, eps, out, rows);
+    // GP_GELU_IMPL=4: the same kernel evaluating its table per block (A/B and bit-identity reference)
+    const bool copy = impl == 5 && gelu_tab_ready(s);
+    if (cols == 3072) {
+      if (copy) gelu_ln_lut_kernel<48, 8, true><<<nb, 512, 0, s>>>(h, ln_w, ln_b, eps, out, rows);
+      else gelu_ln_lut_kernel<48><<<nb, 512, 0, s>>>(h, ln_w, ln_b, eps, out, rows);
+    } else {
+      if (copy) gelu_ln_lut_kernel<64, 8, true><<<nb, 512, 0, s>>>(h, ln_w, ln_b, eps, out, rows);
+      else gelu_ln_lut_kernel<64><<<nb, 512, 0, s>>>(h, ln_w, ln_b, eps, out, rows);
+    }
     return gp_check_launch("gp_gelu_layernorm");
   }
   if (impl == 3) {     // v2 (default for F = 6144): wave per row, grid-stride with next-row prefetch, bf16-rounded GELU

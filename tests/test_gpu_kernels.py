@@ -366,6 +366,27 @@ def test_gelu_layernorm_grid_stride_rows(F):
     assert err <= 2 ** -8 * ref.abs().max().item(), err
 
 
+def test_gelu_table_copy_bit_identical(monkeypatch):
+    """The default GELU+LN launch copies a once-per-device table (g_gelu_tab) into LDS; it must equal,
+    bit for bit, the kernel that evaluates its table per block (GP_GELU_IMPL=4) and the v2 kernel that
+    evaluates GELU per element (GP_GELU_IMPL=3)."""
+    h = _hip()
+    g = torch.Generator().manual_seed(7)
+    M, F = 4099, 3072
+    f = (torch.randn(M, F, generator=g) * 3).bfloat16()
+    f[0, :1024] = torch.arange(-512, 512).float().bfloat16() * 0.03   # a sweep across the GELU knee
+    fw = (1 + 0.1 * torch.randn(F, generator=g)).to(DEV)
+    fb = (0.1 * torch.randn(F, generator=g)).to(DEV)
+    outs = {}
+    for impl in ("5", "4", "3", "5"):
+        monkeypatch.setenv("GP_GELU_IMPL", impl)
+        o = torch.empty(M, F, dtype=torch.bfloat16, device=DEV)
+        h.gelu_layernorm(f.to(DEV), fw, fb, 1e-5, o, M, F)
+        torch.cuda.synchronize()
+        outs.setdefault(impl, o.cpu())
+        assert torch.equal(o.cpu().view(torch.int16), outs["5"].view(torch.int16)), impl
+
+
 def test_residual_gelu_layernorm_kernels():
     h = _hip()
     rng = np.random.default_rng(0)
