@@ -3,6 +3,10 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--tiles T]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
+Without a launcher (`WORLD_SIZE` unset), `--gpus N > 1` starts the N ranks itself: it runs
+torch.distributed.run as a child process before anything touches the GPU.  Under a launcher,
+WORLD_SIZE must equal --gpus (exit 2 otherwise).
+
 A step = one gigapath_slide_enc12l768d forward (bf16, inference) over one synthetic slide of
 --tiles tiles, inputs and weights resident in HBM.  Default: 70,000 tiles (BASELINE config C3,
 the north star's 1-GPU target) at N = 1; 256,000 tiles (config C4, the north star's 8-GPU
@@ -70,8 +74,48 @@ def cpu_baseline(n_tiles, threads):
         t2 = time.perf_counter()
     full = (t1 - t0) + cfg["depth"] * (t2 - t1)
     return {"value": round(n_tiles / full, 2), "unit": "tiles/s", "cores": threads, "kind": "port",
-            "sample": "oracle fp32 torch-CPU: embed + 1 of 12 layers of the %d-tile slide (%.1f s), x12 layers "
-                      "extrapolated (%.1f s per forward)" % (n_tiles, t2 - t0, full)}
+            "sample": "EXTRAPOLATED: oracle fp32 torch-CPU, embed + 1 of 12 layers of the %d-tile slide (%.1f s), "
+                      "x12 layers (%.1f s per forward)" % (n_tiles, t2 - t0, full)}
+
+
+def cpu_full_forwards(sizes, threads):
+    """The fp32 CPU oracle's WHOLE 12-layer forward (all_layer_embed=True) of the C1 / C2 slides,
+    timed in full (no extrapolation): BASELINE.md §4's CPU rows."""
+    import oracle
+    torch.set_num_threads(threads)
+    cfg = oracle.arch_config(ARCH)
+    W = {k: torch.from_numpy(v) for k, v in oracle.make_weights(cfg, seed=0).items()}
+    res = {}
+    for name, n in sizes:
+        x, coords = make_slide(n)
+        with torch.no_grad():
+            t0 = time.perf_counter()
+            out = oracle.slide_encoder_forward(W, x, coords, cfg, all_layer_embed=True)
+            dt = time.perf_counter() - t0
+        assert all(torch.isfinite(o).all() for o in out)
+        res[name] = {"tiles": n, "value": round(n / dt, 2), "unit": "tiles/s", "seconds": round(dt, 2),
+                     "cores": threads, "kind": "port", "sample": "full 12-layer fp32 forward, timed"}
+    return res
+
+
+def config_label(n_tiles, world, sp):
+    """BASELINE.json config this slide size is (C1..C4), or a plain description."""
+    if sp:
+        return "C4" if n_tiles == 256000 else "SP"
+    return {1024: "C1", 16384: "C2", 70000: "C3"}.get(n_tiles, "custom (%d tiles)" % n_tiles)
+
+
+def spawn_ranks(ngpus):
+    """`python bench.py --gpus N` without a launcher: start N ranks under torch.distributed.run as a
+    CHILD process (nothing here has touched the GPU yet) and return its exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(ngpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 def pmc_traffic(n_tiles, kernel):
@@ -107,9 +151,19 @@ def main():
     ap.add_argument("--timing-steps", type=int, default=2, help="eager steps with per-kernel HIP events")
     ap.add_argument("--mixed-slides", type=int, default=32, help="--mode mixed: slides in the batch")
     ap.add_argument("--no-graphs", action="store_true", help="eager launches instead of HIP graph replay")
+    ap.add_argument("--no-cpu-full", action="store_true", help="skip the full C1/C2 CPU forwards")
+    ap.add_argument("--dry-run", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print("bench.py: WORLD_SIZE=%d but --gpus %d" % (world, args.gpus), file=sys.stderr)
+        sys.exit(2)
+    if args.dry_run:        # launcher plumbing check only (tests/test_bench_cli.py): no GPU, no work
+        print(json.dumps({"rank": int(os.environ.get("RANK", "0")), "world": world}), flush=True)
+        return
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     sp = world > 1 and args.mode == "sp"
@@ -235,9 +289,11 @@ def main():
         "config": {"workload": ("C5: %s forward of a 32-slide mixed batch (%d tiles, 2k-100k per slide), "
                                 "LPT data parallel over %d GPUs, all_layer_embed=True" % (ARCH, args.tiles, world))
                                if mixed else
-                               ("%s forward, one %d-tile slide sharded over %d GPUs (sequence parallel), "
-                                "all_layer_embed=True" % (ARCH, args.tiles, world)) if sp else
-                               ("C3: %s forward, one %d-tile slide per GPU, all_layer_embed=True" % (ARCH, args.tiles)),
+                               ("%s: %s forward, one %d-tile slide sharded over %d GPUs (sequence parallel), "
+                                "all_layer_embed=True" % (config_label(args.tiles, world, sp), ARCH, args.tiles, world))
+                               if sp else
+                               ("%s: %s forward, one %d-tile slide per GPU, all_layer_embed=True"
+                                % (config_label(args.tiles, world, sp), ARCH, args.tiles)),
                    "tiles_per_slide": args.tiles, "slides_per_gpu": (1.0 / world) if sp else 1,
                    "parallelism": ("dp%d-lpt" % world) if mixed else ("sp%d" % world) if sp else ("replica x%d" % world)},
         "roofline": {"bound": "mfma", "kernel": "gp_dilated_attn_fwd", "achieved": round(achieved, 2),
@@ -270,6 +326,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not mixed:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         result["cpu_baseline"] = cpu_baseline(args.tiles, threads)
+        if not args.no_cpu_full:
+            result["cpu_full_forwards"] = cpu_full_forwards([("C1", 1024), ("C2", 16384)], threads)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
