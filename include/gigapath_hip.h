@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define GP_ABI_VERSION 3
+#define GP_ABI_VERSION 4
 #define GP_EARG (-1)
 #define GP_MAX_BRANCHES 8
 #define GP_MAX_DESTS 8
@@ -199,11 +199,6 @@ int gp_dilated_attn_fwd_varlen(const void* plan_host, const void* plan_dev, int 
                                void* stream);
 int gp_branch_merge_ln_varlen(const void* plan_host, const void* plan_dev, const float* ln_w,
                               const float* ln_b, float eps, uint16_t* out, void* stream);
-
-/* Diagnostics: per-segment in-kernel cycle sums (s_memtime stamps) of the attention kernel's
- * stamped build (GP_ATTN_VAR=34818), summed over waves: [S MFMAs, softmax, PV, stage store,
- * barrier, whole wave, tiles, waves].  reset != 0 zeroes them.  Not used by the forward. */
-int gp_debug_attn_stamps(int64_t* out8, int reset);
 
 /* Residual add fused with the next pre-LN (encoder.py:141,147 / :159,126):
  *   x += y + bias (fp32 residual stream, in place);  ln_out = LayerNorm(x) (skipped if ln_w == NULL).

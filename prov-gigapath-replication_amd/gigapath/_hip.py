@@ -14,8 +14,8 @@ from typing import Optional, Sequence
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("GIGAPATH_HIP_LIB", os.path.join(_HERE, "_lib", "libgigapath_hip.so"))
-ABI_VERSION = 3
+LIB_PATH = os.path.join(_HERE, "_lib", "libgigapath_hip.so")
+ABI_VERSION = 4
 MAX_BRANCHES = 8
 MAX_DESTS = 8
 
@@ -59,7 +59,6 @@ SIGNATURES = {
     "gp_varlen_plan": [c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp],
     "gp_dilated_attn_fwd_varlen": [c_vp, c_vp, c_i32, c_vp],
     "gp_branch_merge_ln_varlen": [c_vp, c_vp, c_vp, c_vp, c_f32, c_vp, c_vp],
-    "gp_debug_attn_stamps": [c_vp, c_i32],
 }
 _RESTYPES = {"gp_last_error_string": ctypes.c_char_p, "gp_varlen_plan_bytes": c_i64}
 
@@ -71,7 +70,9 @@ class HipLibraryError(RuntimeError):
 
 
 def load_library(path: Optional[str] = None) -> ctypes.CDLL:
-    """Load (once) and type the C ABI.  Raises HipLibraryError if it is absent."""
+    """Load (once) and type the C ABI.  Raises HipLibraryError if it is absent.  `path` loads another
+    build of the same ABI without installing it (tools/attn_lab's A/B library); the typed wrappers
+    below always call the in-tree product library."""
     global _lib
     if _lib is not None and path is None:
         return _lib
@@ -338,11 +339,3 @@ def branch_merge_ln_varlen(plan: VarlenPlan, ln_w, ln_b, eps, out):
     _dev(out, torch.bfloat16, "out")
     _check(lib.gp_branch_merge_ln_varlen(plan.host, _ptr(plan.dev), _ptr(ln_w), _ptr(ln_b), eps, _ptr(out),
                                          _stream()), "gp_branch_merge_ln_varlen")
-
-
-def debug_attn_stamps(reset: bool = True):
-    """Per-segment cycle sums of the stamped attention build (GP_ATTN_VAR=34818), see the header."""
-    lib = load_library()
-    out = (c_i64 * 8)()
-    _check(lib.gp_debug_attn_stamps(out, int(bool(reset))), "gp_debug_attn_stamps")
-    return list(out)

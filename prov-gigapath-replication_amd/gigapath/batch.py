@@ -2,8 +2,9 @@
 
 The reference encodes one slide per call; its fine-tuning collate pads a batch to the longest
 slide (finetune/utils.py:63-98), which changes the result (padded tiles are attended to) and is
-not the parity target.  Here every slide keeps its own B = 1 forward, bit-identical to encoding
-it alone:
+not the parity target.  Here every slide keeps its own B = 1 forward: with packed=False each
+output is bit-identical to encoding the slide alone; the default varlen-packed path matches it up
+to the GEMMs' row-count-dependent rounding (same attention and merge math per slide):
 
 * slides are assigned to ranks by LPT (longest processing time first) on the modelled cost of
   a forward (valid attention FLOPs + GEMM FLOPs + row-kernel bytes, seqpar.token_cost), so the

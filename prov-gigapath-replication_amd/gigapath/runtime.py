@@ -21,6 +21,7 @@ across calls of the same shape.  No CPU fallback exists: every non-GEMM op is a 
 """
 from __future__ import annotations
 
+import functools
 import math
 import os
 from dataclasses import dataclass, field
@@ -49,6 +50,19 @@ def use_tuned_gemms(dev=None):
     torch.cuda.tunable.tuning_enable(False)
     torch.cuda.tunable.record_untuned_enable(False)
     torch.cuda.tunable.read_file(_TUNED)
+
+
+def bf16_compute(fn):
+    """The MI355X path computes in bf16 (BASELINE's dtype) whatever autocast region its caller has
+    open: the reference pipeline runs the slide encoder under torch.cuda.amp.autocast(fp16)
+    (pipeline.py:186-187), and autocast must not retarget the GEMMs that write into the bf16
+    workspaces (out=).  fp16 / fp32 inputs are converted to bf16 on entry; outputs keep the
+    model's parameter dtype (fp32), as the reference's autocast LayerNorm readout does."""
+    @functools.wraps(fn)
+    def wrapped(*args, **kw):
+        with torch.autocast("cuda", enabled=False):
+            return fn(*args, **kw)
+    return wrapped
 
 
 # ------------------------------------------------------------------------------------------

@@ -167,6 +167,7 @@ class LongNetViT(nn.Module):
         return self._top
 
     # ---------------------------------------------------------------- forward
+    @runtime.bf16_compute
     def forward(self, x, coords, all_layer_embed=False):
         """x [B, N, in_chans], coords [B, N, 2] (pixels) -> list of [B, E] slide embeddings:
         1 (final, after encoder.layer_norm) or, with all_layer_embed, 1 + depth (embedding and
@@ -259,6 +260,7 @@ class LongNetViT(nn.Module):
         return ent
 
     # ---------------------------------------------------------------- varlen packing (C5)
+    @runtime.bf16_compute
     def forward_packed(self, slides, all_layer_embed=False):
         """Several slides in ONE forward (config C5 "varlen segment packing").
 

@@ -47,6 +47,7 @@ class EncoderLayer(nn.Module):
         return DilatedAttention(args, embed_dim, args.encoder_attention_heads, dropout=args.attention_dropout,
                                 self_attention=True, subln=args.subln)
 
+    @runtime.bf16_compute
     def forward(self, x, encoder_padding_mask=None, attn_mask=None, rel_pos=None, multiway_split_position=None,
                 incremental_state=None):
         if self.training and (self.dropout > 0 or self.drop_path_prob > 0):
@@ -85,6 +86,7 @@ class Encoder(nn.Module):
         if self.training and (self.args.dropout > 0 or self.args.drop_path_rate > 0):
             raise RuntimeError("the MI355X slide encoder is inference-only: call model.eval()")
 
+    @runtime.bf16_compute
     def forward(self, src_tokens, encoder_padding_mask=None, attn_mask=None, return_all_hiddens=False,
                 token_embeddings=None, multiway_split_position=None, features_only=False,
                 incremental_state=None, positions=None, **kwargs):

@@ -46,6 +46,7 @@ class DilatedAttention(nn.Module):
             self._packed_sig = sig
         return self._packed
 
+    @runtime.bf16_compute
     def forward(self, query, key, value, incremental_state=None, key_padding_mask=None, attn_mask=None,
                 rel_pos=None, is_first_step=False, is_causal=False):
         if incremental_state is not None or is_causal or rel_pos is not None or attn_mask is not None:

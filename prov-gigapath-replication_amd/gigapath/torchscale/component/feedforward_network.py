@@ -24,6 +24,7 @@ class FeedForwardNetwork(nn.Module):
         self.fc2 = nn.Linear(ffn_dim, embed_dim)
         self.ffn_layernorm = nn.LayerNorm(ffn_dim, eps=layernorm_eps)
 
+    @runtime.bf16_compute
     def forward(self, x):
         if x.device.type != "cuda":
             raise RuntimeError("FeedForwardNetwork (MI355X path) needs ROCm device tensors")

@@ -190,5 +190,38 @@ def main():
     print("done %.1fs" % (time.time() - t0))
 
 
+def add_e2e(N, B=1):
+    """Append ONE end-to-end case (all_layer_embed and last output, fp32 reference) to the existing
+    golden set without regenerating the others:  python tests/golden/make_golden.py --e2e 16384
+    (config C2; ~1 min on 8 CPU threads)."""
+    t0 = time.time()
+    se, _, _ = ref_harness.load_reference()
+    arch = "gigapath_slide_enc12l768d"
+    cfg = orc.arch_config(arch)
+    with open(os.path.join(HERE, "golden_meta.json")) as f:
+        meta = json.load(f)
+    W = orc.make_weights(cfg, seed=0, perturb=True)
+    assert orc.weights_sha256(W) == meta["weights_sha256"]
+    model = se.create_model("", arch, 1536).eval()
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()}, strict=True)
+    x, coords = orc.synthetic_slide(N, B=B)
+    res = {"x_sha256": sha(x), "coords_sha256": sha(coords)}
+    with torch.no_grad():
+        xt, ct = torch.from_numpy(x), torch.from_numpy(coords)
+        t1 = time.time()
+        allv = torch.stack(model(xt, ct, all_layer_embed=True), 0).numpy()
+        res["sec_all_layer"] = time.time() - t1
+        last = model(xt, ct)[0].numpy()
+    save("e2e_N%d_B%d.npz" % (N, B), all_layer=allv, last=last)
+    res.update(N=N, B=B)
+    meta["e2e"] = [e for e in meta["e2e"] if not (e["N"] == N and e["B"] == B)] + [res]
+    with open(os.path.join(HERE, "golden_meta.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+    print("e2e", N, B, "done %.1fs" % (time.time() - t0))
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) == 3 and sys.argv[1] == "--e2e":
+        add_e2e(int(sys.argv[2]))
+    else:
+        main()

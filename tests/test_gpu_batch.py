@@ -185,3 +185,29 @@ def test_forward_packed_edge_cases():
                 _close(o, r)
         one = model.forward_packed(slides[1:2], all_layer_embed=False)
         _close(one[0][0], model(slides[1][0][None], slides[1][1][None])[0])
+
+
+@pytest.mark.timeout(600)
+def test_c5_full_mixed_batch_packed_matches_individual_forwards():
+    """Config C5 at its real size: the 32-slide batch of batch.mixed_batch_sizes() (2k-100k tiles,
+    675,587 in all) encoded by encode_slides (varlen-packed, one forward) == every slide's own B = 1
+    forward (GEMM row-count rounding aside), all 13 embeddings; the smallest slide also against the
+    fp32 oracle."""
+    sizes = batch.mixed_batch_sizes()
+    assert len(sizes) == 32 and sum(sizes) == 675587
+    model = _model()
+    slides = _slides(sizes, seed=200)
+    out = batch.encode_slides(model, slides, all_layer_embed=True)
+    assert len(out) == 32
+    with torch.no_grad():
+        for (x, c), o in zip(slides, out):
+            ref = model(x[None], c[None], all_layer_embed=True)
+            assert len(o) == len(ref) == 13
+            _close(torch.stack(o), torch.stack(ref))
+    i = int(np.argmin(sizes))
+    cfg = orc.arch_config("gigapath_slide_enc12l768d")
+    Wt = {k: torch.from_numpy(v) for k, v in orc.make_weights(cfg, seed=0).items()}
+    x, c = slides[i]
+    want = torch.stack(orc.slide_encoder_forward(Wt, x[None].cpu().numpy(), c[None].cpu().numpy(), cfg,
+                                                 all_layer_embed=True))
+    _close(torch.stack(out[i]).cpu(), want)

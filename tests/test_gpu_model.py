@@ -56,6 +56,52 @@ def test_end_to_end_vs_reference_golden(model, golden_meta, N, B):
             assert ok, (name, idx, rel, cos)
 
 
+def test_c2_16k_end_to_end_vs_reference_golden(model, golden_meta):
+    """Config C2 (16,384 tiles: 17 / 3 / 1 / 1 / 1 segments per branch) against the reference's own
+    fp32 output (make_golden.py --e2e 16384), all 13 embeddings and the default output, eager and
+    as a HIP-graph replay."""
+    g = load_golden("e2e_N16384_B1.npz")
+    x, coords = orc.synthetic_slide(16384)
+    xt, ct = torch.from_numpy(x).to(DEV), torch.from_numpy(coords).to(DEV)
+    with torch.no_grad():
+        allv = torch.stack(model(xt, ct, all_layer_embed=True)).cpu().numpy()
+        last = model(xt, ct)[0].cpu().numpy()
+        model.use_hip_graphs = True
+        try:
+            rep = torch.stack(model(xt, ct, all_layer_embed=True)).cpu().numpy()
+        finally:
+            model.use_hip_graphs = False
+            model._graphs.clear()
+            model._graph_ws.clear()
+    assert np.array_equal(rep, allv)
+    for name, got in (("all_layer", allv), ("last", last)):
+        ref = g[name]
+        assert got.shape == ref.shape
+        for idx in np.ndindex(*got.shape[:-1]):
+            rel, cos, ok = close_enough(got[idx], ref[idx])
+            assert ok, (name, idx, rel, cos)
+
+
+def test_fp16_autocast_caller_vs_reference_golden(model, golden_meta):
+    """The reference pipeline's call (pipeline.py:186-187): fp16 tile embeddings into
+    model(x, coords, all_layer_embed=True) inside torch.cuda.amp.autocast(dtype=torch.float16).
+    The MI355X path computes in bf16 regardless (runtime.bf16_compute) and returns
+    fp32 embeddings, within the model tolerance of the reference's fp32 golden."""
+    g = load_golden("e2e_N1024_B1.npz")
+    ent = [e for e in golden_meta["e2e"] if e["N"] == 1024 and e["B"] == 1][0]
+    x, coords = orc.synthetic_slide(1024)
+    xt, ct = torch.from_numpy(x).to(DEV).half(), torch.from_numpy(coords).to(DEV)
+    with torch.no_grad(), torch.cuda.amp.autocast(dtype=torch.float16):
+        out = model(xt, ct, all_layer_embed=True)
+        last = model(xt, ct)[0]
+    assert len(out) == 13 and all(o.dtype == torch.float32 for o in out) and last.dtype == torch.float32
+    allv = torch.stack(out).cpu().numpy()
+    for name, got in (("all_layer", allv), ("last", last.cpu().numpy())):
+        for idx in np.ndindex(*got.shape[:-1]):
+            rel, cos, ok = close_enough(got[idx], g[name][idx], ent.get("ref_bf16_rel_inf", 0.0))
+            assert ok, (name, idx, rel, cos)
+
+
 def test_bf16_error_not_worse_than_reference_bf16(model, golden_meta):
     """At N=1024 the reference's own bf16 run deviates from its fp32 run by ~1.4e-2; ours must
     be at least as close to the fp32 reference."""

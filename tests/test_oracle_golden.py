@@ -105,3 +105,18 @@ def test_end_to_end_golden(N, B, golden_meta):
     np.testing.assert_allclose(allv, g["all_layer"], rtol=0, atol=tol * np.abs(g["all_layer"]).max())
     np.testing.assert_allclose(last, g["last"], rtol=0, atol=tol * np.abs(g["last"]).max())
     np.testing.assert_allclose(gp, g["gp_last"], rtol=0, atol=tol * np.abs(g["gp_last"]).max())
+
+
+def test_end_to_end_golden_c2_16k(golden_meta):
+    """The oracle at config C2's size (16,384 tiles, multi-segment branches 0-1) against the
+    reference's own fp32 output: one all_layer_embed forward (~40 s on 8 threads)."""
+    N = 16384
+    g = load_golden("e2e_N%d_B1.npz" % N)
+    W = {k: torch.from_numpy(v) for k, v in orc.make_weights(CFG, seed=0).items()}
+    x, coords = orc.synthetic_slide(N)
+    ent = [e for e in golden_meta["e2e"] if e["N"] == N and e["B"] == 1][0]
+    assert sha(x) == ent["x_sha256"] and sha(coords) == ent["coords_sha256"]
+    torch.set_num_threads(min(8, torch.get_num_threads()))
+    with torch.no_grad():
+        allv = torch.stack(orc.slide_encoder_forward(W, x, coords, CFG, all_layer_embed=True)).numpy()
+    np.testing.assert_allclose(allv, g["all_layer"], rtol=0, atol=1e-4 * np.abs(g["all_layer"]).max())

@@ -13,6 +13,16 @@ import torch  # noqa: E402
 
 from gigapath import _hip, runtime  # noqa: E402
 
+def _lab_stamps():
+    import ctypes
+    out = (ctypes.c_int64 * 8)()
+    _hip._lib.gp_debug_attn_stamps(out, 1)
+    return list(out)
+
+
+# the run-time variant switches (GP_ATTN_IMPL / GP_ATTN_VAR / GP_GELU_IMPL) live in the lab build only
+_hip._lib = _hip.load_library(os.path.join(ROOT, "tools", "attn_lab", "liblab_r01.so"))
+
 ap = argparse.ArgumentParser()
 ap.add_argument("--L", type=int, default=70001)
 ap.add_argument("--iters", type=int, default=10)
@@ -57,7 +67,7 @@ for impl, (outs, lses) in first.items():
     dl = max(float((a - b).abs().max()) for a, b in zip(lses, first[ref_impl][1]))
     print("impl %s vs %s: max|d out| %.3g  max|d lse| %.3g" % (impl, ref_impl, do, dl))
 if any(i.endswith("@34818") for i in res):      # stamped build: cycles per segment per tile
-    st = _hip.debug_attn_stamps(reset=True)
+    st = _lab_stamps()
     names = ["S MFMAs", "softmax", "PV", "stage store", "barrier"]
     tiles = max(st[6], 1)
     print("stamps: %d waves, %d tiles, %.0f wave-cycles/tile; per tile: %s" % (

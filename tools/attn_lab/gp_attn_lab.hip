@@ -6,15 +6,15 @@
 //   * work item = (branch, batch*segment, head, 128-row q-block); items ordered heaviest
 //     branch first (LPT) and regrouped so that 8 consecutive q-blocks of one (segment, head)
 //     run on one XCD and share its L2 for K/V;
-//   * 4 waves x 32 query rows; K/V tiles of 64 keys staged in LDS, double buffered (one barrier
-//     per tile).  The dilated gather is folded into the addressing: sparse row i of (segment n,
-//     head h) is token n*s + i*r + h/(Hp/r);
-//   * D = 48 / 64 (v2 kernel, dilated_attn32_kernel): S^T = K.Q^T and O^T += V^T.P^T with
-//     v_mfma_f32_32x32x16_bf16; D = 96 (dilated_attn_kernel): v_mfma_f32_16x16x32_bf16;
+//   * 4 waves x 32 query rows; K/V tiles of 64 keys are register-staged into LDS, double
+//     buffered (one barrier per tile).  The dilated gather is folded into the addressing:
+//     sparse row i of (segment n, head h) is token n*s + i*r + h/(Hp/r);
+//   * S^T = K.Q^T with v_mfma_f32_16x16x32_bf16 (D padded to 32*KS with zero Q lanes), so
+//     each lane owns one query's scores: softmax needs only 2 cross-lane max steps per tile;
+//   * O^T += V^T.P^T with the same MFMA: P is taken straight from the S accumulators (no lane
+//     movement), V^T fragments come from ds_read_b64_tr_b16 on the row-major V tile;
 //   * the reference's zero-padded keys (dilated_attention.py:85-91, unmasked in flash-attn)
 //     are added analytically at the end: n_pad * exp(0 - max) in the denominator.
-// Every launch configuration is fixed at compile time (no run-time variant switches); measured
-// alternatives live in tools/attn_lab/ (a separate build target).
 #include <math.h>
 #include <type_traits>
 #include <stdlib.h>
@@ -390,51 +390,85 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 GP_DEV float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// Diagnostic in-kernel cycle stamps (VAR & 32768 builds only; read with gp_debug_attn_stamps):
+// per wave, cycles spent between fixed points of each tile, summed over all waves.
+__device__ unsigned long long g_attn_stamps[8];
+GP_DEV unsigned long long stamp_now() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+
 // lse bit pattern (a quiet NaN no real row produces) that flags a row for the fixup pass
 constexpr uint32_t kLseRedo = 0x7fc0dead;
 
-// Three builds of the v2 kernel (all 4 waves x 32 queries, 64-key K/V tiles, one barrier per tile):
-//   kModeFast (D = 48, q pre-scaled by D^-0.5*log2 e; the product launch): K/V tiles staged by
-//     LDS-DMA (buffer_load ... lds, 1 KiB per wave-instruction, lane-linear) straight into the
-//     padded K image and the swizzled V image through a per-tile buffer descriptor whose record
-//     count ends at the last valid key row (rows past c read as zero in hardware); tile loop
-//     unrolled by two so each tile's LDS buffer is a compile-time constant; NO row max and NO
-//     offset: S starts from C = 0 and p = exp2(s).  Valid while a row's real-key sum l stays in
-//     [2^-100, 2^100]; outside it (or not finite) the row's lse gets the kLseRedo marker;
-//   kModeFix: the exact kernel run right after kModeFast on the same stream (the fixup pass):
-//     kFixItems work items per block, the block reads the lse of every row of all of them and
-//     exits unless one holds the marker, else recomputes the flagged items with a running row
-//     max (tile 0 sets it exactly; lazy rescale when a row's max grows by > kThr log2 units),
-//     the -m start block of S from one extra MFMA of an exact hi + lo bf16 pair;
-//   kModeGen (D = 48 / 64, q pre-scaled or not): the same exact arithmetic with register-staged
-//     K/V tiles (global loads, addresses computed once), for k / v layouts the descriptor cannot
-//     cover (the operator seam's separate q / k / v tensors) and for D = 64.
-enum AttnMode { kModeFast = 0, kModeFix = 1, kModeGen = 2 };
-constexpr int kFixItems = 32;
-
-template <int D, bool kPre, int MODE, bool kTab>
+// VAR bits (A/B variants, all numerically identical): 1 = S's first k-step takes its C operand
+// from a persistent -m_run block (no per-tile accumulator init), 2 = staging addresses computed
+// once (no per-tile 64-bit index math, no bound checks on full tiles), 4 = all K fragments read
+// before the S MFMAs, 8 = the running max rides in a 4th k-step of S (D = 48, kPre): K image
+// column 48 holds 1.0, Q column 48 holds -m (m kept bf16-exact), so S arrives already shifted
+// with no per-tile accumulator initialisation and no extra registers (2 more MFMAs per tile,
+// ~17 fewer VALU).  OCC = waves per SIMD the register budget must allow.
+template <int D, bool kPre, int NW, int VAR = 0, int OCC = 2, bool kTab = false>
 __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_idx) {
   static_assert(D == 48 || D == 64, "v2 kernel covers D = 48 and 64");
-  static_assert(MODE == kModeGen || (D == 48 && kPre), "LDS-DMA modes need D = 48 and a pre-scaled q");
-  constexpr int NT = 256;                    // 4 waves
-  constexpr int QB = 128;                    // query rows per workgroup
-  constexpr int KT = 64;                     // keys per staged tile
+  static_assert(NW == 4 || NW == 8, "");
+  constexpr int NT = NW * 64;                // threads
+  constexpr int QB = NW * 32;                // query rows per workgroup
+  // keys per staged tile: 16*NW (3 chunks / thread), or 64 with VAR & 512 (8 waves sharing one
+  // 64-key tile: 256 queries per K/V load)
+  constexpr int KT = ((VAR & 512) != 0) ? 64 : 16 * NW;
   constexpr int KS = D / 16;                 // k-steps of Q.K^T
   constexpr bool kOnes = (D % 32) != 0;      // spare d rows carry the row-sum ones
-  constexpr bool kDMA = MODE != kModeGen;
-  constexpr bool kZM = MODE == kModeFast;    // no max, no offset
-  constexpr bool kMI = MODE == kModeFix;     // -m start block from one MFMA
-  constexpr int KROWB = D * 2 + 16;          // K image row bytes (padded)
+  constexpr bool kMK = (VAR & 8) != 0;       // running max in an extra k-step
+  static_assert(!kMK || (D == 48 && kPre), "VAR 8 needs D = 48 and a pre-scaled q");
+  constexpr int KSS = kMK ? KS + 1 : KS;     // k-steps of S
+  // VAR & 4096: the -m_run start block of S comes from ONE extra MFMA per 64-key sub-tile,
+  // [1, 0 ...] (A) x [-m_run, 0 ...] (B) with C = 0, instead of 16 v_mov per sub-tile (the loop
+  // is VALU-issue bound; the MFMA pipe has slack); m_run kept bf16-exact as with VAR 8
+  constexpr bool kMI = (VAR & 4096) != 0;
+  // VAR & 262144: no per-tile row max after the first 64 keys.  Tile 0 sets m_run to its exact max;
+  // later tiles only watch the running row sum l (the ones row of O, exact bookkeeping of
+  // sum exp2(s - m_run)) and renormalise when l > 2^24 (m_run += log2 l, so m_run stays within
+  // log2(c) of the true running max and no p can underflow against it).  A later key more than
+  // ~127 log2 units above the running max would overflow exp2: every query's final l is checked,
+  // a query whose l is not finite gets an lse marker (kLseRedo) and the fixup launch (VAR &
+  // 524288, the exact per-tile-max kernel, run right after on the same stream) recomputes every
+  // block holding a marker and exits at once elsewhere.
+  constexpr bool kNM = (VAR & 262144) != 0;
+  // VAR & 1048576 (with 262144): no offset at all -- S starts from C = 0 (no init MFMA, m = 0), so
+  // p = exp2(s) of the pre-scaled log2-domain score; no max, no renormalisation.  Valid while the
+  // real-key row sum l stays in [2^-100, 2^100] (every p then keeps full bf16 precision relative to
+  // the largest); outside it (or non-finite) the row gets the lse marker and the exact fixup pass
+  // recomputes its block.  With zero-pad keys (npad > 0) a tiny l is not flagged: the pads (p = 1)
+  // then dominate exactly as in the reference.
+  constexpr bool kZM = (VAR & 1048576) != 0;
+  static_assert(!kZM || kNM, "VAR 1048576 builds on VAR 262144");
+  constexpr bool kFix = (VAR & 524288) != 0;
+  static_assert(!(kNM && kFix), "the fixup pass is the exact kernel");
+  static_assert(!kMI || (D == 48 && kPre && !kMK && (VAR & 1) == 0), "VAR 4096 needs D = 48, kPre, no VAR 8/1");
+  constexpr int KROWB = (kMK ? 64 : D) * 2 + 16;   // K image row bytes (padded)
   constexpr int VROWB = 128;                 // V image row bytes (64 bf16, swizzled 32-B blocks)
   constexpr int KTILE = KT * KROWB;
   constexpr int VTILE = KT * VROWB;
   constexpr int BUF = KTILE + VTILE;
   constexpr int CH = D / 8;                  // 16-byte chunks per K/V row in HBM
   constexpr int TOT = 2 * KT * CH;           // 16-byte chunks of one K tile + one V tile
-  constexpr int LPT = TOT / NT;
-  static_assert(TOT % NT == 0, "");
+  constexpr int LPT = (TOT + NT - 1) / NT;
+  static_assert(TOT % NT == 0 || (VAR & 2) != 0, "uneven chunk split needs VAR & 2");
   constexpr float kThr = 8.0f;               // lazy-rescale threshold (log2 units)
-  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  // VAR & 131072: the two tile buffers are two distinct LDS objects (each selected at compile time
+  // by the unrolled loop), so the LDS lowering gives them distinct alias scopes and the wait
+  // insertion no longer orders this tile's LDS reads after the next tile's in-flight LDS-DMA
+  constexpr bool kTwo = (VAR & 131072) != 0;
+  __shared__ __attribute__((aligned(16))) char smem[kTwo ? BUF : 2 * BUF];
+  __shared__ __attribute__((aligned(16))) char smem_b[kTwo ? BUF : 16];
+  auto bufp_of = [&](int b) -> char* {
+    if constexpr (kTwo) return b ? smem_b : smem;
+    else return smem + b * BUF;
+  };
 
   // ---- work item (32-bit index math: items < 2^31, checked on the host)
   WorkItem wi;
@@ -447,9 +481,8 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   const int rows_needed = wi.i_hi;
   const int q0 = wi.i_lo + wi.qb * QB;
   if (q0 >= rows_needed) return;
-  // rows >= c are zero-padded queries (their q is 0): load nothing for them
-  const int qvalid = c < rows_needed ? c : rows_needed;
-  if constexpr (MODE == kModeFix) {          // only blocks the fast kernel flagged are recomputed
+  const int qvalid = c < rows_needed ? c : rows_needed;   // see dilated_attn_kernel
+  if constexpr (kFix) {      // fixup pass: only blocks the kNM kernel flagged are recomputed
     const int i = q0 + (int)threadIdx.x;
     bool flagged = false;
     if (threadIdx.x < QB && i < rows_needed)
@@ -468,17 +501,26 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   const uint16_t* kbase = brr.k + (tok0 - brr.kv_tok_base) * brr.kv_stride + kcol;
   const uint16_t* vbase = brr.v + (tok0 - brr.kv_tok_base) * brr.kv_stride + kcol;
 
+  if constexpr (kMK) {   // K image columns 48..63: [1, 0 x 15] (never overwritten by staging)
+    for (int idx = threadIdx.x; idx < 2 * KT * 2; idx += NT) {   // 2 bufs x KT rows x 2 chunks
+      const int buf = idx / (2 * KT), rem = idx % (2 * KT), row = rem >> 1, half = rem & 1;
+      const uint4 col = half ? make_uint4(0, 0, 0, 0) : make_uint4(0x3F80u, 0, 0, 0);
+      *reinterpret_cast<uint4*>(bufp_of(buf) + row * KROWB + 96 + 16 * half) = col;
+    }
+  }
   // V images: the d-columns >= D of every row (block 3 for D = 48) hold bf16 1.0
   if constexpr (kOnes) {
     for (int idx = threadIdx.x; idx < 2 * KT * 2; idx += NT) {   // 2 bufs x KT rows x 2 chunks
       const int buf = idx / (2 * KT), rem = idx % (2 * KT), row = rem >> 1, half = rem & 1;
       const uint4 ones = make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
-      *reinterpret_cast<uint4*>(smem + buf * BUF + KTILE + row * VROWB + 32 * (3 ^ (row & 3)) + 16 * half) = ones;
+      *reinterpret_cast<uint4*>(bufp_of(buf) + KTILE + row * VROWB + 32 * (3 ^ (row & 3)) + 16 * half) = ones;
     }
   }
 
-  // Q fragments (B operand): lane holds Q[q = l32][d = 16ks + 8h .. +7]
-  bf16x8 qf[KS];
+  // Q fragments (B operand): lane holds Q[q = l32][d = 16ks + 8h .. +7]; with kMK, qf[KS] is
+  // [-m, 0 x 7] on h = 0 lanes and zeros on h = 1 lanes
+  bf16x8 qf[KSS];
+  if constexpr (kMK) qf[KS] = bf16x8{};
   {
     const int i = q0 + w * 32 + l32;
 #pragma unroll
@@ -489,16 +531,45 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
     }
   }
 
-  // ---- K/V staging
-  const int64_t kv_dv = (int64_t)((const char*)vbase - (const char*)kbase);   // V row = K row + kv_dv bytes
-  // kModeGen: per-thread staging chunks (source of key 0, row, LDS offset), computed once
+  uint4 stage[LPT];
+  // VAR & 2: per-thread staging chunks (source of key 0, row, LDS offset) computed once
   const uint16_t* lsrc[LPT];
   int lrow[LPT], loff[LPT];
-  uint4 stage[LPT];
-  // kDMA: piece p of the 15 (7 K + 8 V) goes to wave p % 4; lane-linear 16-B units.  K image:
-  // 112-B rows = 6 chunks + 1 pad unit (pad lanes off); V image: 128-B rows, swizzled 32-B blocks
-  // (the lanes of the bf16-ones block are off: the prologue wrote it)
-  constexpr int kPieces = (KT * KROWB + KT * VROWB) / 1024;
+  if constexpr ((VAR & 2) != 0) {
+#pragma unroll
+    for (int u = 0; u < LPT; ++u) {
+      const int idx = (threadIdx.x + NT * u) % TOT;   // (an out-of-range chunk repeats a valid one)
+      const int tsel = idx / (KT * CH);
+      const int rem = idx % (KT * CH);
+      const int row = rem / CH, ch = rem % CH;
+      lsrc[u] = (tsel ? vbase : kbase) + (int64_t)row * kvstride + ch * 8;
+      lrow[u] = row;
+      loff[u] = tsel ? KTILE + row * VROWB + 32 * ((ch >> 1) ^ (row & 3)) + 16 * (ch & 1) : row * KROWB + ch * 16;
+    }
+  }
+  // VAR & 2048: byte offset of every staging chunk from the K row of key 0 (V chunks at kv_dv)
+  const int64_t kv_dv = (int64_t)((const char*)vbase - (const char*)kbase);
+  int lvo[LPT];
+  if constexpr ((VAR & 2048) != 0) {
+#pragma unroll
+    for (int u = 0; u < LPT; ++u) {
+      const int idx = (threadIdx.x + NT * u) % TOT;
+      const int tsel = idx / (KT * CH);
+      const int rem = idx % (KT * CH);
+      lvo[u] = (int)(tsel * kv_dv + (int64_t)(rem / CH) * kvstride * 2 + (rem % CH) * 16);
+    }
+  }
+  // VAR & 8192: LDS-DMA staging -- buffer_load ... lds writes each 1 KiB piece (64 lanes x 16 B,
+  // lane-linear) straight into the tile image: no stage registers, no ds_write pass.  K image:
+  // 7 pieces (112-B rows = 6 chunks + 1 pad unit, pad lanes off); V image: 8 pieces (128-B
+  // rows, swizzled 32-B blocks; the lanes of the bf16-ones block are off, the prologue wrote
+  // it).  Piece p of the 15 goes to wave p % 4.
+  constexpr bool kDMA = (VAR & 8192) != 0;
+  static_assert(!kNM || (kMI && kOnes), "VAR 262144 needs VAR 4096 (D = 48)");
+  static_assert(!kTwo || (kDMA && (VAR & 65536) != 0), "VAR 131072 needs VAR 8192 + 65536");
+  static_assert(!kDMA || (D == 48 && NW == 4 && KT == 64 && (VAR & 2048) != 0 && !kMK),
+                "VAR 8192 needs D = 48, 4 waves, 64-key tiles and VAR 2048");
+  constexpr int kPieces = (KT * KROWB + KT * VROWB) / 1024;      // 15
   int dvo[4];
   unsigned dmask = 0;
   if constexpr (kDMA) {
@@ -518,25 +589,14 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
         if (b < 3) dmask |= 1u << sl;
       }
     }
-  } else {
-#pragma unroll
-    for (int u = 0; u < LPT; ++u) {
-      const int idx = threadIdx.x + NT * u;
-      const int tsel = idx / (KT * CH);
-      const int rem = idx % (KT * CH);
-      const int row = rem / CH, ch = rem % CH;
-      lsrc[u] = (tsel ? vbase : kbase) + (int64_t)row * kvstride + ch * 8;
-      lrow[u] = row;
-      loff[u] = tsel ? KTILE + row * VROWB + 32 * ((ch >> 1) ^ (row & 3)) + 16 * (ch & 1) : row * KROWB + ch * 16;
-    }
   }
-  auto load_tile = [&](int kv0) {
+  auto load_tile = [&](int kv0, int nbuf = -1) {
     if constexpr (kDMA) {
       const int64_t tb = (int64_t)kv0 * kvstride * 2;
       const int64_t nrec = (int64_t)(c - kv0 - 1) * kvstride * 2 + kv_dv + 2 * D;
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
           (void*)((const char*)kbase + tb), (short)0, (int)(nrec < 0x7fffffff ? nrec : 0x7fffffff), 0x00020000);
-      char* bufp = smem + ((kv0 / KT) & 1) * BUF;
+      char* bufp = (kTwo && nbuf >= 0) ? bufp_of(nbuf) : bufp_of((kv0 / KT) & 1);
 #pragma unroll
       for (int sl = 0; sl < 4; ++sl) {
         const int pc = w + 4 * sl;
@@ -545,34 +605,75 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
               rs, (__attribute__((address_space(3))) void*)(bufp + (pc < KTILE / 1024 ? pc * 1024 : KTILE + (pc - KTILE / 1024) * 1024)),
               16, dvo[sl], 0, 0, 0);
       }
-    } else {
+    } else if constexpr ((VAR & 2048) != 0) {
+      // buffer loads through a per-tile descriptor whose record count ends at the last valid key
+      // row: rows past c read as zero in hardware (no branch, no zero-filled stage registers,
+      // so the compiler has no reason to wait on the loads before the tile's compute)
+      const int64_t tb = (int64_t)kv0 * kvstride * 2;                    // bytes, wave-uniform
+      const int64_t nrec = (int64_t)(c - kv0 - 1) * kvstride * 2 + kv_dv + 2 * D;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)((const char*)kbase + tb), (short)0, (int)(nrec < 0x7fffffff ? nrec : 0x7fffffff), 0x00020000);
+#pragma unroll
+      for (int u = 0; u < LPT; ++u)
+        if (TOT % NT == 0 || threadIdx.x + NT * u < TOT)
+          stage[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, lvo[u], 0, 0));
+    } else if constexpr ((VAR & 2) != 0) {
       const int64_t toff = (int64_t)kv0 * kvstride;      // wave-uniform
       if (kv0 + KT <= c) {                                // full tile: no per-key bound checks
 #pragma unroll
-        for (int u = 0; u < LPT; ++u) stage[u] = *reinterpret_cast<const uint4*>(lsrc[u] + toff);
+        for (int u = 0; u < LPT; ++u)
+          if (TOT % NT == 0 || threadIdx.x + NT * u < TOT) stage[u] = *reinterpret_cast<const uint4*>(lsrc[u] + toff);
       } else {
 #pragma unroll
         for (int u = 0; u < LPT; ++u) {
           uint4 z = make_uint4(0, 0, 0, 0);
-          if (kv0 + lrow[u] < c) z = *reinterpret_cast<const uint4*>(lsrc[u] + toff);
+          if (kv0 + lrow[u] < c && (TOT % NT == 0 || threadIdx.x + NT * u < TOT))
+            z = *reinterpret_cast<const uint4*>(lsrc[u] + toff);
           stage[u] = z;
         }
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < LPT; ++u) {
+        const int idx = threadIdx.x + NT * u;
+        const int tsel = idx / (KT * CH);
+        const int rem = idx % (KT * CH);
+        const int row = rem / CH, ch = rem % CH;
+        const int key = kv0 + row;
+        uint4 z = make_uint4(0, 0, 0, 0);
+        if (key < c) z = *reinterpret_cast<const uint4*>((tsel ? vbase : kbase) + (int64_t)key * kvstride + ch * 8);
+        stage[u] = z;
       }
     }
   };
   auto store_tile = [&](int buf) {
-    if constexpr (!kDMA) {
+    if constexpr (kDMA) return;
 #pragma unroll
-      for (int u = 0; u < LPT; ++u) *reinterpret_cast<uint4*>(smem + buf * BUF + loff[u]) = stage[u];
+    for (int u = 0; u < LPT; ++u) {
+      int off;
+      if constexpr ((VAR & 2) != 0) {
+        if (TOT % NT != 0 && threadIdx.x + NT * u >= TOT) continue;
+        off = loff[u];
+      } else {
+        const int idx = threadIdx.x + NT * u;
+        const int tsel = idx / (KT * CH);
+        const int rem = idx % (KT * CH);
+        const int row = rem / CH, ch = rem % CH;
+        off = tsel ? KTILE + row * VROWB + 32 * ((ch >> 1) ^ (row & 3)) + 16 * (ch & 1) : row * KROWB + ch * 16;
+      }
+      *reinterpret_cast<uint4*>(bufp_of(buf) + off) = stage[u];
     }
   };
 
-  bf16x8 onesA = {}, mqB = {};    // kMI operands: [1, 1, 0 ...] x [hi, lo, 0 ...] = -m_run
+  bf16x8 onesA = {}, mqB = {};    // kMI operands
   if constexpr (kMI) {
     if (h == 0) { onesA[0] = (__bf16)1.0f; onesA[1] = (__bf16)1.0f; }
   }
   float m_run = -INFINITY;   // running max, log2 domain, of query l32
   float lsum = 0.f;          // row sum (VALU path, D % 32 == 0 only)
+  f32x16 minit;              // kPre: -m_run (0 before the first tile); else 0
+#pragma unroll
+  for (int r = 0; r < 16; ++r) minit[r] = 0.f;
   f32x16 oacc[2];
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt)
@@ -580,9 +681,48 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
     for (int r = 0; r < 16; ++r) oacc[mt][r] = 0.f;
 
   const int ntiles = (c + KT - 1) / KT;
+  // kTwo: the lane part of each V^T fragment offset (row & 3 does not depend on the sub-tile),
+  // made opaque so the reads stay one GEP from their LDS object -- the LDS lowering tags an access
+  // with its object's alias scope only a few GEPs deep, and an untagged read waits on every DMA
+  int vlane[2];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+    const int rl = 4 * (lane >> 5) + ((lane >> 2) & 3);
+    vlane[mt] = rl * VROWB + 32 * ((2 * mt + ((lane >> 4) & 1)) ^ (rl & 3)) + 8 * (lane & 3);
+    if constexpr (kTwo) asm volatile("" : "+v"(vlane[mt]));
+  }
+  // VAR & 1024: prefetch distance 2 -- two register stage sets (tile t+2 loads while tile t+1
+  // waits in the other set), the loop unrolled by 2 so each set is a compile-time choice
+  constexpr bool kPF2 = (VAR & 1024) != 0;
+  static_assert(!kPF2 || (VAR & 2) != 0, "VAR 1024 builds on VAR 2");
+  static_assert((VAR & 2048) == 0 || (VAR & 2) != 0, "VAR 2048 builds on VAR 2");
+  uint4 stage2[kPF2 ? 2 : 1][LPT];
+  auto load_into = [&](uint4 (&st)[LPT], int kv0) {
+    const int64_t toff = (int64_t)kv0 * kvstride;
+#pragma unroll
+    for (int u = 0; u < LPT; ++u) {
+      uint4 z = make_uint4(0, 0, 0, 0);
+      if (kv0 + lrow[u] < c && (TOT % NT == 0 || threadIdx.x + NT * u < TOT))
+        z = *reinterpret_cast<const uint4*>(lsrc[u] + toff);
+      st[u] = z;
+    }
+  };
+  auto store_from = [&](const uint4 (&st)[LPT], int buf) {
+#pragma unroll
+    for (int u = 0; u < LPT; ++u) {
+      if (TOT % NT != 0 && threadIdx.x + NT * u >= TOT) continue;
+      *reinterpret_cast<uint4*>(bufp_of(buf) + loff[u]) = st[u];
+    }
+  };
   if (ntiles > 0) {
-    load_tile(0);
-    store_tile(0);
+    if constexpr (kPF2) {
+      load_into(stage2[0], 0);
+      store_from(stage2[0], 0);
+      if (ntiles > 1) load_into(stage2[1], KT);
+    } else {
+      load_tile(0);
+      store_tile(0);
+    }
   }
   __syncthreads();
   // every vector load so far (Q fragments, tile 0) is complete here; saying so with a real
@@ -591,184 +731,317 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   // prefetch -- before the first MFMA of every tile
   __builtin_amdgcn_s_waitcnt(0x0f70);
 
-  // one 64-key tile; SET = the tile's LDS buffer when the loop is unrolled by two (kDMA), so the
-  // buffer offsets fold into the ds_read immediates
+  constexpr bool kStamp = (VAR & 32768) != 0;
+  unsigned long long sacc_t[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long t_prev = 0;
+  auto mark = [&](int seg) {
+    if constexpr (kStamp) {
+      const unsigned long long now = stamp_now();
+      if (seg >= 0) sacc_t[seg] += now - t_prev;
+      t_prev = now;
+    }
+  };
+  const unsigned long long t_kernel0 = kStamp ? stamp_now() : 0;
   auto tile_step = [&](int t, auto setc) {
     constexpr int SET = decltype(setc)::value;
-    if (t + 1 < ntiles) load_tile((t + 1) * KT);
-    const int kv0 = t * KT;
-    const int bsel = kDMA ? SET : (t & 1);
-    const char* Kb = smem + bsel * BUF;
-    const char* Vb = smem + bsel * BUF + KTILE;
-    // ---- S^T for two 32-key sub-tiles.  kPre (q pre-multiplied by scale*log2 e): the
-    // accumulator starts at -m_run, so it already holds log2-domain scores minus the max.
-    f32x16 sacc[2];
-    f32x16 ini;
-    if constexpr (kMI) {
-      f32x16 zero;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) zero[r] = 0.f;
-      ini = __builtin_amdgcn_mfma_f32_32x32x16_bf16(onesA, mqB, zero, 0, 0, 0);
+    (void)SET;
+    mark(-1);
+    // VAR 128/256/64: timing-only ablations (wrong results): no K/V streaming after tile 0 /
+    // no barrier / no exp
+    if constexpr (kPF2) {
+      if (t + 2 < ntiles) load_into(stage2[SET], (t + 2) * KT);
+    } else if constexpr ((VAR & 16384) == 0) {
+      if (t + 1 < ntiles && (VAR & 128) == 0) load_tile((t + 1) * KT, 1 - SET);
     }
-    const float init = (kPre && !kZM && !kMI && t > 0) ? -m_run : 0.f;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      f32x16 acc;
-      if constexpr (kMI) {
-        acc = ini;
-      } else {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[r] = init;
+    for (int hf = 0; hf < KT / 64; ++hf) {
+      // 64-key sub-tile; a sub-tile past c (only in the last tile) is fully masked: p = 0
+      const int sub = t * (KT / 64) + hf;
+      const int kv0 = sub * 64;
+      // VAR & 65536: loop unrolled by two, so the buffer is the compile-time SET (LDS offsets fold
+      // into the ds_read immediates instead of a per-tile v_add)
+      constexpr bool kU2 = (VAR & 65536) != 0;
+      const int bsel = ((VAR & 128) != 0) ? 0 : (kU2 ? SET : (t & 1));
+      const char* Kb = bufp_of(bsel) + hf * 64 * KROWB;
+      const char* Vb = bufp_of(bsel) + KTILE + hf * 64 * VROWB;
+      // ---- S^T for two 32-key sub-tiles.  kPre (q pre-multiplied by scale*log2 e): the
+      // accumulator starts at -m_run, so it already holds log2-domain scores minus the max.
+      f32x16 sacc[2];
+      // VAR & 1: the first k-step takes its C operand from minit (= -m_run in every element, kept
+      // in its own registers, rewritten only on a rescale) instead of initialising per tile
+      const float init = (kPre && sub > 0) ? -m_run : 0.f;
+      f32x16 ini;
+      if constexpr (kMI && !kZM) {
+        f32x16 zero;
+  #pragma unroll
+        for (int r = 0; r < 16; ++r) zero[r] = 0.f;
+        ini = __builtin_amdgcn_mfma_f32_32x32x16_bf16(onesA, mqB, zero, 0, 0, 0);
       }
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const bf16x8 kk = *reinterpret_cast<const bf16x8*>(Kb + (32 * u + l32) * KROWB + 32 * ks + 16 * h);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kk, qf[ks], acc, 0, 0, 0);
+      bf16x8 kf[2][KSS];
+      if constexpr ((VAR & 4) != 0) {      // all K fragments first: one LDS wait, not one per MFMA
+  #pragma unroll
+        for (int u = 0; u < 2; ++u)
+  #pragma unroll
+          for (int ks = 0; ks < KSS; ++ks)
+            kf[u][ks] = *reinterpret_cast<const bf16x8*>(Kb + (32 * u + l32) * KROWB + 32 * ks + 16 * h);
       }
-      sacc[u] = acc;
-    }
-    if (kv0 + 64 > c) {      // keys >= c are zero pads (added analytically at the end)
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (kv0 + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * h >= c) sacc[u][r] = -INFINITY;
-    }
+      if constexpr ((VAR & 32) != 0) __builtin_amdgcn_s_setprio(1);
+  #pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        f32x16 acc;
+        if constexpr (kZM) {
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+        } else if constexpr (kMI) {
+          acc = ini;
+        } else if constexpr (kMK) {
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+        } else if constexpr ((VAR & 1) == 0) {
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) acc[r] = init;
+        }
+  #pragma unroll
+        for (int ks = 0; ks < KSS; ++ks) {
+          bf16x8 kk;
+          if constexpr ((VAR & 4) != 0) kk = kf[u][ks];
+          else kk = *reinterpret_cast<const bf16x8*>(Kb + (32 * u + l32) * KROWB + 32 * ks + 16 * h);
+          if constexpr ((VAR & 1) != 0 && !kMK)
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kk, qf[ks], ks == 0 ? minit : acc, 0, 0, 0);
+          else
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kk, qf[ks], acc, 0, 0, 0);
+        }
+        sacc[u] = acc;
+      }
+      if constexpr ((VAR & 32) != 0) __builtin_amdgcn_s_setprio(0);
+      mark(0);                 // S MFMAs issued (K fragment reads waited)
+      if (kv0 + 64 > c) {      // keys >= c are zero pads (added analytically at the end)
+        // (the -inf below also holds for the kPre accumulator offset)
+  #pragma unroll
+        for (int u = 0; u < 2; ++u)
+  #pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (kv0 + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * h >= c) sacc[u][r] = -INFINITY;
+      }
 
-    // ---- online softmax with deferred rescale (two independent max chains)
-    float mx = 0.f;
-    if constexpr (!kZM) {
+      // ---- online softmax with deferred rescale (two independent max chains)
+      const bool do_max = !kZM && (!kNM || sub == 0);
+      float mx = 0.f;
+      if (do_max) {
       float mxa = sacc[0][0], mxb = sacc[1][0];
-#pragma unroll
+  #pragma unroll
       for (int r = 1; r < 16; ++r) {
         mxa = fmaxf(mxa, sacc[0][r]);
         mxb = fmaxf(mxb, sacc[1][r]);
       }
       mx = fmaxf(mxa, mxb);
-      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-      mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
-    }
-    bf16x8 pf[2][2];
-    if constexpr (kPre) {
-      if constexpr (!kZM) {
-        // scores are s*c - m_run; rescale only when a query's max moved up by > kThr
-        // (tile 0: always, which sets m_run to that tile's exact max)
-        const bool need = (t == 0) || (mx > kThr);
-        if (__builtin_amdgcn_ballot_w64(need)) {
-          if constexpr (kMI) {
-            // m kept as an exact hi + lo pair of bf16 values (two rows of the init MFMA), so it
-            // tracks the max to ~2^-16 relative and numerator and denominator stay consistent
-            const float m_old = (t == 0) ? 0.f : m_run;
-            float m_new = m_old;
-            if (need) {
-              const float tt = -(m_old + mx);
+      {
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+        mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+      }
+      }
+      bf16x8 pf[2][2];
+      if constexpr (kNM && !kZM) {
+        if (!do_max) {
+          // l of the tiles so far (the ones row); renormalise when it grew past 2^24
+          const float lc = oacc[1][8];
+          const bool big = lc > 0x1p24f && (__float_as_uint(lc) & 0x7f800000u) != 0x7f800000u;
+          if (__builtin_amdgcn_ballot_w64(big)) {
+            float m_new = m_run;
+            if (big) {
+              const float tt = -(m_run + __builtin_amdgcn_logf(lc));
               const __bf16 hi = (__bf16)tt;
               const __bf16 lo = (__bf16)(tt - (float)hi);
               m_new = -((float)hi + (float)lo);
             }
-            const float d = m_new - m_old;
-            if (t > 0) {
-              const float alpha = fast_exp2(-d);
-#pragma unroll
-              for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) oacc[mt][r] *= alpha;
-              lsum *= alpha;
-            }
+            const float d = m_new - m_run;
+            const float alpha = fast_exp2(-d);
+  #pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+  #pragma unroll
+              for (int r = 0; r < 16; ++r) oacc[mt][r] *= alpha;
             m_run = m_new;
-#pragma unroll
+  #pragma unroll
             for (int u = 0; u < 2; ++u)
-#pragma unroll
+  #pragma unroll
               for (int r = 0; r < 16; ++r) sacc[u][r] -= d;
             if (h == 0) {
               const __bf16 hi = (__bf16)(-m_run);
               mqB[0] = hi;
               mqB[1] = (__bf16)(-m_run - (float)hi);
             }
-          } else {
-            const float delta = need ? mx : 0.f;
-            const float alpha = fast_exp2(-delta);
-            if (t > 0) {
-#pragma unroll
+          }
+        }
+      }
+      if constexpr (kPre) {
+        // scores are s*c - m_run; rescale only when a query's max moved up by > kThr
+        // (tile 0: always, which sets m_run to that tile's exact max)
+        const bool need = do_max && ((sub == 0) || (mx > kThr));
+        if (__builtin_amdgcn_ballot_w64(need)) {
+          if constexpr (kMK || kMI) {
+            // m stays exactly representable in bf16 (it enters the MFMA through q); the shift
+            // applied is the rounded one, so numerator and denominator stay consistent
+            const float m_old = (sub == 0) ? 0.f : m_run;
+            // kMK: m kept bf16-exact; kMI: m kept as an exact hi + lo pair of bf16 values (two rows of
+            // the init MFMA), so it tracks the max to ~2^-16 relative and the bookkeeping stays exact
+            float m_new = m_old;
+            if (need) {
+              if constexpr (kMI) {
+                const float tt = -(m_old + mx);
+                const __bf16 hi = (__bf16)tt;
+                const __bf16 lo = (__bf16)(tt - (float)hi);
+                m_new = -((float)hi + (float)lo);
+              } else {
+                m_new = (float)(__bf16)(m_old + mx);
+              }
+            }
+            const float d = m_new - m_old;
+            if (sub > 0) {
+              const float alpha = fast_exp2(-d);
+  #pragma unroll
               for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
+  #pragma unroll
                 for (int r = 0; r < 16; ++r) oacc[mt][r] *= alpha;
               lsum *= alpha;
             }
-            m_run = (t == 0) ? delta : m_run + delta;
-#pragma unroll
+            m_run = m_new;
+  #pragma unroll
             for (int u = 0; u < 2; ++u)
-#pragma unroll
+  #pragma unroll
+              for (int r = 0; r < 16; ++r) sacc[u][r] -= d;
+            if constexpr (kMK) {
+              if (h == 0) qf[KS][0] = (__bf16)(-m_run);
+            } else {
+              if (h == 0) {
+                const __bf16 hi = (__bf16)(-m_run);
+                mqB[0] = hi;
+                mqB[1] = (__bf16)(-m_run - (float)hi);
+              }
+            }
+          } else {
+            const float delta = need ? mx : 0.f;
+            const float alpha = fast_exp2(-delta);
+            if (sub > 0) {
+  #pragma unroll
+              for (int mt = 0; mt < 2; ++mt)
+  #pragma unroll
+                for (int r = 0; r < 16; ++r) oacc[mt][r] *= alpha;
+              lsum *= alpha;
+            }
+            m_run = (sub == 0) ? delta : m_run + delta;
+  #pragma unroll
+            for (int u = 0; u < 2; ++u)
+  #pragma unroll
               for (int r = 0; r < 16; ++r) sacc[u][r] -= delta;
+  #pragma unroll
+            for (int r = 0; r < 16; ++r) minit[r] = -m_run;
           }
         }
+  #pragma unroll
+        for (int u = 0; u < 2; ++u)
+  #pragma unroll
+          for (int s = 0; s < 2; ++s)
+  #pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float p = (VAR & 64) ? sacc[u][8 * s + e] : fast_exp2(sacc[u][8 * s + e]);
+              if constexpr (!kOnes) lsum += p;
+              pf[u][s][e] = (__bf16)p;
+            }
+      } else {
+        const float tm = mx * a.c_log2;
+        const bool need = tm > m_run + kThr;
+        if (__builtin_amdgcn_ballot_w64(need)) {
+          const float m_new = need ? tm : m_run;
+          const float alpha = fast_exp2(m_run - m_new);
+  #pragma unroll
+          for (int mt = 0; mt < 2; ++mt)
+  #pragma unroll
+            for (int r = 0; r < 16; ++r) oacc[mt][r] *= alpha;
+          lsum *= alpha;
+          m_run = m_new;
+        }
+  #pragma unroll
+        for (int u = 0; u < 2; ++u)
+  #pragma unroll
+          for (int s = 0; s < 2; ++s)
+  #pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float p = fast_exp2(fmaf(sacc[u][8 * s + e], a.c_log2, -m_run));
+              if constexpr (!kOnes) lsum += p;
+              pf[u][s][e] = (__bf16)p;
+            }
       }
-#pragma unroll
+
+      mark(1);                 // max, rescale, exp2, cvt (waits on the S results)
+      // ---- O^T += V^T . P^T  (2 sub-tiles x 2 k-steps x 2 d-tiles)
+      if constexpr ((VAR & 32) != 0) __builtin_amdgcn_s_setprio(1);   // MFMA-issuing wave first
+  #pragma unroll
       for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float p = fast_exp2(sacc[u][8 * s + e]);
-            if constexpr (!kOnes) lsum += p;
-            pf[u][s][e] = (__bf16)p;
+  #pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const int row = 32 * u + 16 * s + 4 * (lane >> 5) + ((lane >> 2) & 3);
+  #pragma unroll
+          for (int mt = 0; mt < 2; ++mt) {
+            const int blk = 2 * mt + ((lane >> 4) & 1);
+            const char* p0;
+            if constexpr (kTwo) {
+              p0 = Vb + (vlane[mt] + (32 * u + 16 * s) * VROWB);
+            } else {
+              p0 = Vb + row * VROWB + 32 * (blk ^ (row & 3)) + 8 * (lane & 3);
+            }
+            const char* p1 = p0 + 8 * VROWB;   // rows + 8 keep (row & 3)
+            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
+            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p1);
+            const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+            oacc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[u][s], oacc[mt], 0, 0, 0);
           }
-    } else {
-      const float tm = mx * a.c_log2;
-      const bool need = tm > m_run + kThr;
-      if (__builtin_amdgcn_ballot_w64(need)) {
-        const float m_new = need ? tm : m_run;
-        const float alpha = fast_exp2(m_run - m_new);
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) oacc[mt][r] *= alpha;
-        lsum *= alpha;
-        m_run = m_new;
-      }
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float p = fast_exp2(fmaf(sacc[u][8 * s + e], a.c_log2, -m_run));
-            if constexpr (!kOnes) lsum += p;
-            pf[u][s][e] = (__bf16)p;
-          }
+        }
+      if constexpr ((VAR & 32) != 0) __builtin_amdgcn_s_setprio(0);
     }
 
-    // ---- O^T += V^T . P^T  (2 sub-tiles x 2 k-steps x 2 d-tiles)
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int row = 32 * u + 16 * s + 4 * (lane >> 5) + ((lane >> 2) & 3);
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
-          const int blk = 2 * mt + ((lane >> 4) & 1);
-          const char* p0 = Vb + row * VROWB + 32 * (blk ^ (row & 3)) + 8 * (lane & 3);
-          const char* p1 = p0 + 8 * VROWB;   // rows + 8 keep (row & 3)
-          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
-          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p1);
-          const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-          oacc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[u][s], oacc[mt], 0, 0, 0);
-        }
-      }
-
-    if (t + 1 < ntiles) store_tile((t + 1) & 1);
+    mark(2);                   // PV MFMAs issued (V fragment reads waited)
+    if constexpr (kPF2) {
+      if (t + 1 < ntiles) store_from(stage2[1 - SET], (t + 1) & 1);
+    } else {
+      if (t + 1 < ntiles && (VAR & 128) == 0) store_tile((t + 1) & 1);
+    }
+    // VAR & 16384 (with 8192): issue the next tile's DMA after this tile's last LDS read -- the
+    // compiler orders every LDS read after any in-flight LDS-DMA (vmcnt(0)), so an early issue
+    // makes the V reads wait for it
+    if constexpr ((VAR & 16384) != 0) {
+      if (t + 1 < ntiles) load_tile((t + 1) * KT);
+    }
     if constexpr (kDMA) __builtin_amdgcn_s_waitcnt(0x0f70);   // this wave's DMA pieces landed
-    __syncthreads();
-  };
-  if constexpr (kDMA) {
+    mark(3);                   // next tile's stage stored to LDS (waits on its loads)
+    if constexpr ((VAR & 256) == 0) __syncthreads();
+    mark(4);                   // barrier
+    };
+  if constexpr (kPF2) {
     for (int t = 0; t < ntiles; t += 2) {
       tile_step(t, std::integral_constant<int, 0>());
       if (t + 1 < ntiles) tile_step(t + 1, std::integral_constant<int, 1>());
     }
   } else {
-    for (int t = 0; t < ntiles; ++t) tile_step(t, std::integral_constant<int, 0>());
+    if constexpr ((VAR & 65536) != 0) {
+      for (int t = 0; t < ntiles; t += 2) {
+        tile_step(t, std::integral_constant<int, 0>());
+        if (t + 1 < ntiles) tile_step(t + 1, std::integral_constant<int, 1>());
+      }
+    } else {
+      for (int t = 0; t < ntiles; ++t) tile_step(t, std::integral_constant<int, 0>());
+    }
   }
 
+  if constexpr (kStamp) {
+    const unsigned long long t_end = stamp_now();
+    sacc_t[5] = t_end - t_kernel0;
+    if (lane == 0) {
+#pragma unroll
+      for (int i2 = 0; i2 < 6; ++i2) atomicAdd(&g_attn_stamps[i2], sacc_t[i2]);
+      atomicAdd(&g_attn_stamps[6], (unsigned long long)ntiles);
+      atomicAdd(&g_attn_stamps[7], 1ull);
+    }
+  }
   // ---- epilogue
   float l;
   if constexpr (kOnes) {
@@ -782,11 +1055,8 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   if constexpr (kZM) {
     m_run = 0.f;
     const uint32_t eb = __float_as_uint(l) & 0x7f800000u;
-    // with zero-pad keys (p = 1 each) a tiny real-key sum is not flagged: the pads then dominate
-    // exactly as in the reference
     zm_bad = eb == 0x7f800000u || !(l <= 0x1p100f) || (npad == 0 && !(l >= 0x1p-100f));
   }
-  // the reference's unmasked zero-padded keys (dilated_attention.py:85-91): npad keys of score 0
   float mr = m_run, so = 1.f;
   if (npad > 0) {
     const float mf = fmaxf(mr, 0.f);
@@ -796,8 +1066,9 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   }
   const float inv = so / l;
   const int i = q0 + w * 32 + l32;
+  const AttnBranch& br = brr;
   if (i < rows_needed) {
-    uint16_t* orow = brr.o + (((int64_t)bn * g.m + i) * a.H + hh) * (int64_t)D;
+    uint16_t* orow = br.o + (((int64_t)bn * g.m + i) * a.H + hh) * (int64_t)D;
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
@@ -810,21 +1081,25 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
         }
       }
     float lse = (mr + __builtin_amdgcn_logf(l)) * 0.69314718055994530942f;
-    if constexpr (kZM) {     // overflowed / out of range: flag the row for the fixup pass
+    if constexpr (kNM) {     // overflowed (some p = inf): flag the row for the fixup pass
       if ((__float_as_uint(l) & 0x7f800000u) == 0x7f800000u || !(l > 0.f) || zm_bad) lse = __uint_as_float(kLseRedo);
     }
-    if (h == 0) brr.lse[((int64_t)bn * a.H + hh) * g.m + i] = lse;
+    if (h == 0) br.lse[((int64_t)bn * a.H + hh) * g.m + i] = lse;
   }
 }
 
-// One work item per block (XCD-grouped order), or, for the fixup pass (kModeFix), kFixItems
-// consecutive items per block: the block reads the lse of every needed row of all of them at once
-// (wave w: items 8w .. 8w + 7; 16 independent loads per lane) and exits unless some row holds the
-// kLseRedo marker, so the pass costs about one load latency per 32 items when nothing overflowed.
-template <int D, bool kPre, int MODE, bool kTab = false>
-__global__ __launch_bounds__(256, 2) void dilated_attn32_kernel(const AttnArgs a) {
-  if constexpr (MODE == kModeFix) {
-    constexpr int NW = 4, QB = 128;
+// The kernel: one work item per block, or (VAR & 524288, the fixup pass after a VAR & 262144
+// launch) kFixItems consecutive items per block -- the block reads the lse of every needed row of
+// all of them at once (wave w: items 8w .. 8w + 7; 16 independent loads per lane) and exits unless
+// some row holds the kLseRedo marker, so the pass costs about one load latency per 32 items when
+// nothing overflowed.
+constexpr int kFixItems = 32;
+
+template <int D, bool kPre, int NW, int VAR = 0, int OCC = 2, bool kTab = false>
+__global__ __launch_bounds__(NW * 64, OCC) void dilated_attn32_kernel(const AttnArgs a) {
+  if constexpr ((VAR & 524288) != 0) {
+    static_assert(NW == 4 && kFixItems % NW == 0, "fixup scan: 4 waves x kFixItems / 4 items");
+    constexpr int QB = NW * 32;
     const int it0 = (int)blockIdx.x * kFixItems;
     // wave index made provably uniform: the item decode then runs on the scalar unit (s_load from
     // the kernel arguments), not as a chain of dependent per-lane global loads
@@ -858,11 +1133,603 @@ __global__ __launch_bounds__(256, 2) void dilated_attn32_kernel(const AttnArgs a
 #pragma unroll
     for (int n = 0; n < NV; ++n) flagged |= use[n] && vals[n] == kLseRedo;
     if (!__syncthreads_or(flagged)) return;
-    for (int k = 0; k < kFixItems && it0 + k < a.total_items; ++k) attn32_item<D, kPre, MODE, kTab>(a, it0 + k);
+    for (int k = 0; k < kFixItems && it0 + k < a.total_items; ++k) attn32_item<D, kPre, NW, VAR, OCC, kTab>(a, it0 + k);
   } else {
-    attn32_item<D, kPre, MODE, kTab>(a, (int)xcd_group(blockIdx.x, gridDim.x));
+    attn32_item<D, kPre, NW, VAR, OCC, kTab>(a, (int)xcd_group(blockIdx.x, gridDim.x));
   }
 }
+
+// ---------------------------------------------------------------------------------------
+// v4 (D = 48, q pre-scaled): the v2 math with TWO 32-query blocks per wave (64 queries, 256 per
+// workgroup).  Every K fragment (ds_read_b128) and V^T fragment (2 x ds_read_b64_tr_b16) read
+// from LDS feeds two MFMAs, and a staged 64-key tile serves 256 queries: half the LDS reads
+// and writes (and half the K/V fetches) per FLOP of v2.  K/V tiles are staged with buffer loads
+// through a per-tile descriptor whose record count ends at the last valid key row, so rows past
+// c read as zero in hardware (no branch, no zero-filled registers).  Two waves per SIMD.
+// WV bits (A/B): 1 = all six K fragments read before the S MFMAs; 2 = one rescale decision (and
+// branch) for both query blocks, so the exps of both blocks and the PV MFMAs share one block.
+template <int NW, int WV = 0>
+__global__ __launch_bounds__(NW * 64, 2) void dilated_attn_w64_kernel(const AttnArgs a) {
+  constexpr int D = 48;
+  constexpr int NT = NW * 64;
+  constexpr int QB = NW * 64;                // query rows per workgroup
+  constexpr int KT = 64;                     // keys per staged tile
+  constexpr int KS = D / 16;
+  constexpr int KROWB = D * 2 + 16;          // K image row bytes (16-B pad: conflict-free b128 reads)
+  constexpr int VROWB = 128;                 // V image row: 64 bf16 (48 values + 16 ones), swizzled blocks
+  constexpr int KTILE = KT * KROWB;
+  constexpr int VTILE = KT * VROWB;
+  constexpr int BUF = KTILE + VTILE;
+  constexpr int CH = D / 8;
+  constexpr int TOT = 2 * KT * CH;           // 16-byte chunks of one K tile + one V tile
+  constexpr int LPT = (TOT + NT - 1) / NT;
+  constexpr float kThr = 8.0f;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+
+  WorkItem wi;
+  decode_item(a, (int)xcd_group(blockIdx.x, gridDim.x), wi);
+  const GpBranch g = a.br[wi.bi].g;
+  const int hh = wi.hh, c = wi.c, bn = wi.bn;
+  const int rows_needed = wi.i_hi;
+  const int q0 = wi.i_lo + wi.qb * QB;
+  if (q0 >= rows_needed) return;
+  const int qvalid = c < rows_needed ? c : rows_needed;
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int l32 = lane & 31, h = lane >> 5;
+  const AttnBranch& brr = a.br[wi.bi];
+  const int64_t tok0 = (int64_t)wi.bidx * a.L + (int64_t)wi.n * g.s + wi.j;
+  const int64_t qstride = (int64_t)g.r * a.q_stride;
+  const int64_t kvstride = (int64_t)g.r * brr.kv_stride;
+  const int kcol = brr.kv_sparse ? (hh % g.hpg) * D : hh * D;
+  const uint16_t* qbase = a.q + (tok0 - a.q_tok_base) * a.q_stride + hh * D;
+  const uint16_t* kbase = brr.k + (tok0 - brr.kv_tok_base) * brr.kv_stride + kcol;
+  const int64_t kv_dv = (int64_t)((const char*)(brr.v + (tok0 - brr.kv_tok_base) * brr.kv_stride + kcol) -
+                                  (const char*)kbase);
+
+  // V images: d-columns 48..63 of every row hold bf16 1.0 (the MFMA then yields the row sum)
+  for (int idx = threadIdx.x; idx < 2 * KT * 2; idx += NT) {
+    const int buf = idx / (2 * KT), rem = idx % (2 * KT), row = rem >> 1, half = rem & 1;
+    const uint4 ones = make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
+    *reinterpret_cast<uint4*>(smem + buf * BUF + KTILE + row * VROWB + 32 * (3 ^ (row & 3)) + 16 * half) = ones;
+  }
+
+  // Q fragments of both query blocks: lane holds Q[q = l32][d = 16ks + 8h .. +7]
+  bf16x8 qf[2][KS];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int i = q0 + w * 64 + qb * 32 + l32;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      bf16x8 z = {};
+      if (i < qvalid) z = *reinterpret_cast<const bf16x8*>(qbase + (int64_t)i * qstride + 16 * ks + 8 * h);
+      qf[qb][ks] = z;
+    }
+  }
+
+  // staging chunks: byte offset from key 0's K row (V chunks at kv_dv) and LDS offset
+  int lvo[LPT], loff[LPT];
+#pragma unroll
+  for (int u = 0; u < LPT; ++u) {
+    const int idx = (threadIdx.x + NT * u) % TOT;
+    const int tsel = idx / (KT * CH);
+    const int rem = idx % (KT * CH);
+    const int row = rem / CH, ch = rem % CH;
+    lvo[u] = (int)(tsel * kv_dv + (int64_t)row * kvstride * 2 + ch * 16);
+    loff[u] = tsel ? KTILE + row * VROWB + 32 * ((ch >> 1) ^ (row & 3)) + 16 * (ch & 1) : row * KROWB + ch * 16;
+  }
+  uint4 stage[LPT];
+  auto load_tile = [&](int kv0) {
+    const int64_t tb = (int64_t)kv0 * kvstride * 2;
+    const int64_t nrec = (int64_t)(c - kv0 - 1) * kvstride * 2 + kv_dv + 2 * D;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((const char*)kbase + tb), (short)0, (int)(nrec < 0x7fffffff ? nrec : 0x7fffffff), 0x00020000);
+#pragma unroll
+    for (int u = 0; u < LPT; ++u)
+      if (TOT % NT == 0 || threadIdx.x + NT * u < TOT)
+        stage[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, lvo[u], 0, 0));
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < LPT; ++u) {
+      if (TOT % NT != 0 && threadIdx.x + NT * u >= TOT) continue;
+      *reinterpret_cast<uint4*>(smem + buf * BUF + loff[u]) = stage[u];
+    }
+  };
+
+  float m_run[2] = {0.f, 0.f};   // running max (log2 domain) of query l32 of each block
+  f32x16 oacc[2][2];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) oacc[qb][mt][r] = 0.f;
+
+  // WV & 4: persistent C blocks holding -m_run of each query block (0 before the first tile):
+  // S's first k-step reads them, so no per-tile accumulator initialisation
+  f32x16 minit[2];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) minit[qb][r] = 0.f;
+  const int ntiles = (c + KT - 1) / KT;
+  if (ntiles > 0) {
+    load_tile(0);
+    store_tile(0);
+  }
+  __syncthreads();
+  __builtin_amdgcn_s_waitcnt(0x0f70);    // vmcnt(0): see dilated_attn32_kernel
+
+  for (int t = 0; t < ntiles; ++t) {
+    if (t + 1 < ntiles) load_tile((t + 1) * KT);
+    const int kv0 = t * KT;
+    const char* Kb = smem + (t & 1) * BUF;
+    const char* Vb = Kb + KTILE;
+    // ---- S^T = K.Q^T for 2 key halves x 2 query blocks; accumulators start at -m_run
+    f32x16 sacc[2][2];
+    if constexpr ((WV & 4) == 0) {
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        const float init = (t > 0) ? -m_run[qb] : 0.f;
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) sacc[qb][u][r] = init;
+      }
+    }
+    bf16x8 kf[2][KS];
+    if constexpr ((WV & 1) != 0) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+          kf[u][ks] = *reinterpret_cast<const bf16x8*>(Kb + (32 * u + l32) * KROWB + 32 * ks + 16 * h);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const bf16x8 kk = ((WV & 1) != 0) ? kf[u][ks]
+                                          : *reinterpret_cast<const bf16x8*>(Kb + (32 * u + l32) * KROWB + 32 * ks + 16 * h);
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+          sacc[qb][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kk, qf[qb][ks],
+                                                                ((WV & 4) != 0 && ks == 0) ? minit[qb] : sacc[qb][u], 0, 0, 0);
+      }
+    if (kv0 + KT > c) {      // keys >= c: zero pads, added analytically at the end
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (kv0 + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * h >= c) sacc[qb][u][r] = -INFINITY;
+    }
+    // ---- online softmax with deferred rescale, per query block
+    bf16x8 pf[2][2][2];
+    if constexpr ((WV & 2) != 0) {
+      float mxq[2];
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        float mxa = sacc[qb][0][0], mxb = sacc[qb][1][0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) {
+          mxa = fmaxf(mxa, sacc[qb][0][r]);
+          mxb = fmaxf(mxb, sacc[qb][1][r]);
+        }
+        float mx = fmaxf(mxa, mxb);
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+        mxq[qb] = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+      }
+      const bool need0 = (t == 0) || (mxq[0] > kThr), need1 = (t == 0) || (mxq[1] > kThr);
+      if (__builtin_amdgcn_ballot_w64(need0 || need1)) {
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+          const float delta = (qb ? need1 : need0) ? mxq[qb] : 0.f;
+          if (t > 0) {
+            const float alpha = fast_exp2(-delta);
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+              for (int r = 0; r < 16; ++r) oacc[qb][mt][r] *= alpha;
+          }
+          m_run[qb] = (t == 0) ? delta : m_run[qb] + delta;
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sacc[qb][u][r] -= delta;
+          if constexpr ((WV & 4) != 0) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) minit[qb][r] = -m_run[qb];
+          }
+        }
+      }
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) pf[qb][u][s2][e] = (__bf16)fast_exp2(sacc[qb][u][8 * s2 + e]);
+    } else
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      float mxa = sacc[qb][0][0], mxb = sacc[qb][1][0];
+#pragma unroll
+      for (int r = 1; r < 16; ++r) {
+        mxa = fmaxf(mxa, sacc[qb][0][r]);
+        mxb = fmaxf(mxb, sacc[qb][1][r]);
+      }
+      float mx = fmaxf(mxa, mxb);
+      {
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+        mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+      }
+      const bool need = (t == 0) || (mx > kThr);
+      if (__builtin_amdgcn_ballot_w64(need)) {
+        const float delta = need ? mx : 0.f;
+        if (t > 0) {
+          const float alpha = fast_exp2(-delta);
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) oacc[qb][mt][r] *= alpha;
+        }
+        m_run[qb] = (t == 0) ? delta : m_run[qb] + delta;
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) sacc[qb][u][r] -= delta;
+        if constexpr ((WV & 4) != 0) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) minit[qb][r] = -m_run[qb];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) pf[qb][u][s2][e] = (__bf16)fast_exp2(sacc[qb][u][8 * s2 + e]);
+    }
+    // ---- O^T += V^T . P^T: each V^T fragment feeds both query blocks
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int row = 32 * u + 16 * s2 + 4 * (lane >> 5) + ((lane >> 2) & 3);
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          const int blk = 2 * mt + ((lane >> 4) & 1);
+          const char* p0 = Vb + row * VROWB + 32 * (blk ^ (row & 3)) + 8 * (lane & 3);
+          const char* p1 = p0 + 8 * VROWB;
+          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
+          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p1);
+          const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+          for (int qb = 0; qb < 2; ++qb)
+            oacc[qb][mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[qb][u][s2], oacc[qb][mt], 0, 0, 0);
+        }
+      }
+    if (t + 1 < ntiles) store_tile((t + 1) & 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue (per query block)
+  const AttnBranch& br = a.br[wi.bi];
+  const int npad = g.m - c;
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    float l = oacc[qb][1][8];               // d-row 48 (+4h): the ones row = sum_k P
+    float mr = m_run[qb], so = 1.f;
+    if (npad > 0) {
+      const float mf = fmaxf(mr, 0.f);
+      so = fast_exp2(mr - mf);
+      l = l * so + (float)npad * fast_exp2(-mf);
+      mr = mf;
+    }
+    const float inv = so / l;
+    const int i = q0 + w * 64 + qb * 32 + l32;
+    if (i < rows_needed) {
+      uint16_t* orow = br.o + (((int64_t)bn * g.m + i) * a.H + hh) * (int64_t)D;
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int rg = 0; rg < 4; ++rg) {
+          const int d0 = 32 * mt + 8 * rg + 4 * h;
+          if (d0 < D) {
+            float vv[4] = {oacc[qb][mt][4 * rg] * inv, oacc[qb][mt][4 * rg + 1] * inv,
+                           oacc[qb][mt][4 * rg + 2] * inv, oacc[qb][mt][4 * rg + 3] * inv};
+            store_bf16<4>(orow + d0, vv);
+          }
+        }
+      if (h == 0) br.lse[((int64_t)bn * a.H + hh) * g.m + i] = (mr + __builtin_amdgcn_logf(l)) * 0.69314718055994530942f;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// v3: the v2 formulation (q pre-scaled into the log2 domain) software-pipelined across 64-key
+// tiles so every MFMA has independent VALU work beside it in the same wave:
+//   phase A: S(t+1) = K(t+1).Q^T MFMAs      | exp2/cvt of S(t), keys 0..31
+//   phase B: O += V(t)^T.P(t)^T, keys 0..31 | exp2/cvt of S(t), keys 32..63
+//   phase C: O += V(t)^T.P(t)^T, keys 32..63| row max of S(t+1), deferred-rescale decision
+// LDS holds K one tile ahead of V: iteration t reads K(t+1) and V(t) and stages K(t+2), V(t+1)
+// (both double buffered; one barrier per tile).
+template <int D>
+__global__ __launch_bounds__(256, 2) void dilated_attn_pp_kernel(const AttnArgs a) {
+  static_assert(D == 48 || D == 64, "v3 kernel covers D = 48 and 64");
+  constexpr int NT = 256;
+  constexpr int QB = 128;
+  constexpr int KT = 64;                     // keys per tile
+  constexpr int KS = D / 16;
+  constexpr bool kOnes = (D % 32) != 0;
+  constexpr int KROWB = D * 2 + 16;
+  constexpr int VROWB = 128;
+  constexpr int KTILE = KT * KROWB;
+  constexpr int VTILE = KT * VROWB;
+  constexpr int VOFF = 2 * KTILE;            // [K0 | K1 | V0 | V1]
+  constexpr int CH = D / 8;
+  constexpr int KCH = KT * CH;               // 16-byte chunks of one K (or V) tile
+  constexpr int LPT = 2 * KCH / NT;          // chunks per thread for one K tile + one V tile
+  static_assert((2 * KCH) % NT == 0, "");
+  constexpr float kThr = 8.0f;
+  __shared__ __attribute__((aligned(16))) char smem[2 * KTILE + 2 * VTILE];
+
+  WorkItem wi;
+  decode_item(a, (int)xcd_group(blockIdx.x, gridDim.x), wi);
+  const GpBranch g = a.br[wi.bi].g;
+  const int hh = wi.hh, c = wi.c, bn = wi.bn;
+  const int rows_needed = wi.i_hi;
+  const int q0 = wi.i_lo + wi.qb * QB;
+  if (q0 >= rows_needed) return;
+  const int qvalid = c < rows_needed ? c : rows_needed;
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int l32 = lane & 31, h = lane >> 5;
+  const AttnBranch& brr = a.br[wi.bi];
+  const int64_t tok0 = (int64_t)wi.bidx * a.L + (int64_t)wi.n * g.s + wi.j;
+  const int64_t qstride = (int64_t)g.r * a.q_stride;
+  const int64_t kvstride = (int64_t)g.r * brr.kv_stride;
+  const int kcol = brr.kv_sparse ? (hh % g.hpg) * D : hh * D;
+  const uint16_t* qbase = a.q + (tok0 - a.q_tok_base) * a.q_stride + hh * D;
+  const uint16_t* kbase = brr.k + (tok0 - brr.kv_tok_base) * brr.kv_stride + kcol;
+  const uint16_t* vbase = brr.v + (tok0 - brr.kv_tok_base) * brr.kv_stride + kcol;
+
+  if constexpr (kOnes) {
+    for (int idx = threadIdx.x; idx < 2 * KT * 2; idx += NT) {
+      const int buf = idx / (2 * KT), rem = idx % (2 * KT), row = rem >> 1, half = rem & 1;
+      const uint4 ones = make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
+      *reinterpret_cast<uint4*>(smem + VOFF + buf * VTILE + row * VROWB + 32 * (3 ^ (row & 3)) + 16 * half) = ones;
+    }
+  }
+
+  bf16x8 qf[KS];
+  {
+    const int i = q0 + w * 32 + l32;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      bf16x8 z = {};
+      if (i < qvalid) z = *reinterpret_cast<const bf16x8*>(qbase + (int64_t)i * qstride + 16 * ks + 8 * h);
+      qf[ks] = z;
+    }
+  }
+
+  const int ntiles = (c + KT - 1) / KT;
+  // staging: chunk idx < KCH is K of tile tk, else V of tile tv
+  uint4 stage[LPT];
+  auto load_stage = [&](int tk, int tv) {
+#pragma unroll
+    for (int u = 0; u < LPT; ++u) {
+      const int idx = threadIdx.x + NT * u;
+      const int tsel = idx / KCH;
+      const int rem = idx % KCH;
+      const int row = rem / CH, ch = rem % CH;
+      const int key = (tsel ? tv : tk) * KT + row;
+      uint4 z = make_uint4(0, 0, 0, 0);
+      if (key < c) z = *reinterpret_cast<const uint4*>((tsel ? vbase : kbase) + (int64_t)key * kvstride + ch * 8);
+      stage[u] = z;
+    }
+  };
+  auto store_stage = [&](int bk, int bv) {
+#pragma unroll
+    for (int u = 0; u < LPT; ++u) {
+      const int idx = threadIdx.x + NT * u;
+      const int tsel = idx / KCH;
+      const int rem = idx % KCH;
+      const int row = rem / CH, ch = rem % CH;
+      const int off = tsel ? VOFF + bv * VTILE + row * VROWB + 32 * ((ch >> 1) ^ (row & 3)) + 16 * (ch & 1)
+                           : bk * KTILE + row * KROWB + ch * 16;
+      *reinterpret_cast<uint4*>(smem + off) = stage[u];
+    }
+  };
+  auto compute_s = [&](int bk, const f32x16& init, f32x16 (&acc)[2]) {
+    const char* Kb = smem + bk * KTILE;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Kb + (32 * u + l32) * KROWB + 32 * ks + 16 * h);
+        acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], ks == 0 ? init : acc[u], 0, 0, 0);
+      }
+    }
+  };
+  auto mask_tail = [&](int t, f32x16 (&acc)[2]) {
+    const int kv0 = t * KT;
+    if (kv0 + KT > c) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (kv0 + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * h >= c) acc[u][r] = -INFINITY;
+    }
+  };
+  auto row_max = [&](const f32x16 (&acc)[2]) {
+    float mxa = acc[0][0], mxb = acc[1][0];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) {
+      mxa = fmaxf(mxa, acc[0][r]);
+      mxb = fmaxf(mxb, acc[1][r]);
+    }
+    float mx = fmaxf(mxa, mxb);
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+    return fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+  };
+
+  float m_run = 0.f;
+  float lsum = 0.f;
+  f32x16 oacc[2];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) oacc[mt][r] = 0.f;
+
+  f32x16 scur[2], snext[2];
+  f32x16 minit;                             // -m_run in every element (C operand of S's first k-step)
+#pragma unroll
+  for (int r = 0; r < 16; ++r) minit[r] = 0.f;
+  if (ntiles > 0) {
+    // prologue: K(0), V(0) -> LDS; S(0) with its exact max; K(1) -> LDS
+    load_stage(0, 0);
+    store_stage(0, 0);
+    __syncthreads();
+    load_stage(1, ntiles);                  // K(1); the V half loads nothing (tile past the end)
+    compute_s(0, minit, scur);
+    mask_tail(0, scur);
+    m_run = row_max(scur);
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) scur[u][r] -= m_run;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) minit[r] = -m_run;
+#pragma unroll
+    for (int u = 0; u < LPT; ++u) {         // store only the K half (the V half is tile 'ntiles')
+      const int idx = threadIdx.x + NT * u;
+      if (idx < KCH) {
+        const int row = idx / CH, ch = idx % CH;
+        *reinterpret_cast<uint4*>(smem + KTILE + row * KROWB + ch * 16) = stage[u];
+      }
+    }
+    __syncthreads();
+  }
+
+  for (int t = 0; t < ntiles; ++t) {
+    load_stage(t + 2, t + 1);
+    // phase A: S(t+1) | P(t) keys 0..31.  Branch-free: after the last tile S(t+1) reads a zeroed
+    // K buffer and is fully masked (row max -inf: no rescale), so nothing of it is used.
+    compute_s((t + 1) & 1, minit, snext);
+    bf16x8 pf[2][2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float p = fast_exp2(scur[0][8 * s2 + e]);
+        if constexpr (!kOnes) lsum += p;
+        pf[0][s2][e] = (__bf16)p;
+      }
+    const char* Vb = smem + VOFF + (t & 1) * VTILE;
+    // phase B: O += V(t)^T P(t)^T keys 0..31 | P(t) keys 32..63
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int row = 16 * s2 + 4 * (lane >> 5) + ((lane >> 2) & 3);
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const int blk = 2 * mt + ((lane >> 4) & 1);
+        const char* p0 = Vb + row * VROWB + 32 * (blk ^ (row & 3)) + 8 * (lane & 3);
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0 + 8 * VROWB));
+        const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        oacc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[0][s2], oacc[mt], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float p = fast_exp2(scur[1][8 * s2 + e]);
+        if constexpr (!kOnes) lsum += p;
+        pf[1][s2][e] = (__bf16)p;
+      }
+    // phase C: O += V(t)^T P(t)^T keys 32..63 | row max of S(t+1)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int row = 32 + 16 * s2 + 4 * (lane >> 5) + ((lane >> 2) & 3);
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const int blk = 2 * mt + ((lane >> 4) & 1);
+        const char* p0 = Vb + row * VROWB + 32 * (blk ^ (row & 3)) + 8 * (lane & 3);
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0 + 8 * VROWB));
+        const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        oacc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[1][s2], oacc[mt], 0, 0, 0);
+      }
+    }
+    {
+      mask_tail(t + 1, snext);
+      const float mx = row_max(snext);       // scores of tile t+1 minus m_run
+      const bool need = mx > kThr;
+      if (__builtin_amdgcn_ballot_w64(need)) {
+        const float delta = need ? mx : 0.f;
+        const float alpha = fast_exp2(-delta);
+        m_run += delta;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) minit[r] = -m_run;
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) snext[u][r] -= delta;
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) oacc[mt][r] *= alpha;
+        lsum *= alpha;
+      }
+    }
+    store_stage(t & 1, (t + 1) & 1);
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 2; ++u) scur[u] = snext[u];
+  }
+
+  // ---- epilogue (as v2)
+  float l;
+  if constexpr (kOnes) {
+    l = oacc[1][8];
+  } else {
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(lsum), __float_as_uint(lsum), false, false);
+    l = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+  }
+  const int npad = g.m - c;
+  float mr = m_run, so = 1.f;
+  if (npad > 0) {
+    const float mf = fmaxf(mr, 0.f);
+    so = fast_exp2(mr - mf);
+    l = l * so + (float)npad * fast_exp2(-mf);
+    mr = mf;
+  }
+  const float inv = so / l;
+  const int i = q0 + w * 32 + l32;
+  const AttnBranch& br = a.br[wi.bi];
+  if (i < rows_needed) {
+    uint16_t* orow = br.o + (((int64_t)bn * g.m + i) * a.H + hh) * (int64_t)D;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        const int d0 = 32 * mt + 8 * rg + 4 * h;
+        if (d0 < D) {
+          float vv[4] = {oacc[mt][4 * rg] * inv, oacc[mt][4 * rg + 1] * inv, oacc[mt][4 * rg + 2] * inv,
+                         oacc[mt][4 * rg + 3] * inv};
+          store_bf16<4>(orow + d0, vv);
+        }
+      }
+    if (h == 0) br.lse[((int64_t)bn * a.H + hh) * g.m + i] = (mr + __builtin_amdgcn_logf(l)) * 0.69314718055994530942f;
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 struct MergeBranch {
   GpBranch g;
@@ -1087,10 +1954,17 @@ extern "C" int gp_dilated_attn_fwd_ex(const uint16_t* q, int64_t q_row_stride, i
   a.nbranch = nbranch;
   const float scale = softmax_scale > 0.f ? softmax_scale : 1.0f / sqrtf((float)D);
   a.c_log2 = q_log2_prescaled ? 1.0f : scale * 1.44269504088896340736f;
-  GP_REQUIRE(!q_log2_prescaled || D != 96, "gp_dilated_attn_fwd: q_log2_prescaled needs D in {48, 64}");
-  // LDS-DMA staging addresses V as K + dv inside one buffer descriptor whose record count ends at
-  // the last valid row: needs v at or after k in memory, a row stride that covers dv + one head
-  // (rows past c then fall outside the records) and 32-bit tile offsets
+  const char* impl_env = getenv("GP_ATTN_IMPL");   // A/B switch: 1 = 16x16x32 kernel, 2 = 32x32x16 kernel
+  const int impl = (D == 96) ? 1 : (impl_env ? atoi(impl_env) : 2);
+  GP_REQUIRE(impl >= 1 && impl <= 4, "gp_dilated_attn_fwd: GP_ATTN_IMPL must be 1..4");
+  GP_REQUIRE(impl != 4 || (D == 48 && q_log2_prescaled), "gp_dilated_attn_fwd: GP_ATTN_IMPL=4 needs D = 48, prescaled q");
+  GP_REQUIRE(impl != 3 || q_log2_prescaled, "gp_dilated_attn_fwd: GP_ATTN_IMPL=3 needs q_log2_prescaled");
+  GP_REQUIRE(!q_log2_prescaled || impl != 1, "gp_dilated_attn_fwd: q_log2_prescaled needs D in {48, 64}");
+  const char* var_env = getenv("GP_ATTN_VAR");
+  const int var = var_env ? atoi(var_env) : 0;
+  // buffer-descriptor staging (impl 4, VAR 2048) addresses V as K + dv inside one descriptor whose
+  // record count ends at the last valid row: needs v at or after k in memory, a row stride that
+  // covers dv + one head (rows past c then fall outside the records), 32-bit tile offsets
   bool kv_desc_ok = true;
   for (int b = 0; b < nbranch; ++b) {
     const GpAttnBranch& d = branches[b];
@@ -1098,7 +1972,9 @@ extern "C" int gp_dilated_attn_fwd_ex(const uint16_t* q, int64_t q_row_stride, i
     const int64_t rs2 = 2 * d.kv_row_stride;
     kv_desc_ok = kv_desc_ok && dv >= 0 && rs2 >= dv + 2 * D && dv + 64 * (int64_t)d.ratio * rs2 < 0x7fffffff;
   }
-  const int qblk = 128;   // query rows per workgroup
+  GP_REQUIRE(impl != 4 || kv_desc_ok, "gp_dilated_attn_fwd: GP_ATTN_IMPL=4 needs v after k within one row stride");
+  GP_REQUIRE(impl == 4 || !(var & 2048) || kv_desc_ok, "gp_dilated_attn_fwd: GP_ATTN_VAR & 2048 needs v after k within one row stride");
+  const int qblk = (impl == 2 && var >= 512 && (var & 512)) ? 256 : (impl == 4 ? 256 : 128);   // query rows per workgroup
   // order branches by keys per work item (descending) so the longest items start first
   int order[GP_MAX_BRANCHES];
   GpBranch geo[GP_MAX_BRANCHES];
@@ -1160,18 +2036,96 @@ extern "C" int gp_dilated_attn_fwd_ex(const uint16_t* q, int64_t q_row_stride, i
   a.ntab = 0;
   GP_REQUIRE(items < (int64_t)0x7fffffff, "gp_dilated_attn_fwd: too many work items");
   hipStream_t s = gp_stream(stream);
-  if (D == 96) {
-    dilated_attn_kernel<96><<<(unsigned)items, 256, 0, s>>>(a);
-  } else if (D == 48 && q_log2_prescaled && kv_desc_ok) {
-    // the product launch: no-max kernel, then the fixup pass (exits at once unless a row was flagged)
-    dilated_attn32_kernel<48, true, kModeFast><<<(unsigned)items, 256, 0, s>>>(a);
-    dilated_attn32_kernel<48, true, kModeFix><<<(unsigned)((items + kFixItems - 1) / kFixItems), 256, 0, s>>>(a);
-  } else if (D == 48) {
-    if (q_log2_prescaled) dilated_attn32_kernel<48, true, kModeGen><<<(unsigned)items, 256, 0, s>>>(a);
-    else dilated_attn32_kernel<48, false, kModeGen><<<(unsigned)items, 256, 0, s>>>(a);
+  if (impl == 1) {
+    switch (D) {
+      case 48: dilated_attn_kernel<48><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 64: dilated_attn_kernel<64><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 96: dilated_attn_kernel<96><<<(unsigned)items, 256, 0, s>>>(a); break;
+    }
+  } else if (impl == 4) {
+    switch (var) {
+      case 0: dilated_attn_w64_kernel<4, 0><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 1: dilated_attn_w64_kernel<4, 1><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 2: dilated_attn_w64_kernel<4, 2><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 3: dilated_attn_w64_kernel<4, 3><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 6: dilated_attn_w64_kernel<4, 6><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 7: dilated_attn_w64_kernel<4, 7><<<(unsigned)items, 256, 0, s>>>(a); break;
+      default: return gp_set_error("gp_dilated_attn_fwd: impl 4 GP_ATTN_VAR=%d unknown", var), GP_EARG;
+    }
+  } else if (impl == 3) {
+    if (D == 48) dilated_attn_pp_kernel<48><<<(unsigned)items, 256, 0, s>>>(a);
+    else dilated_attn_pp_kernel<64><<<(unsigned)items, 256, 0, s>>>(a);
+  } else if (q_log2_prescaled && D == 48 && var != 0) {
+    switch (var) {   // A/B variants of the v2 kernel (GP_ATTN_VAR; 100 = VAR 0)
+      case 100: dilated_attn32_kernel<48, true, 4, 0><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 1: dilated_attn32_kernel<48, true, 4, 1><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 2: dilated_attn32_kernel<48, true, 4, 2><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 3: dilated_attn32_kernel<48, true, 4, 3><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 4: dilated_attn32_kernel<48, true, 4, 4><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 7: dilated_attn32_kernel<48, true, 4, 7><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 11: dilated_attn32_kernel<48, true, 4, 3, 4><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 12: dilated_attn32_kernel<48, true, 4, 2, 4><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 15: dilated_attn32_kernel<48, true, 4, 7, 4><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 10: dilated_attn32_kernel<48, true, 4, 10><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 14: dilated_attn32_kernel<48, true, 4, 14><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 66: dilated_attn32_kernel<48, true, 4, 66><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 130: dilated_attn32_kernel<48, true, 4, 130><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 258: dilated_attn32_kernel<48, true, 4, 258><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 386: dilated_attn32_kernel<48, true, 4, 386><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 450: dilated_attn32_kernel<48, true, 4, 450><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 514: dilated_attn32_kernel<48, true, 8, 514><<<(unsigned)items, 512, 0, s>>>(a); break;
+      case 1538: dilated_attn32_kernel<48, true, 8, 1538><<<(unsigned)items, 512, 0, s>>>(a); break;
+      case 1026: dilated_attn32_kernel<48, true, 4, 1026><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 2050: dilated_attn32_kernel<48, true, 4, 2050><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 34818: dilated_attn32_kernel<48, true, 4, 34818><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 2054: dilated_attn32_kernel<48, true, 4, 2054><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 10246: dilated_attn32_kernel<48, true, 4, 10246><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 10242: dilated_attn32_kernel<48, true, 4, 10242><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 10243: dilated_attn32_kernel<48, true, 4, 10242, 5><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 79874: dilated_attn32_kernel<48, true, 4, 79874><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 210946: dilated_attn32_kernel<48, true, 4, 210946><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 1390594:  // 342018 with no offset at all (S from C = 0), then the fixup pass
+        dilated_attn32_kernel<48, true, 4, 1390594><<<(unsigned)items, 256, 0, s>>>(a);
+        dilated_attn32_kernel<48, true, 4, 79874 + 524288><<<(unsigned)((items + kFixItems - 1) / kFixItems), 256, 0, s>>>(a);
+        break;
+      case 1390595:  // test hook: 1390594 WITHOUT the fixup pass
+        dilated_attn32_kernel<48, true, 4, 1390594><<<(unsigned)items, 256, 0, s>>>(a);
+        break;
+      case 342019:   // test hook: 342018 WITHOUT the fixup pass (overflowed rows keep the lse marker)
+        dilated_attn32_kernel<48, true, 4, 342018><<<(unsigned)items, 256, 0, s>>>(a);
+        break;
+      case 342018:   // no per-tile max after tile 0, then the fixup pass for flagged blocks
+        dilated_attn32_kernel<48, true, 4, 342018><<<(unsigned)items, 256, 0, s>>>(a);
+        dilated_attn32_kernel<48, true, 4, 79874 + 524288><<<(unsigned)((items + kFixItems - 1) / kFixItems), 256, 0, s>>>(a);
+        break;
+      case 26626: dilated_attn32_kernel<48, true, 4, 26626><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 26627: dilated_attn32_kernel<48, true, 4, 26626, 5><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 14338: dilated_attn32_kernel<48, true, 4, 14338><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 6146: dilated_attn32_kernel<48, true, 4, 6146><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 6150: dilated_attn32_kernel<48, true, 4, 6150><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 2562: dilated_attn32_kernel<48, true, 8, 2562><<<(unsigned)items, 512, 0, s>>>(a); break;
+      case 34: dilated_attn32_kernel<48, true, 4, 34><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 26: dilated_attn32_kernel<48, true, 4, 10, 4><<<(unsigned)items, 256, 0, s>>>(a); break;
+      case 30: dilated_attn32_kernel<48, true, 4, 14, 4><<<(unsigned)items, 256, 0, s>>>(a); break;
+      default: return gp_set_error("gp_dilated_attn_fwd: GP_ATTN_VAR=%d unknown", var), GP_EARG;
+    }
+  } else if (q_log2_prescaled) {
+    // default: VAR 79874 = 14338 with the tile loop unrolled by two (+2-3 %); 14338: K/V tiles by LDS-DMA (buffer_load ... lds) through a bounded descriptor
+    // straight into the tile images (VAR 10242: +2-3 % over VAR 2050's buffer loads into registers,
+    // itself +5-7 % over VAR 2) and the -m start block of S from one MFMA of an exact hi + lo bf16
+    // pair instead of 16 v_mov (VAR 4096: +1.5 %); VAR 2 where the descriptor layout does not fit
+    if (D == 48 && kv_desc_ok) {
+      // VAR 1390594 = 79874 without any row max or offset (S from C = 0, p = exp2(s); 342018 keeps the
+      // first tile's max as the offset: +1 % in the forward for it, lse error up to ~2^-8 instead of
+      // ~2^-9), then the fixup pass (exact kernel, exits at once unless a block was flagged)
+      dilated_attn32_kernel<48, true, 4, 1390594><<<(unsigned)items, 256, 0, s>>>(a);
+      dilated_attn32_kernel<48, true, 4, 79874 + 524288><<<(unsigned)((items + kFixItems - 1) / kFixItems), 256, 0, s>>>(a);
+    }
+    else if (D == 48) dilated_attn32_kernel<48, true, 4, 2><<<(unsigned)items, 256, 0, s>>>(a);
+    else dilated_attn32_kernel<64, true, 4><<<(unsigned)items, 256, 0, s>>>(a);
   } else {
-    if (q_log2_prescaled) dilated_attn32_kernel<64, true, kModeGen><<<(unsigned)items, 256, 0, s>>>(a);
-    else dilated_attn32_kernel<64, false, kModeGen><<<(unsigned)items, 256, 0, s>>>(a);
+    if (D == 48) dilated_attn32_kernel<48, false, 4><<<(unsigned)items, 256, 0, s>>>(a);
+    else dilated_attn32_kernel<64, false, 4><<<(unsigned)items, 256, 0, s>>>(a);
   }
   return gp_check_launch("gp_dilated_attn_fwd");
 }
@@ -1410,8 +2364,8 @@ extern "C" int gp_dilated_attn_fwd_varlen(const void* plan_host, const void* pla
   a.ntab = h.ntab;
   a.d_H = make_div_magic((uint32_t)h.H);
   // the single-slide default's variant, so each packed slide's outputs equal its own launch's
-  dilated_attn32_kernel<48, true, kModeFast, true><<<(unsigned)h.total_items, 256, 0, gp_stream(stream)>>>(a);
-  dilated_attn32_kernel<48, true, kModeFix, true><<<(unsigned)((h.total_items + kFixItems - 1) / kFixItems), 256, 0, gp_stream(stream)>>>(a);
+  dilated_attn32_kernel<48, true, 4, 1390594, 2, true><<<(unsigned)h.total_items, 256, 0, gp_stream(stream)>>>(a);
+  dilated_attn32_kernel<48, true, 4, 79874 + 524288, 2, true><<<(unsigned)((h.total_items + kFixItems - 1) / kFixItems), 256, 0, gp_stream(stream)>>>(a);
   return gp_check_launch("gp_dilated_attn_fwd_varlen");
 }
 
@@ -1541,4 +2495,19 @@ extern "C" int gp_dilated_sparsify(const uint16_t* src, int64_t src_row_stride, 
   }
   return gp_dilated_sparsify_dests(src, src_row_stride, k_col, v_col, tok_lo, n_tok, L, H, D, seg_len, ratios,
                                    nbranch, dests, nd, stream);
+}
+
+// Diagnostics: the per-segment cycle sums of the last VAR & 32768 launches (see stamp_now).
+extern "C" int gp_debug_attn_stamps(int64_t* out8, int reset) {
+  GP_REQUIRE(out8 != nullptr, "gp_debug_attn_stamps: null output");
+  unsigned long long h[8];
+  hipError_t e = hipMemcpyFromSymbol(h, HIP_SYMBOL(g_attn_stamps), sizeof(h), 0, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return gp_set_error("gp_debug_attn_stamps: %s", hipGetErrorString(e)), (int)e;
+  for (int i = 0; i < 8; ++i) out8[i] = (int64_t)h[i];
+  if (reset) {
+    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_attn_stamps), z, sizeof(z), 0, hipMemcpyHostToDevice);
+    if (e != hipSuccess) return gp_set_error("gp_debug_attn_stamps: %s", hipGetErrorString(e)), (int)e;
+  }
+  return 0;
 }

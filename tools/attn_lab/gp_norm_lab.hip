@@ -149,6 +149,92 @@ GP_DEV float gelu_erf(float x) {
 }
 
 // ---------------------------------------------------------------------------------------
+// GELU + LN over a 3072/4096/6144-wide bf16 row: one 256-thread block per row, thread t owns
+// elements k*1024 + 4t + {0..3} (k < EPT/4: each wave-instruction covers 512 contiguous bytes);
+// mean and variance through a 4-wave LDS reduction.  Small register footprint keeps many rows
+// in flight (the erf polynomial is VALU-heavy).
+template <int EPT>
+__global__ __launch_bounds__(256) void gelu_ln_kernel(const uint16_t* h, const float* __restrict__ ln_w,
+                                                      const float* __restrict__ ln_b, float eps, uint16_t* out,
+                                                      int64_t rows, int cols) {
+  __shared__ float red[2][4];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int64_t row = blockIdx.x;
+  const uint16_t* src = h + row * cols;
+  float v[EPT];
+#pragma unroll
+  for (int k = 0; k < EPT / 4; ++k) load_bf16<4>(src + k * 1024 + 4 * t, v + 4 * k);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < EPT; ++i) {
+    v[i] = gelu_erf(v[i]);
+    s += v[i];
+  }
+  s = wave_sum(s);
+  if (lane == 0) red[0][w] = s;
+  __syncthreads();
+  const float mean = (red[0][0] + red[0][1] + red[0][2] + red[0][3]) / (float)cols;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < EPT; ++i) {
+    const float d = v[i] - mean;
+    q += d * d;
+  }
+  q = wave_sum(q);
+  if (lane == 0) red[1][w] = q;
+  __syncthreads();
+  const float rstd = rsqrtf((red[1][0] + red[1][1] + red[1][2] + red[1][3]) / (float)cols + eps);
+#pragma unroll
+  for (int k = 0; k < EPT / 4; ++k) {
+    float wv[4], bv[4];
+    load_f32<4>(ln_w + k * 1024 + 4 * t, wv);
+    load_f32<4>(ln_b + k * 1024 + 4 * t, bv);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[4 * k + i] = (v[4 * k + i] - mean) * rstd * wv[i] + bv[i];
+  }
+  uint16_t* dst = out + row * cols;
+#pragma unroll
+  for (int k = 0; k < EPT / 4; ++k) store_bf16<4>(dst + k * 1024 + 4 * t, v + 4 * k);
+}
+
+// GELU + LN, one 64-lane wave per row (no LDS, no barrier): lane owns elements
+// k*512 + 8*lane + {0..7}, k < EPL/8 (16-byte accesses, each wave-instruction one contiguous
+// 1 KiB span); LN weights are read per 8-element chunk in the epilogue (L1/L2 resident).
+template <int EPL>
+__global__ __launch_bounds__(256) void gelu_ln_wave_kernel(const uint16_t* h, const float* __restrict__ ln_w,
+                                                           const float* __restrict__ ln_b, float eps,
+                                                           uint16_t* out, int64_t rows) {
+  constexpr int C = 64 * EPL;
+  const int lane = threadIdx.x & 63;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += (int64_t)gridDim.x * 4) {
+    float v[EPL];
+    ld_x8_bf16<EPL>(h + row * C, lane, v);
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < EPL; ++i) {
+      v[i] = gelu_erf(v[i]);
+      s += v[i];
+    }
+    const float mean = wave_sum(s) / (float)C;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < EPL; ++i) {
+      const float d = v[i] - mean;
+      q += d * d;
+    }
+    const float rstd = rsqrtf(wave_sum(q) / (float)C + eps);
+#pragma unroll
+    for (int k = 0; k < EPL / 8; ++k) {
+      float wv[8], bv[8];
+      load_f32<8>(ln_w + k * 512 + 8 * lane, wv);
+      load_f32<8>(ln_b + k * 512 + 8 * lane, bv);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[8 * k + i] = (v[8 * k + i] - mean) * rstd * wv[i] + bv[i];
+    }
+    st_x8_bf16<EPL>(out + row * C, lane, v);
+  }
+}
+
 // GELU + LN v2, one wave per row, grid-stride over rows with the NEXT row's 16-byte loads
 // issued before the current row's math (memory-level parallelism at the occupancy the
 // registers allow).  The GELU outputs are rounded to bf16 in place -- as the reference's
@@ -344,17 +430,10 @@ __global__ __launch_bounds__(NW * 64) void gelu_ln_lut_kernel(const uint16_t* h,
   }
 }
 
-// the device a stream's work runs on (the null stream: the current device)
-static int stream_device(hipStream_t s) {
-  hipDevice_t dev = 0;
-  if (hipStreamGetDevice(s, &dev) != hipSuccess) return -1;
-  return (int)dev;
-}
-
-static int gp_num_cus(hipStream_t s) {       // per-device cache of the CU count (LUT kernel: one block per CU)
+static int gp_num_cus() {       // per-device cache of the CU count (LUT kernel: one block per CU)
   static int cache[64] = {0};
-  const int dev = stream_device(s);
-  if (dev < 0 || dev >= 64) return 256;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
   if (cache[dev] == 0) {
     int n = 0;
     if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
@@ -363,23 +442,20 @@ static int gp_num_cus(hipStream_t s) {       // per-device cache of the CU count
   return cache[dev];
 }
 
-// g_gelu_tab of the stream's device is filled (once: a fill launch on the caller's stream, then a
-// synchronize of that stream, so no other stream can see the flag before the table is complete).  The
-// flag is keyed by the device the stream runs on, not the current device.  While
+// g_gelu_tab of the current device is filled (once: a fill launch on the caller's stream, then a
+// synchronize of that stream, so no other stream can see the flag before the table is complete).  While
 // the stream is being captured into a graph the fill cannot be synchronised: the caller then takes the
 // self-filling kernel until an eager call has filled the table.  Two threads filling at once write the
 // same bytes.
 static bool gelu_tab_ready(hipStream_t s) {
   static std::atomic<bool> ready[64];
-  const int dev = stream_device(s);
-  if (dev < 0 || dev >= 64) return false;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
   if (ready[dev].load(std::memory_order_acquire)) return true;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
-  // a launch error here is reported by this call only (hipPeekAtLastError leaves earlier errors
-  // pending for the caller's own check)
   gelu_tab_fill_kernel<<<65536 / 8 / 256, 256, 0, s>>>();
-  if (hipPeekAtLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess) return false;
+  if (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess) return false;
   ready[dev].store(true, std::memory_order_release);
   return true;
 }
@@ -491,13 +567,15 @@ extern "C" int gp_gelu_layernorm(const uint16_t* h, const float* ln_w, const flo
   GP_REQUIRE(h && ln_w && ln_b && out, "gp_gelu_layernorm: null pointer");
   hipStream_t s = gp_stream(stream);
   GP_REQUIRE(rows < (int64_t)0x7fffffff, "gp_gelu_layernorm: too many rows");
-  if (cols == 3072 || cols == 4096) {
-    // GELU by lookup table (the table + LN weights fit in LDS): one block per CU, the table copied
-    // from g_gelu_tab, or evaluated per block while a graph capture runs before any eager call
+  const char* impl_env = getenv("GP_GELU_IMPL");    // A/B: 1 = block per row, 2 = wave per row (v1), 3 = v2, 5 = table
+  const int impl = impl_env ? atoi(impl_env) : ((cols == 3072 || cols == 4096) ? 5 : 3);
+  if (impl == 5 || impl == 4) {     // default where the table + LN weights fit in LDS: GELU by lookup table
+    GP_REQUIRE(cols == 3072 || cols == 4096, "gp_gelu_layernorm: GP_GELU_IMPL=4/5 needs cols 3072 or 4096");
     const int64_t want = (rows + 7) / 8;
-    const int cus = gp_num_cus(s);
+    const int cus = gp_num_cus();
     const unsigned nb = (unsigned)(want < cus ? want : cus);
-    const bool copy = gelu_tab_ready(s);
+    // GP_GELU_IMPL=4: the same kernel evaluating its table per block (A/B and bit-identity reference)
+    const bool copy = impl == 5 && gelu_tab_ready(s);
     if (cols == 3072) {
       if (copy) gelu_ln_lut_kernel<48, 8, true><<<nb, 512, 0, s>>>(h, ln_w, ln_b, eps, out, rows);
       else gelu_ln_lut_kernel<48><<<nb, 512, 0, s>>>(h, ln_w, ln_b, eps, out, rows);
@@ -505,11 +583,31 @@ extern "C" int gp_gelu_layernorm(const uint16_t* h, const float* ln_w, const flo
       if (copy) gelu_ln_lut_kernel<64, 8, true><<<nb, 512, 0, s>>>(h, ln_w, ln_b, eps, out, rows);
       else gelu_ln_lut_kernel<64><<<nb, 512, 0, s>>>(h, ln_w, ln_b, eps, out, rows);
     }
-  } else {
-    // v2 (F = 6144): wave per row, grid-stride with next-row prefetch, bf16-rounded GELU
+    return gp_check_launch("gp_gelu_layernorm");
+  }
+  if (impl == 3) {     // v2 (default for F = 6144): wave per row, grid-stride with next-row prefetch, bf16-rounded GELU
     const int64_t want = (rows + 3) / 4;
     const unsigned nb = (unsigned)(want < 1024 ? want : 1024);
-    gelu_ln_wave2_kernel<96><<<nb, 256, 0, s>>>(h, ln_w, ln_b, eps, out, rows);
+    switch (cols / 64) {
+      case 48: gelu_ln_wave2_kernel<48><<<nb, 256, 0, s>>>(h, ln_w, ln_b, eps, out, rows); break;
+      case 64: gelu_ln_wave2_kernel<64><<<nb, 256, 0, s>>>(h, ln_w, ln_b, eps, out, rows); break;
+      case 96: gelu_ln_wave2_kernel<96><<<nb, 256, 0, s>>>(h, ln_w, ln_b, eps, out, rows); break;
+    }
+    return gp_check_launch("gp_gelu_layernorm");
+  }
+  if (impl == 1) {
+    switch (cols / 256) {
+      case 12: gelu_ln_kernel<12><<<(unsigned)rows, 256, 0, s>>>(h, ln_w, ln_b, eps, out, rows, cols); break;
+      case 16: gelu_ln_kernel<16><<<(unsigned)rows, 256, 0, s>>>(h, ln_w, ln_b, eps, out, rows, cols); break;
+      case 24: gelu_ln_kernel<24><<<(unsigned)rows, 256, 0, s>>>(h, ln_w, ln_b, eps, out, rows, cols); break;
+    }
+  } else {
+    const unsigned nb = (unsigned)((rows + 3) / 4 < (1 << 20) ? (rows + 3) / 4 : (1 << 20));
+    switch (cols / 64) {
+      case 48: gelu_ln_wave_kernel<48><<<nb, 256, 0, s>>>(h, ln_w, ln_b, eps, out, rows); break;
+      case 64: gelu_ln_wave_kernel<64><<<nb, 256, 0, s>>>(h, ln_w, ln_b, eps, out, rows); break;
+      case 96: gelu_ln_wave_kernel<96><<<nb, 256, 0, s>>>(h, ln_w, ln_b, eps, out, rows); break;
+    }
   }
   return gp_check_launch("gp_gelu_layernorm");
 }

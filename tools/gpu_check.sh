@@ -6,7 +6,8 @@ TAG=${1:-run}; shift
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
+timeout -k 10 120 python tools/lab_check.py --out $OUT/lab_check.json > $OUT/lab_check.log 2>&1; echo "lab_check rc=$?"; tail -2 $OUT/lab_check.log
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 $OUT/pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python bench.py "$@" > $OUT/bench.json 2> $OUT/bench.err

@@ -13,6 +13,9 @@ import torch  # noqa: E402
 
 from gigapath import _hip  # noqa: E402
 
+# the run-time variant switches (GP_ATTN_IMPL / GP_ATTN_VAR / GP_GELU_IMPL) live in the lab build only
+_hip._lib = _hip.load_library(os.path.join(ROOT, "tools", "attn_lab", "liblab_r01.so"))
+
 ap = argparse.ArgumentParser()
 ap.add_argument("--rows", type=int, default=70001)
 ap.add_argument("--cols", type=int, default=3072)
