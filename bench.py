@@ -268,7 +268,7 @@ def main():
         total_tf = (runtime.gemm_flops(1, args.tiles, 768, 3072, 1536, 12)
                     + 12 * runtime.attention_valid_flops(L, segs, ratios, 16, 48)) / 1e12
     plain = not (sp or mixed)          # the PMC summary was collected on the plain C3 run
-    traffic = pmc_traffic(args.tiles, "dilated_attn32_kernel<48, true, 4") if plain else None
+    traffic = pmc_traffic(args.tiles, "dilated_attn32_kernel<48, true, 0,") if plain else None
     # HBM-bound merge kernel: algorithmic bytes per launch over its live launch time
     n_mg, ms_mg = kt.get("merge", (0, 0.0))
     if sp:

@@ -153,14 +153,24 @@ constexpr int kQT = 2;                       // 16-row q-tiles per wave
 constexpr int kQB = kWaves * kQT * 16;       // 128 query rows per workgroup
 constexpr int kKB = 64;                      // keys per K/V tile
 
-// Blocks b, b+8, b+16, ... share an XCD (round-robin dispatch).  Within each chunk of 64
-// blocks give the 8 blocks of one XCD 8 consecutive work items (same segment and head).
+// Blocks b, b+8, b+16, ... share an XCD (round-robin dispatch).  Within each chunk of 8*G blocks
+// give the blocks of one XCD G consecutive work items (q-blocks of one segment and head), so they
+// read the same K/V rows from that XCD's L2.  G is a compile-time tunable (tools/attn_lab).
+#ifndef GP_ATTN_XCDG
+#define GP_ATTN_XCDG 8
+#endif
+// GP_ATTN_WIDE_STORE: the epilogue pairs the two half-waves' 4-element groups with
+// v_permlane32_swap so every lane stores 16 contiguous bytes (3 stores instead of 6 per row)
+#ifndef GP_ATTN_WIDE_STORE
+#define GP_ATTN_WIDE_STORE 1
+#endif
 GP_DEV int64_t xcd_group(int64_t bid, int64_t nb) {
-  const int64_t full = nb & ~int64_t(63);
+  constexpr int64_t G = GP_ATTN_XCDG, C = 8 * G;
+  const int64_t full = nb - nb % C;
   if (bid >= full) return bid;
-  const int64_t base = bid & ~int64_t(63);
-  const int64_t in = bid & 63;
-  return base + (in & 7) * 8 + (in >> 3);
+  const int64_t base = bid - bid % C;
+  const int64_t in = bid % C;
+  return base + (in & 7) * G + (in >> 3);
 }
 
 template <int D>
@@ -412,12 +422,27 @@ constexpr uint32_t kLseRedo = 0x7fc0dead;
 enum AttnMode { kModeFast = 0, kModeFix = 1, kModeGen = 2 };
 constexpr int kFixItems = 32;
 
-template <int D, bool kPre, int MODE, bool kTab>
+// Waves per workgroup of the LDS-DMA kernels (each wave 32 queries; the K/V tile is shared by all):
+// a compile-time tunable (tools/attn_lab); the register-staged kernel always runs 4 waves.
+#ifndef GP_ATTN_NW
+#define GP_ATTN_NW 8
+#endif
+constexpr int kNWFast = GP_ATTN_NW;
+// GP_ATTN_PRIO: the second-dispatched half of the workgroup's waves (w >= NW/2, the arbitration
+// losers of each SIMD pair) runs at s_setprio 1 for the whole kernel (MI355X_MICROARCH.md §Two waves
+// per SIMD, item 4)
+#ifndef GP_ATTN_PRIO
+#define GP_ATTN_PRIO 1
+#endif
+static_assert(kNWFast == 4 || kNWFast == 8 || kNWFast == 16, "GP_ATTN_NW must be 4, 8 or 16");
+
+template <int D, bool kPre, int MODE, bool kTab, int NW>
 __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_idx) {
   static_assert(D == 48 || D == 64, "v2 kernel covers D = 48 and 64");
   static_assert(MODE == kModeGen || (D == 48 && kPre), "LDS-DMA modes need D = 48 and a pre-scaled q");
-  constexpr int NT = 256;                    // 4 waves
-  constexpr int QB = 128;                    // query rows per workgroup
+  static_assert(NW == 4 || ((NW == 8 || NW == 16) && MODE != kModeGen), "8 / 16 waves: LDS-DMA modes only");
+  constexpr int NT = NW * 64;
+  constexpr int QB = NW * 32;                // query rows per workgroup
   constexpr int KT = 64;                     // keys per staged tile
   constexpr int KS = D / 16;                 // k-steps of Q.K^T
   constexpr bool kOnes = (D % 32) != 0;      // spare d rows carry the row-sum ones
@@ -431,8 +456,8 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   constexpr int BUF = KTILE + VTILE;
   constexpr int CH = D / 8;                  // 16-byte chunks per K/V row in HBM
   constexpr int TOT = 2 * KT * CH;           // 16-byte chunks of one K tile + one V tile
-  constexpr int LPT = TOT / NT;
-  static_assert(TOT % NT == 0, "");
+  constexpr int LPT = (MODE == kModeGen) ? TOT / NT : 1;
+  static_assert(MODE != kModeGen || TOT % NT == 0, "");
   constexpr float kThr = 8.0f;               // lazy-rescale threshold (log2 units)
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
 
@@ -495,16 +520,17 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   const uint16_t* lsrc[LPT];
   int lrow[LPT], loff[LPT];
   uint4 stage[LPT];
-  // kDMA: piece p of the 15 (7 K + 8 V) goes to wave p % 4; lane-linear 16-B units.  K image:
+  // kDMA: piece p of the 15 (7 K + 8 V) goes to wave p % NW; lane-linear 16-B units.  K image:
   // 112-B rows = 6 chunks + 1 pad unit (pad lanes off); V image: 128-B rows, swizzled 32-B blocks
   // (the lanes of the bf16-ones block are off: the prologue wrote it)
   constexpr int kPieces = (KT * KROWB + KT * VROWB) / 1024;
-  int dvo[4];
+  constexpr int PPW = (kPieces + NW - 1) / NW;   // pieces per wave
+  int dvo[PPW];
   unsigned dmask = 0;
   if constexpr (kDMA) {
 #pragma unroll
-    for (int sl = 0; sl < 4; ++sl) {
-      const int pc = w + 4 * sl;
+    for (int sl = 0; sl < PPW; ++sl) {
+      const int pc = w + NW * sl;
       dvo[sl] = 0;
       if (pc >= kPieces) continue;
       if (pc < KTILE / 1024) {
@@ -538,8 +564,8 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
           (void*)((const char*)kbase + tb), (short)0, (int)(nrec < 0x7fffffff ? nrec : 0x7fffffff), 0x00020000);
       char* bufp = smem + ((kv0 / KT) & 1) * BUF;
 #pragma unroll
-      for (int sl = 0; sl < 4; ++sl) {
-        const int pc = w + 4 * sl;
+      for (int sl = 0; sl < PPW; ++sl) {
+        const int pc = w + NW * sl;
         if (pc < kPieces && ((dmask >> sl) & 1u))
           __builtin_amdgcn_raw_ptr_buffer_load_lds(
               rs, (__attribute__((address_space(3))) void*)(bufp + (pc < KTILE / 1024 ? pc * 1024 : KTILE + (pc - KTILE / 1024) * 1024)),
@@ -591,6 +617,9 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   // prefetch -- before the first MFMA of every tile
   __builtin_amdgcn_s_waitcnt(0x0f70);
 
+  if constexpr (GP_ATTN_PRIO != 0 && NW >= 8) {
+    if (__builtin_amdgcn_readfirstlane((int)threadIdx.x) >= NT / 2) __builtin_amdgcn_s_setprio(1);
+  }
   // one 64-key tile; SET = the tile's LDS buffer when the loop is unrolled by two (kDMA), so the
   // buffer offsets fold into the ds_read immediates
   auto tile_step = [&](int t, auto setc) {
@@ -796,7 +825,31 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   }
   const float inv = so / l;
   const int i = q0 + w * 32 + l32;
-  if (i < rows_needed) {
+  if constexpr (GP_ATTN_WIDE_STORE != 0) {
+    // lane (q, h) holds d = 8k + 4h .. +3 for the D/8 groups k.  For each pair of groups (k, k+1)
+    // one permlane32_swap per dword gives lanes 0-31 d = 8k .. 8k+7 and lanes 32-63 d = 8k+8 .. 8k+15
+    // (T21): one 16-byte store per pair.  The swap needs EXEC full: it runs before the row check.
+    uint2 pk[D / 8];
+#pragma unroll
+    for (int k = 0; k < D / 8; ++k) {
+      const int mt = k / 4, rg = k % 4;
+      pk[k].x = (uint32_t)f2bf(oacc[mt][4 * rg] * inv) | ((uint32_t)f2bf(oacc[mt][4 * rg + 1] * inv) << 16);
+      pk[k].y = (uint32_t)f2bf(oacc[mt][4 * rg + 2] * inv) | ((uint32_t)f2bf(oacc[mt][4 * rg + 3] * inv) << 16);
+    }
+#pragma unroll
+    for (int k = 0; k < D / 8; k += 2) {
+      const auto rx = __builtin_amdgcn_permlane32_swap(pk[k].x, pk[k + 1].x, false, false);
+      const auto ry = __builtin_amdgcn_permlane32_swap(pk[k].y, pk[k + 1].y, false, false);
+      pk[k].x = rx[0]; pk[k + 1].x = rx[1];
+      pk[k].y = ry[0]; pk[k + 1].y = ry[1];
+    }
+    if (i < rows_needed) {
+      uint16_t* orow = brr.o + (((int64_t)bn * g.m + i) * a.H + hh) * (int64_t)D + 8 * h;
+#pragma unroll
+      for (int k = 0; k < D / 8; k += 2)
+        *reinterpret_cast<uint4*>(orow + 8 * k) = make_uint4(pk[k].x, pk[k].y, pk[k + 1].x, pk[k + 1].y);
+    }
+  } else if (i < rows_needed) {
     uint16_t* orow = brr.o + (((int64_t)bn * g.m + i) * a.H + hh) * (int64_t)D;
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
@@ -809,6 +862,8 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
           store_bf16<4>(orow + d0, vv);
         }
       }
+  }
+  if (i < rows_needed) {
     float lse = (mr + __builtin_amdgcn_logf(l)) * 0.69314718055994530942f;
     if constexpr (kZM) {     // overflowed / out of range: flag the row for the fixup pass
       if ((__float_as_uint(l) & 0x7f800000u) == 0x7f800000u || !(l > 0.f) || zm_bad) lse = __uint_as_float(kLseRedo);
@@ -821,10 +876,10 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
 // consecutive items per block: the block reads the lse of every needed row of all of them at once
 // (wave w: items 8w .. 8w + 7; 16 independent loads per lane) and exits unless some row holds the
 // kLseRedo marker, so the pass costs about one load latency per 32 items when nothing overflowed.
-template <int D, bool kPre, int MODE, bool kTab = false>
-__global__ __launch_bounds__(256, 2) void dilated_attn32_kernel(const AttnArgs a) {
+template <int D, bool kPre, int MODE, bool kTab = false, int NW = 4>
+__global__ __launch_bounds__(NW * 64, 2) void dilated_attn32_kernel(const AttnArgs a) {
   if constexpr (MODE == kModeFix) {
-    constexpr int NW = 4, QB = 128;
+    constexpr int QB = NW * 32;
     const int it0 = (int)blockIdx.x * kFixItems;
     // wave index made provably uniform: the item decode then runs on the scalar unit (s_load from
     // the kernel arguments), not as a chain of dependent per-lane global loads
@@ -858,9 +913,9 @@ __global__ __launch_bounds__(256, 2) void dilated_attn32_kernel(const AttnArgs a
 #pragma unroll
     for (int n = 0; n < NV; ++n) flagged |= use[n] && vals[n] == kLseRedo;
     if (!__syncthreads_or(flagged)) return;
-    for (int k = 0; k < kFixItems && it0 + k < a.total_items; ++k) attn32_item<D, kPre, MODE, kTab>(a, it0 + k);
+    for (int k = 0; k < kFixItems && it0 + k < a.total_items; ++k) attn32_item<D, kPre, MODE, kTab, NW>(a, it0 + k);
   } else {
-    attn32_item<D, kPre, MODE, kTab>(a, (int)xcd_group(blockIdx.x, gridDim.x));
+    attn32_item<D, kPre, MODE, kTab, NW>(a, (int)xcd_group(blockIdx.x, gridDim.x));
   }
 }
 // ---------------------------------------------------------------------------------------
@@ -1098,7 +1153,8 @@ extern "C" int gp_dilated_attn_fwd_ex(const uint16_t* q, int64_t q_row_stride, i
     const int64_t rs2 = 2 * d.kv_row_stride;
     kv_desc_ok = kv_desc_ok && dv >= 0 && rs2 >= dv + 2 * D && dv + 64 * (int64_t)d.ratio * rs2 < 0x7fffffff;
   }
-  const int qblk = 128;   // query rows per workgroup
+  const bool fast = D == 48 && q_log2_prescaled && kv_desc_ok;   // the LDS-DMA no-max kernel + fixup pass
+  const int qblk = fast ? 32 * kNWFast : 128;   // query rows per workgroup
   // order branches by keys per work item (descending) so the longest items start first
   int order[GP_MAX_BRANCHES];
   GpBranch geo[GP_MAX_BRANCHES];
@@ -1162,10 +1218,11 @@ extern "C" int gp_dilated_attn_fwd_ex(const uint16_t* q, int64_t q_row_stride, i
   hipStream_t s = gp_stream(stream);
   if (D == 96) {
     dilated_attn_kernel<96><<<(unsigned)items, 256, 0, s>>>(a);
-  } else if (D == 48 && q_log2_prescaled && kv_desc_ok) {
+  } else if (fast) {
     // the product launch: no-max kernel, then the fixup pass (exits at once unless a row was flagged)
-    dilated_attn32_kernel<48, true, kModeFast><<<(unsigned)items, 256, 0, s>>>(a);
-    dilated_attn32_kernel<48, true, kModeFix><<<(unsigned)((items + kFixItems - 1) / kFixItems), 256, 0, s>>>(a);
+    dilated_attn32_kernel<48, true, kModeFast, false, kNWFast><<<(unsigned)items, 64 * kNWFast, 0, s>>>(a);
+    dilated_attn32_kernel<48, true, kModeFix, false, kNWFast>
+        <<<(unsigned)((items + kFixItems - 1) / kFixItems), 64 * kNWFast, 0, s>>>(a);
   } else if (D == 48) {
     if (q_log2_prescaled) dilated_attn32_kernel<48, true, kModeGen><<<(unsigned)items, 256, 0, s>>>(a);
     else dilated_attn32_kernel<48, false, kModeGen><<<(unsigned)items, 256, 0, s>>>(a);
@@ -1306,7 +1363,7 @@ extern "C" int gp_varlen_plan(const int64_t* L, int nslide, int H, int D, const 
     T += L[i];
   }
   GP_REQUIRE(T < (int64_t)0x7fffffff, "gp_varlen_plan: %lld packed tokens is too many", (long long)T);
-  const int qblk = 128;                            // query rows per work item (v2 kernel)
+  const int qblk = 32 * kNWFast;                   // query rows per work item (the LDS-DMA kernel)
   for (int b = 0; b < nbranch; ++b) { o_elems[b] = 0; lse_elems[b] = 0; }
   // per (slide, branch) output region offsets, in slide order
   std::vector<int64_t> ooff((size_t)nslide * nbranch), loff((size_t)nslide * nbranch);
@@ -1410,8 +1467,9 @@ extern "C" int gp_dilated_attn_fwd_varlen(const void* plan_host, const void* pla
   a.ntab = h.ntab;
   a.d_H = make_div_magic((uint32_t)h.H);
   // the single-slide default's variant, so each packed slide's outputs equal its own launch's
-  dilated_attn32_kernel<48, true, kModeFast, true><<<(unsigned)h.total_items, 256, 0, gp_stream(stream)>>>(a);
-  dilated_attn32_kernel<48, true, kModeFix, true><<<(unsigned)((h.total_items + kFixItems - 1) / kFixItems), 256, 0, gp_stream(stream)>>>(a);
+  dilated_attn32_kernel<48, true, kModeFast, true, kNWFast><<<(unsigned)h.total_items, 64 * kNWFast, 0, gp_stream(stream)>>>(a);
+  dilated_attn32_kernel<48, true, kModeFix, true, kNWFast>
+      <<<(unsigned)((h.total_items + kFixItems - 1) / kFixItems), 64 * kNWFast, 0, gp_stream(stream)>>>(a);
   return gp_check_launch("gp_dilated_attn_fwd_varlen");
 }
 
