@@ -434,9 +434,6 @@ constexpr int kNWFast = GP_ATTN_NW;
 #ifndef GP_ATTN_PRIO
 #define GP_ATTN_PRIO 1
 #endif
-#ifndef GP_ATTN_STAGGER
-#define GP_ATTN_STAGGER 0
-#endif
 static_assert(kNWFast == 4 || kNWFast == 8 || kNWFast == 16, "GP_ATTN_NW must be 4, 8 or 16");
 
 template <int D, bool kPre, int MODE, bool kTab, int NW>
@@ -462,11 +459,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   constexpr int LPT = (MODE == kModeGen) ? TOT / NT : 1;
   static_assert(MODE != kModeGen || TOT % NT == 0, "");
   constexpr float kThr = 8.0f;               // lazy-rescale threshold (log2 units)
-  // kStag (GP_ATTN_STAGGER, fast mode, 8+ waves): the second half of the waves runs half a tile
-  // behind the first (its softmax + P.V of tile t-1 beside the first half's S of tile t, MI355X_MICROARCH.md
-  // §Two waves per SIMD item 9); a K/V tile then stays live one barrier longer: a 3-buffer ring
-  constexpr bool kStag = GP_ATTN_STAGGER != 0 && MODE == kModeFast && NW >= 8;
-  constexpr int NBUF = kStag ? 3 : 2;
+  constexpr int NBUF = 2;                    // double-buffered K/V tiles
   __shared__ __attribute__((aligned(16))) char smem[NBUF * BUF];
 
   // ---- work item (32-bit index math: items < 2^31, checked on the host)
@@ -797,92 +790,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
     if constexpr (kDMA) __builtin_amdgcn_s_waitcnt(0x0f70);   // this wave's DMA pieces landed
     __syncthreads();
   };
-  if constexpr (kStag) {
-    // fast mode only: S from C = 0, p = exp2(s), no running max (see tile_step)
-    auto s_tile = [&](int t, const char* Kb, f32x16 (&sacc)[2]) {
-      const int kv0 = t * KT;
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        f32x16 acc;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-          const bf16x8 kk = *reinterpret_cast<const bf16x8*>(Kb + (32 * u + l32) * KROWB + 32 * ks + 16 * h);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kk, qf[ks], acc, 0, 0, 0);
-        }
-        sacc[u] = acc;
-      }
-      if (kv0 + 64 > c) {
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            if (kv0 + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * h >= c) sacc[u][r] = -INFINITY;
-      }
-    };
-    auto pv_tile = [&](const f32x16 (&sacc)[2], const char* Vb) {
-      bf16x8 pf[2][2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) pf[u][s2][e] = (__bf16)fast_exp2(sacc[u][8 * s2 + e]);
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const int row = 32 * u + 16 * s2 + 4 * (lane >> 5) + ((lane >> 2) & 3);
-#pragma unroll
-          for (int mt = 0; mt < 2; ++mt) {
-            const int blk = 2 * mt + ((lane >> 4) & 1);
-            const char* p0 = Vb + row * VROWB + 32 * (blk ^ (row & 3)) + 8 * (lane & 3);
-            const char* p1 = p0 + 8 * VROWB;
-            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
-            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p1);
-            const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-            oacc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[u][s2], oacc[mt], 0, 0, 0);
-          }
-        }
-    };
-    // one barrier per tile in both halves: tile t + 1's DMA is issued after barrier t - 1 into the
-    // buffer tile t - 2 used (its last reader, the second half's P.V, ran before barrier t - 1) and
-    // waited for before barrier t
-    auto step_a = [&](int t, auto setc) {
-      constexpr int SET = decltype(setc)::value;
-      if (t + 1 < ntiles) load_tile((t + 1) * KT);
-      f32x16 sacc[2];
-      s_tile(t, smem + SET * BUF, sacc);
-      pv_tile(sacc, smem + SET * BUF + KTILE);
-      __builtin_amdgcn_s_waitcnt(0x0f70);
-      __syncthreads();
-    };
-    f32x16 sv[2];
-    auto step_b = [&](int t, auto setc) {
-      constexpr int SET = decltype(setc)::value;
-      if (t + 1 < ntiles) load_tile((t + 1) * KT);
-      if (t > 0) pv_tile(sv, smem + ((SET + NBUF - 1) % NBUF) * BUF + KTILE);
-      __builtin_amdgcn_sched_barrier(0);    // no interleave: the half keeps the first half's register budget
-      s_tile(t, smem + SET * BUF, sv);
-      __builtin_amdgcn_s_waitcnt(0x0f70);
-      __syncthreads();
-    };
-    if (__builtin_amdgcn_readfirstlane((int)threadIdx.x) < NT / 2) {
-      for (int t = 0; t < ntiles; t += 3) {
-        step_a(t, std::integral_constant<int, 0>());
-        if (t + 1 < ntiles) step_a(t + 1, std::integral_constant<int, 1>());
-        if (t + 2 < ntiles) step_a(t + 2, std::integral_constant<int, 2>());
-      }
-    } else {
-      for (int t = 0; t < ntiles; t += 3) {
-        step_b(t, std::integral_constant<int, 0>());
-        if (t + 1 < ntiles) step_b(t + 1, std::integral_constant<int, 1>());
-        if (t + 2 < ntiles) step_b(t + 2, std::integral_constant<int, 2>());
-      }
-      if (ntiles > 0) pv_tile(sv, smem + ((ntiles - 1) % NBUF) * BUF + KTILE);
-    }
-  } else if constexpr (kDMA) {
+  if constexpr (kDMA) {
     for (int t = 0; t < ntiles; t += 2) {
       tile_step(t, std::integral_constant<int, 0>());
       if (t + 1 < ntiles) tile_step(t + 1, std::integral_constant<int, 1>());
