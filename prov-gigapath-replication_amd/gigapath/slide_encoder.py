@@ -16,6 +16,7 @@ factor (see pos_embed.py); ``model.pos_embed`` is still available, built lazily 
 from __future__ import annotations
 
 import os
+from collections import OrderedDict
 from functools import partial
 from typing import Dict, List
 
@@ -85,11 +86,19 @@ class LongNetViT(nn.Module):
         self._top = None
         self._pos_full = None
         self._sp = None
-        # HIP graphs: the whole single-device forward as one replay per input shape
+        # HIP graphs: the whole single-device forward as one replay per input shape.  A graph keeps
+        # its shape's workspace alive (~2 GB at 100k tiles, ~5 GB at 256k), so the cache is an LRU
+        # bounded by entries AND bytes; a shape is captured only once it has been seen
+        # graph_min_uses times (real slide sizes rarely repeat: a one-off slide runs eagerly instead of
+        # paying an eager warm-up + capture it never replays); graphs of superseded weights are dropped
         self.use_hip_graphs = False
-        self.max_hip_graphs = 64
-        self._graphs = {}
+        self.max_hip_graphs = 16
+        self.hip_graph_max_bytes = 48 << 30
+        self.graph_min_uses = 2
+        self._graphs = OrderedDict()
         self._graph_ws = {}
+        self._graph_bytes = {}
+        self._graph_seen = {}
         self._capture_streams = {}
         self.initialize_vit_weights()
 
@@ -195,7 +204,10 @@ class LongNetViT(nn.Module):
         c = coords if coords.dtype in (torch.float32, torch.float64) else coords.float()
         if self.validate_positions:
             self.check_positions([c])
-        graph, sx, sc, outs = self.graph_entry(x, c, all_layer_embed)
+        ent = self.graph_entry(x, c, all_layer_embed)
+        if ent is None:                          # shape not (yet) worth a capture
+            return self._forward_device(x, coords, all_layer_embed, False)
+        graph, sx, sc, outs = ent
         sx.copy_(x)
         sc.copy_(c)
         graph.replay()
@@ -222,24 +234,60 @@ class LongNetViT(nn.Module):
 
     def graph_entry(self, x, c, all_layer_embed):
         """(graph, static x, static coords, static outputs) for this input shape, captured if not
-        cached.  No validation, no replay."""
+        cached and seen graph_min_uses times; None while the shape should run eagerly.  No
+        validation, no replay."""
         dev = self.cls_token.device
         self._packed_top(dev)
         self.encoder.engine.pack(self.encoder, dev)
         key = (str(dev), tuple(x.shape), x.dtype, c.dtype, bool(all_layer_embed), bool(self.global_pool),
                self._top_sig, self.encoder.engine._sig)
-        ent = self._graphs.get(key)
-        if ent is None:
-            ent = self._capture(key, x, c, lambda sx, sc: self._forward_device(sx, sc, all_layer_embed, False))
+        ent = self._graph_lookup(key)
+        if ent is None and self._graph_wanted(key):
+            ent = self._capture(key, x, c, lambda sx, sc: self._forward_device(sx, sc, all_layer_embed, False),
+                                lambda: self.encoder.engine.ws)
         return ent
 
-    def _capture(self, key, x, c, run):
+    def _graph_lookup(self, key):
+        ent = self._graphs.get(key)
+        if ent is not None:
+            self._graphs.move_to_end(key)       # LRU
+        return ent
+
+    def _graph_wanted(self, key) -> bool:
+        """Count a miss; True once the shape has been seen graph_min_uses times."""
+        if len(self._graph_seen) > 4096:
+            self._graph_seen.clear()
+        n = self._graph_seen.get(key, 0) + 1
+        self._graph_seen[key] = n
+        return n >= self.graph_min_uses
+
+    def _drop_graph(self, key):
+        self._graphs.pop(key, None)
+        self._graph_ws.pop(key, None)
+        self._graph_bytes.pop(key, None)
+
+    @staticmethod
+    def _tensor_bytes(obj, seen=None) -> int:
+        """Device bytes held by the tensors of a workspace object (recursing into lists / scratch)."""
+        seen = set() if seen is None else seen
+        tot = 0
+        items = obj.__dict__.values() if hasattr(obj, "__dict__") else obj
+        for v in items:
+            if isinstance(v, torch.Tensor):
+                if v.is_cuda and v.data_ptr() not in seen:
+                    seen.add(v.data_ptr())
+                    tot += v.untyped_storage().nbytes()
+            elif isinstance(v, (list, tuple)) or hasattr(v, "outs"):
+                tot += LongNetViT._tensor_bytes(v, seen)
+        return tot
+
+    def _capture(self, key, x, c, run, workspace):
         """Capture run(static_x, static_coords) -> outputs on the side stream (after one eager
-        warm-up run there: allocations, TunableOp lookups) and cache it under `key`."""
-        while len(self._graphs) >= self.max_hip_graphs:          # oldest first (insertion order)
-            old = next(iter(self._graphs))
-            self._graphs.pop(old)
-            self._graph_ws.pop(old, None)
+        warm-up run there: allocations, TunableOp lookups) and cache it under `key`, keeping the
+        workspace the graph bakes in (workspace() after the warm-up) alive with it."""
+        sig = key[-2:]                                             # (top, encoder) weight signatures
+        for old in [k for k in self._graphs if k[-2:] != sig]:    # superseded weights never replay
+            self._drop_graph(old)
         stream = self.graph_stream()
         # the static input is kept in bf16 (the forward's first use converts to bf16 anyway): the
         # per-replay sx.copy_(x) then converts while copying, instead of a full-precision copy plus
@@ -253,10 +301,17 @@ class LongNetViT(nn.Module):
         with torch.cuda.graph(graph, stream=stream, capture_error_mode="thread_local"):
             outs = run(sx, sc)
         cur.wait_stream(stream)
-        # the graph bakes this shape's workspace(s): keep them alive with the graph
+        # the graph bakes this shape's workspace: keep it alive with the graph; evict least recently
+        # used graphs beyond the entry and byte budgets
+        ws = workspace()
+        nbytes = self._tensor_bytes(ws) + sx.untyped_storage().nbytes() + sc.untyped_storage().nbytes()
+        while self._graphs and (len(self._graphs) >= self.max_hip_graphs or
+                                sum(self._graph_bytes.values()) + nbytes > self.hip_graph_max_bytes):
+            self._drop_graph(next(iter(self._graphs)))
         ent = (graph, sx, sc, outs)
         self._graphs[key] = ent
-        self._graph_ws[key] = (self.encoder.engine.ws, self.encoder.engine.pws)
+        self._graph_ws[key] = ws
+        self._graph_bytes[key] = nbytes
         return ent
 
     # ---------------------------------------------------------------- varlen packing (C5)
@@ -301,15 +356,19 @@ class LongNetViT(nn.Module):
             self.encoder.engine.pack(self.encoder, dev)
             key = ("packed", str(dev), Ns, x_cat.dtype, c_cat.dtype, bool(all_layer_embed), bool(self.global_pool),
                    self._top_sig, self.encoder.engine._sig)
-            ent = self._graphs.get(key)
-            if ent is None:
+            ent = self._graph_lookup(key)
+            if ent is None and self._graph_wanted(key):
                 ent = self._capture(key, x_cat, c_cat,
-                                    lambda sx, sc: self._forward_packed_device(sx, sc, Ns, all_layer_embed))
-            graph, sx, sc, res = ent
-            sx.copy_(x_cat)
-            sc.copy_(c_cat)
-            graph.replay()
-            res = res.clone()
+                                    lambda sx, sc: self._forward_packed_device(sx, sc, Ns, all_layer_embed),
+                                    lambda: self.encoder.engine.pws)
+            if ent is None:
+                res = self._forward_packed_device(x_cat, c_cat, Ns, all_layer_embed)
+            else:
+                graph, sx, sc, res = ent
+                sx.copy_(x_cat)
+                sc.copy_(c_cat)
+                graph.replay()
+                res = res.clone()
         else:
             res = self._forward_packed_device(x_cat, c_cat, Ns, all_layer_embed)
         out_dtype = self.norm.weight.dtype

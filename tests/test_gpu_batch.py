@@ -70,6 +70,7 @@ def test_mixed_batch_graph_replays_bit_exact():
     with torch.no_grad():
         ref = [torch.stack(model(x[None], c[None], all_layer_embed=True)) for x, c in slides]
     model.use_hip_graphs = True
+    model.graph_min_uses = 1
     for _ in range(2):                                    # capture pass, then pure replays
         out = batch.encode_slides(model, slides, all_layer_embed=True, packed=False)
         torch.cuda.synchronize()

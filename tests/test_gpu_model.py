@@ -67,12 +67,15 @@ def test_c2_16k_end_to_end_vs_reference_golden(model, golden_meta):
         allv = torch.stack(model(xt, ct, all_layer_embed=True)).cpu().numpy()
         last = model(xt, ct)[0].cpu().numpy()
         model.use_hip_graphs = True
+        model.graph_min_uses = 1
         try:
             rep = torch.stack(model(xt, ct, all_layer_embed=True)).cpu().numpy()
+            assert len(model._graphs) == 1
         finally:
             model.use_hip_graphs = False
-            model._graphs.clear()
-            model._graph_ws.clear()
+            model.graph_min_uses = 2
+            for k in list(model._graphs):
+                model._drop_graph(k)
     assert np.array_equal(rep, allv)
     for name, got in (("all_layer", allv), ("last", last)):
         ref = g[name]
@@ -213,7 +216,9 @@ def test_full_size_70k_one_layer_vs_oracle(model):
 
 def test_hip_graph_replay_matches_eager(model):
     """use_hip_graphs: one graph replay per input shape, bit-identical to the eager launches,
-    across shape changes (each graph keeps its own workspace) and weight updates (re-capture)."""
+    across shape changes (each graph keeps its own workspace) and weight updates (re-capture,
+    graphs of the old weights dropped); with the default graph_min_uses = 2 a shape seen once runs
+    eagerly; the LRU byte budget evicts."""
     shapes = [1500, 700, 1500]
     x = {n: orc.synthetic_slide(n, seed_x=n) for n in set(shapes)}
     with torch.no_grad():
@@ -221,11 +226,18 @@ def test_hip_graph_replay_matches_eager(model):
                                       all_layer_embed=True)) for n in set(shapes)}
         model.use_hip_graphs = True
         try:
+            n0 = shapes[0]
+            got = torch.stack(model(torch.from_numpy(x[n0][0]).to(DEV), torch.from_numpy(x[n0][1]).to(DEV),
+                                    all_layer_embed=True))
+            assert torch.equal(got, eager[n0]) and len(model._graphs) == 0     # first sighting: eager
+            model._graph_seen.clear()
+            model.graph_min_uses = 1
             for n in shapes:
                 xt, ct = torch.from_numpy(x[n][0]).to(DEV), torch.from_numpy(x[n][1]).to(DEV)
                 got = torch.stack(model(xt, ct, all_layer_embed=True))
                 assert torch.equal(got, eager[n]), n
             assert len(model._graphs) == 2
+            assert all(b > 0 for b in model._graph_bytes.values())
             # a weight update changes the packed-weight signature -> new capture, new result
             w = model.encoder.layers[3].ffn.fc2.weight
             saved = w.detach().clone()
@@ -234,18 +246,27 @@ def test_hip_graph_replay_matches_eager(model):
             got = torch.stack(model(torch.from_numpy(x[n][0]).to(DEV), torch.from_numpy(x[n][1]).to(DEV),
                                     all_layer_embed=True))
             assert not torch.equal(got, eager[n])
+            assert len(model._graphs) == 1              # the old weights' graphs were dropped
             w.copy_(saved)
             got = torch.stack(model(torch.from_numpy(x[n][0]).to(DEV), torch.from_numpy(x[n][1]).to(DEV),
                                     all_layer_embed=True))
             assert torch.equal(got, eager[n])
+            # byte budget: room for one graph only -> the least recently used one is evicted
+            model.hip_graph_max_bytes = max(model._graph_bytes.values()) + 1
+            for m in (700, 1500):
+                got = torch.stack(model(torch.from_numpy(x[m][0]).to(DEV), torch.from_numpy(x[m][1]).to(DEV),
+                                        all_layer_embed=True))
+                assert torch.equal(got, eager[m]) and len(model._graphs) == 1
             with pytest.raises(IndexError):
                 bad = torch.from_numpy(x[n][1]).to(DEV).clone()
                 bad[0, 0, 0] = 256.0 * 1000
                 model(torch.from_numpy(x[n][0]).to(DEV), bad)
         finally:
             model.use_hip_graphs = False
-            model._graphs.clear()
-            model._graph_ws.clear()
+            model.graph_min_uses = 2
+            model.hip_graph_max_bytes = 48 << 30
+            for k in list(model._graphs):
+                model._drop_graph(k)
 
 
 @pytest.mark.parametrize("arch", ["gigapath_slide_enc24l1024d", "gigapath_slide_enc12l1536d"])
