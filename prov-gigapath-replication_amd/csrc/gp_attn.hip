@@ -30,9 +30,12 @@ namespace {
 
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
-// Exact unsigned division by a launch constant d < 2^31 via a multiply-high (the libdivide
-// "branchfree" form): the merge kernel's per-token divisions are wave-uniform, so they run on the
-// scalar unit instead of ~25 VALU instructions each.
+// Exact unsigned division by a launch constant d < 2^31 via a multiply-high: the merge kernel's
+// per-token divisions are wave-uniform, so they run on the scalar unit instead of ~25 VALU
+// instructions each.  With m = floor(2^32 (2^l - d) / d) + 1, l = ceil(log2 d), the quotient is
+// (mulhi(n, m) + n) >> l for every n < 2^31 (mulhi(n, m) < n, so the sum cannot wrap); d == 1 is
+// m = 0, l = 0 -- no branch, so a chain of divisions does not split the scalar argument loads
+// into one wait per division.
 struct DivMagic {
   uint32_t m;
   int32_t l;     // 0: d == 1
@@ -46,10 +49,8 @@ inline DivMagic make_div_magic(uint32_t d) {
   r.l = l;
   return r;
 }
-GP_DEV uint32_t div_magic(uint32_t n, DivMagic mg) {
-  if (mg.l == 0) return n;
-  const uint32_t t = __umulhi(n, mg.m);
-  return (t + ((n - t) >> 1)) >> (mg.l - 1);
+GP_DEV uint32_t div_magic(uint32_t n, DivMagic mg) {   // n < 2^31
+  return (__umulhi(n, mg.m) + n) >> mg.l;
 }
 
 
@@ -985,7 +986,6 @@ __global__ __launch_bounds__(256) void branch_merge_kernel(const MergeArgs a) {
   const int nt = (int)a.ntok;
   const int E = 64 * EPL;
   const int col0 = lane * EPL;
-  const int hh = col0 / D;                       // compile-time divisor
   int pn[GP_MAX_BRANCHES], pt[GP_MAX_BRANCHES], pi[GP_MAX_BRANCHES], pj[GP_MAX_BRANCHES];
   int bidx = 0, p = 0;
   for (int k = 0; k < kTPW; ++k) {
@@ -1018,7 +1018,10 @@ __global__ __launch_bounds__(256) void branch_merge_kernel(const MergeArgs a) {
           else if (++pj[b] == g.r) { pj[b] = 0; ++pi[b]; }
         }
     }
-    // issue every load first (the o rows do not depend on the weights), then the math
+    // Every branch's loads are issued before any wait, with no exec-mask region around them: a
+    // lane outside the branch's head group reads the group's first lane's o / lse (the same
+    // cache lines, no extra traffic) and its weight is forced to zero below.  (Loads guarded by
+    // `if (covered)` compiled to one wait per branch -- five serial memory latencies per token.)
     float lse[GP_MAX_BRANCHES];
     bool cov[GP_MAX_BRANCHES];
     uint2 ob[GP_MAX_BRANCHES][EPL / 4];
@@ -1027,23 +1030,28 @@ __global__ __launch_bounds__(256) void branch_merge_kernel(const MergeArgs a) {
       lse[b] = -1e8f;
       cov[b] = false;
       if (b < nbr) {
-        const GpBranch& g = (kTab ? tb[b] : a.br[b]).g;
-        const int lph = g.hpg * (D / EPL);        // lanes per head group
-        cov[b] = lane >= pj[b] * lph && lane < (pj[b] + 1) * lph;
-        if (cov[b]) {
-          lse[b] = (kTab ? tb[b] : a.br[b]).lse[((int64_t)(bidx * g.nseg + pn[b]) * a.H + hh) * g.m + pi[b]];
-          const uint2* src = reinterpret_cast<const uint2*>(
-              (kTab ? tb[b] : a.br[b]).o + ((int64_t)(bidx * g.nseg + pn[b]) * g.m + pi[b]) * E + col0);
+        const MergeBranch& mb = kTab ? tb[b] : a.br[b];
+        const int lph = mb.g.hpg * (D / EPL);     // lanes per head group
+        const int l0 = pj[b] * lph;
+        cov[b] = lane >= l0 && lane < l0 + lph;
+        const int ln = cov[b] ? lane : l0;
+        const int64_t rb = (int64_t)(bidx * mb.g.nseg + pn[b]);
+        lse[b] = mb.lse[(rb * a.H + ln * EPL / D) * mb.g.m + pi[b]];
+        const uint2* src = reinterpret_cast<const uint2*>(mb.o + (rb * mb.g.m + pi[b]) * E + ln * EPL);
 #pragma unroll
-          for (int q = 0; q < EPL / 4; ++q) ob[b][q] = src[q];
-        }
+        for (int q = 0; q < EPL / 4; ++q) ob[b][q] = src[q];
       }
+    }
+    float wv[EPL], bv[EPL];
+    if (a.ln_w != nullptr) {   // LN affine via L1, in flight with the o rows (-5 % vs loading after the sums)
+      load_f32<EPL>(a.ln_w + col0, wv);
+      load_f32<EPL>(a.ln_b + col0, bv);
     }
     float mx = -INFINITY;
 #pragma unroll
     for (int b = 0; b < NBR; ++b)
       if (b < nbr) {
-        if (cov[b] && lse[b] == 0.f) lse[b] = -1e8f;   // dilated_attention.py:46
+        if (!cov[b] || lse[b] == 0.f) lse[b] = -1e8f;   // dilated_attention.py:46
         mx = fmaxf(mx, lse[b]);
       }
     float wsum = 0.f;
@@ -1061,18 +1069,19 @@ __global__ __launch_bounds__(256) void branch_merge_kernel(const MergeArgs a) {
     for (int e = 0; e < EPL; ++e) acc[e] = 0.f;
 #pragma unroll
     for (int b = 0; b < NBR; ++b) {
-      if (b < nbr && cov[b]) {
-        const float wb = lse[b] * inv;
+      if (b < nbr) {
+        const float wb = cov[b] ? lse[b] * inv : 0.f;   // + 0 * finite leaves acc unchanged
 #pragma unroll
         for (int q = 0; q < EPL / 4; ++q) {
-          acc[4 * q + 0] += __uint_as_float(ob[b][q].x << 16) * wb;
-          acc[4 * q + 1] += __uint_as_float(ob[b][q].x & 0xffff0000u) * wb;
-          acc[4 * q + 2] += __uint_as_float(ob[b][q].y << 16) * wb;
-          acc[4 * q + 3] += __uint_as_float(ob[b][q].y & 0xffff0000u) * wb;
+          // explicit fma: every instantiation (and the varlen path) rounds identically
+          acc[4 * q + 0] = __builtin_fmaf(__uint_as_float(ob[b][q].x << 16), wb, acc[4 * q + 0]);
+          acc[4 * q + 1] = __builtin_fmaf(__uint_as_float(ob[b][q].x & 0xffff0000u), wb, acc[4 * q + 1]);
+          acc[4 * q + 2] = __builtin_fmaf(__uint_as_float(ob[b][q].y << 16), wb, acc[4 * q + 2]);
+          acc[4 * q + 3] = __builtin_fmaf(__uint_as_float(ob[b][q].y & 0xffff0000u), wb, acc[4 * q + 3]);
         }
       }
     }
-    if (a.ln_w != nullptr) wave_layernorm<EPL>(acc, E, a.ln_w, a.ln_b, a.eps, col0);   // weights via L1
+    if (a.ln_w != nullptr) wave_layernorm_regs<EPL>(acc, E, wv, bv, a.eps);
     store_bf16<EPL>(a.out + (int64_t)row * E + col0, acc);
   }
 }

@@ -154,28 +154,6 @@ GP_DEV void wave_layernorm_regs(float* v, int cols, const float* w, const float*
   for (int i = 0; i < EPL; ++i) v[i] = (v[i] - mean) * rstd * w[i] + b[i];
 }
 
-// LayerNorm of one row held as EPL values per lane across a 64-lane wave (torch semantics:
-// biased variance, y = (x - mean) / sqrt(var + eps) * w + b), fp32 throughout.
-template <int EPL>
-GP_DEV void wave_layernorm(float* v, int cols, const float* w, const float* b, float eps, int col0) {
-  float s = 0.f;
-#pragma unroll
-  for (int i = 0; i < EPL; ++i) s += v[i];
-  const float mean = wave_sum(s) / (float)cols;
-  float q = 0.f;
-#pragma unroll
-  for (int i = 0; i < EPL; ++i) {
-    const float d = v[i] - mean;
-    q += d * d;
-  }
-  const float rstd = rsqrtf(wave_sum(q) / (float)cols + eps);
-  float wv[EPL], bv[EPL];
-  load_f32<EPL>(w + col0, wv);
-  load_f32<EPL>(b + col0, bv);
-#pragma unroll
-  for (int i = 0; i < EPL; ++i) v[i] = (v[i] - mean) * rstd * wv[i] + bv[i];
-}
-
 // Per-branch geometry of the dilated schedule (dilated_attention.py:16-31, 76-98).
 struct GpBranch {
   int32_t s;      // min(sl, L)

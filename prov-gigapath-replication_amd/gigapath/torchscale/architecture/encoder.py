@@ -102,9 +102,14 @@ class Encoder(nn.Module):
             raise RuntimeError("Encoder (MI355X path) needs ROCm device tensors")
         if encoder_padding_mask is None:
             encoder_padding_mask = torch.zeros(B, L, dtype=torch.bool, device=dev)
-        elif bool(encoder_padding_mask.any()):
-            raise NotImplementedError("non-empty encoder_padding_mask (the reference's flash path ignores it "
-                                      "inside attention but zeroes masked embeddings; not on the path)")
+        else:
+            # encoder.py:358: masked embeddings are zeroed before the first layer (and in
+            # encoder_states[0]); the flash attention path does not see the mask
+            # (multihead_attention.py:103), so padded tokens stay keys of every branch
+            if encoder_padding_mask.shape != (B, L):
+                raise ValueError("encoder_padding_mask must be [B, L] = [%d, %d], got %s"
+                                 % (B, L, tuple(encoder_padding_mask.shape)))
+            x_in = x_in * (1 - encoder_padding_mask.to(dev).unsqueeze(-1).type_as(x_in))
         layers = self.engine.pack(self, dev)
         pa = layers[0].attn
         ws = self.engine.workspace(dev, B, L, E, self.args.encoder_ffn_embed_dim, pa.H, pa.segs, pa.ratios)
@@ -123,5 +128,5 @@ class Encoder(nn.Module):
             _hip.layernorm_f32(x, E, runtime._f32(self.layer_norm.weight, dev), runtime._f32(self.layer_norm.bias, dev),
                                float(self.layer_norm.eps), out, B * L, E)
             x = out
-        return {"encoder_out": x.view(B, L, E).to(x_in.dtype), "encoder_embedding": x_in,
+        return {"encoder_out": x.view(B, L, E).to(x_in.dtype), "encoder_embedding": token_embeddings,
                 "encoder_padding_mask": encoder_padding_mask, "encoder_states": states, "l_aux": [None] * self.num_layers}

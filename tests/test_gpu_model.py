@@ -138,8 +138,11 @@ def test_dilated_attention_module_golden():
         assert ok, (b, rel, cos)
 
 
-def test_encoder_standalone_matches_oracle():
-    """Encoder.forward (reference signature) on random token embeddings, 2 layers."""
+@pytest.mark.parametrize("masked", [False, True])
+def test_encoder_standalone_matches_oracle(masked):
+    """Encoder.forward (reference signature) on random token embeddings, 2 layers.  masked: an
+    encoder_padding_mask zeroes those embeddings before the first layer (encoder.py:358) and is not
+    seen by the flash attention path (multihead_attention.py:103)."""
     from gigapath.torchscale.model.LongNet import make_longnet_from_name
     enc = make_longnet_from_name("LongNet_8_layers_768_dim", segment_length="[64, 128, 256, 512, 1024]",
                                  dropout=0.0, drop_path_rate=0.0)
@@ -152,11 +155,15 @@ def test_encoder_standalone_matches_oracle():
     enc = enc.to(DEV).eval()
     rng = np.random.default_rng(2)
     x = torch.from_numpy(rng.standard_normal((1, 700, 768)).astype(np.float32))
+    mask = torch.zeros(1, 700, dtype=torch.bool)
+    if masked:
+        mask[0, torch.from_numpy(rng.choice(700, 90, replace=False))] = True
     with torch.no_grad():
-        out = enc(None, token_embeddings=x.to(DEV), return_all_hiddens=True)
+        out = enc(None, encoder_padding_mask=mask.to(DEV) if masked else None, token_embeddings=x.to(DEV),
+                  return_all_hiddens=True)
     Wt = {k: torch.from_numpy(v) for k, v in W.items()}
-    h = x
-    states = [x]
+    h = x * (1 - mask.unsqueeze(-1).float())
+    states = [h]
     for li in range(2):
         h = orc.encoder_layer(h, Wt, "encoder.layers.%d" % li, cfg["segment_length"], cfg["dilated_ratio"], 16)
         states.append(h)
@@ -167,6 +174,9 @@ def test_encoder_standalone_matches_oracle():
     for s_got, s_ref in zip(out["encoder_states"], states):
         rel, cos, ok = close_enough(s_got.cpu().numpy(), s_ref.numpy())
         assert ok, (rel, cos)
+    assert torch.equal(out["encoder_embedding"].cpu(), x)
+    if masked:
+        assert not out["encoder_states"][0][0, mask[0]].any()
 
 
 def test_out_of_range_coords_raise_index_error(model):

@@ -1,7 +1,10 @@
 """Interleaved A/B timing of gp_dilated_attn_fwd across library builds (one process, one GPU).
 
     python tools/attn_ab.py --libs prod,tools/attn_lab/liblab_tune1.so [--L 70001] [--rounds 7]
-        [--branches all,0,1,2,3,4]
+        [--branches all,0,1,2,3,4] [--merge]
+
+--merge times gp_branch_merge_ln (the five branches' LSE merge + inner LN of one 70k layer, fed by
+the product attention's outputs) per library instead of the attention launches.
 
 "prod" is the in-tree product library.  Every round times every (library, branch set) pair once
 (HIP events around --iters back-to-back launches on random q/k/v of one layer), so clock drift and
@@ -32,7 +35,10 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--branches", default="all")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--merge", action="store_true")
     args = ap.parse_args()
+    if args.merge:
+        args.branches = "all"
     prod = _hip.load_library()
     libs = []
     for p in args.libs.split(","):
@@ -49,9 +55,14 @@ def main():
         sets.append((b, [SEGS[i] for i in sel], [RATIOS[i] for i in sel]))
     scratch = {name: runtime.AttentionScratch(torch.device("cuda"), 1, L, H, D, s, r) for name, s, r in sets}
     flops = {name: runtime.attention_valid_flops(L, s, r, H, D) for name, s, r in sets}
+    if args.merge:     # report GB/s of the merge's algorithmic bytes instead
+        flops = {name: 1e-3 * L * ((2 * E + 4 * H) * sum(1.0 / x for x in r) + 2 * E) for name, _, r in sets}
     times = {(p, name): [] for p, _ in libs for name, _, _ in sets}
     ident = {}
     ref = {}
+    merge_out = {}
+    ln_w = 1 + 0.1 * torch.randn(E, device="cuda", generator=g)
+    ln_b = 0.1 * torch.randn(E, device="cuda", generator=g)
     for rnd in range(args.rounds + 1):
         for p, lib in libs:
             _hip._lib = lib
@@ -59,6 +70,25 @@ def main():
                 sc = scratch[name]
                 run = lambda: _hip.dilated_attn_fwd(qkv, qkv[:, E:], qkv[:, 2 * E:], 3 * E, 1, L, H, D, s, r,  # noqa
                                                     sc.outs, sc.lses, 0.0, True)
+                if args.merge:
+                    if name not in merge_out:       # attention outputs once, from the product build
+                        _hip._lib = prod
+                        run()
+                        torch.cuda.synchronize()
+                        _hip._lib = lib
+                        merge_out[name] = torch.empty(L, E, device="cuda", dtype=torch.bfloat16)
+                    mo = merge_out[name]
+                    run = lambda: _hip.branch_merge_ln(sc.outs, sc.lses, s, r, 1, L, H, D, ln_w, ln_b, 1e-5, mo)  # noqa
+                    if rnd == 0:
+                        run()
+                        torch.cuda.synchronize()
+                        if name not in ref:
+                            ref[name] = [mo.clone()]
+                        else:
+                            ident[(p, name)] = torch.equal(mo.view(torch.uint8), ref[name][0].view(torch.uint8))
+                            if not ident[(p, name)]:
+                                print("max |diff| vs first:", (mo.float() - ref[name][0].float()).abs().max().item())
+                        continue
                 if rnd == 0:       # warm-up + outputs
                     run()
                     torch.cuda.synchronize()
@@ -82,8 +112,9 @@ def main():
         med, mn = statistics.median(ts), min(ts)
         res.append({"lib": p, "branches": name, "median_ms": round(med, 4), "min_ms": round(mn, 4),
                     "tflops_median": round(flops[name] / med / 1e9, 1), "bit_identical_to_first": ident.get((p, name), True)})
-        print("%-40s br=%-4s median %.4f ms  min %.4f ms  %7.1f TF/s  ident=%s" % (
-            p, name, med, mn, flops[name] / med / 1e9, ident.get((p, name), True)), flush=True)
+        print("%-40s br=%-4s median %.4f ms  min %.4f ms  %7.1f %s  ident=%s" % (
+            p, name, med, mn, flops[name] / med / 1e9, "GB/s" if args.merge else "TF/s",
+            ident.get((p, name), True)), flush=True)
     if args.out:
         with open(args.out, "w") as f:
             json.dump({"L": L, "rounds": args.rounds, "iters": args.iters, "results": res}, f, indent=1)

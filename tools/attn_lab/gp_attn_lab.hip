@@ -33,6 +33,15 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 // Exact unsigned division by a launch constant d < 2^31 via a multiply-high (the libdivide
 // "branchfree" form): the merge kernel's per-token divisions are wave-uniform, so they run on the
 // scalar unit instead of ~25 VALU instructions each.
+// (lab copy) LayerNorm of one row held as EPL values per lane; w / b loaded after the statistics
+template <int EPL>
+GP_DEV void wave_layernorm(float* v, int cols, const float* w, const float* b, float eps, int col0) {
+  float wv[EPL], bv[EPL];
+  load_f32<EPL>(w + col0, wv);
+  load_f32<EPL>(b + col0, bv);
+  wave_layernorm_regs<EPL>(v, cols, wv, bv, eps);
+}
+
 struct DivMagic {
   uint32_t m;
   int32_t l;     // 0: d == 1
