@@ -2,7 +2,8 @@
 solutions the product uses) on the slide encoder's GEMM shapes, interleaved in one process; reports
 median ms, TFLOP/s and the max |difference| relative to max |C|.
 
-    python tools/gemm_bench.py [--M 70001] [--rounds 5] [--iters 10] [--out file.json]
+    python tools/gemm_bench.py [--lib tools/attn_lab/liblab_gemm4.so] [--M 70001] [--rounds 5] [--iters 10]
+        [--shapes qkv,out,fc1,fc2,patch] [--out file.json]
 """
 import argparse
 import json
@@ -18,10 +19,15 @@ import ctypes  # noqa: E402
 
 from gigapath import runtime  # noqa: E402
 
-_lab = ctypes.CDLL(os.path.join(ROOT, "tools", "attn_lab", "liblab_gemm.so"))
-_lab.gp_gemm_bf16_tn.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
-                                 ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
-                                 ctypes.c_int64, ctypes.c_void_p]
+_lab = None
+
+
+def load_lab(path):
+    global _lab
+    _lab = ctypes.CDLL(path if os.path.isabs(path) else os.path.join(ROOT, path))
+    _lab.gp_gemm_bf16_tn.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                     ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                     ctypes.c_int64, ctypes.c_void_p]
 
 
 def gemm_bf16_tn(a, w, b, out):
@@ -41,12 +47,17 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--lib", default="tools/attn_lab/liblab_gemm.so")
+    ap.add_argument("--shapes", default="qkv,out,fc1,fc2,patch")
     args = ap.parse_args()
+    load_lab(args.lib)
     dev = torch.device("cuda")
     runtime.use_tuned_gemms(dev)
     g = torch.Generator(device="cuda").manual_seed(0)
     res = []
     for name, N, K, has_bias in SHAPES:
+        if name not in args.shapes.split(","):
+            continue
         M = args.M - 1 if name == "patch" else args.M
         a = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
         w = (torch.randn(N, K, device=dev, generator=g) * K ** -0.5).to(torch.bfloat16)

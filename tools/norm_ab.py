@@ -60,6 +60,12 @@ def main():
     for p, ts in times.items():
         med, mn = statistics.median(ts), min(ts)
         ident = torch.equal(outs[p].view(torch.int16), outs[first].view(torch.int16))
+        if not ident:
+            ne = outs[p].view(torch.int16) != outs[first].view(torch.int16)
+            rr, cc = torch.nonzero(ne, as_tuple=True)
+            print("%s: %d elements differ in %d rows; first rows %s cols %s; max|d| %.4g" % (
+                p, int(ne.sum()), len(torch.unique(rr)), torch.unique(rr)[:6].tolist(), torch.unique(cc)[:6].tolist(),
+                float((outs[p].float() - outs[first].float()).abs().max())), flush=True)
         res.append({"lib": p, "median_ms": round(med, 4), "min_ms": round(mn, 4),
                     "gbps_median": round(nbytes / med / 1e6, 1), "bit_identical_to_first": ident})
         print("%-40s median %.4f ms  min %.4f ms  %7.1f GB/s  ident=%s" % (p, med, mn, nbytes / med / 1e6, ident),
