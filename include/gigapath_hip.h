@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define GP_ABI_VERSION 4
+#define GP_ABI_VERSION 5
 #define GP_EARG (-1)
 #define GP_MAX_BRANCHES 8
 #define GP_MAX_DESTS 8
@@ -153,6 +153,14 @@ int gp_dilated_sparsify_dests(const uint16_t* src, int64_t src_row_stride, int64
 int gp_seg_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, int64_t nbatch,
                     int64_t seqlen, int H, int D, float softmax_scale, uint16_t* o, float* lse,
                     void* stream);
+
+/* The same seam for fp16 q / k / v / o (the reference pipeline runs the encoder under
+ * torch.cuda.amp.autocast(dtype=torch.float16), pipeline.py:186-187, so flash-attn receives fp16
+ * tensors and computes in fp16: P rounded to fp16, fp32 accumulation).  Exact running-max kernel
+ * with f16 MFMAs (v_mfma_f32_32x32x16_f16 / 16x16x32_f16); D in {48, 64, 96}. */
+int gp_seg_attn_fwd_f16(const uint16_t* q, const uint16_t* k, const uint16_t* v, int64_t nbatch,
+                        int64_t seqlen, int H, int D, float softmax_scale, uint16_t* o, float* lse,
+                        void* stream);
 
 /* Branch merge (DilatedAttention.scattering / sparse_to_dense, dilated_attention.py:33-53,
  * 100-131) fused with inner_attn_ln (:212-213):

@@ -29,6 +29,47 @@
 namespace {
 
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+// 16-bit element format of q / k / v / o: kH = false is bf16 (the forward), kH = true is fp16 (the
+// operator seam called under the reference pipeline's fp16 autocast, pipeline.py:186-187, whose
+// flash-attn computes in fp16).  Operands travel as raw 16-bit containers (bf16x8); only the MFMA
+// opcode, the P rounding and the output rounding depend on the format.
+template <bool kH>
+GP_DEV f32x16 mfma_32x32x16(bf16x8 a, bf16x8 b, f32x16 c) {
+  if constexpr (kH)
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+template <bool kH>
+GP_DEV f32x4 mfma_16x16x32(bf16x8 a, bf16x8 b, f32x4 c) {
+  if constexpr (kH)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+// fp32 -> the format's 16-bit pattern, round to nearest even
+template <bool kH>
+GP_DEV uint16_t f2e(float f) {
+  if constexpr (kH) return __builtin_bit_cast(uint16_t, (_Float16)f);
+  else return f2bf(f);
+}
+template <bool kH>
+GP_DEV __bf16 f2e_slot(float f) { return __builtin_bit_cast(__bf16, f2e<kH>(f)); }
+template <bool kH, int N>
+GP_DEV void store_e(uint16_t* p, const float* v) {
+  static_assert(N % 4 == 0, "");
+  uint2* q = reinterpret_cast<uint2*>(p);
+#pragma unroll
+  for (int i = 0; i < N / 4; ++i) {
+    uint2 u;
+    u.x = (uint32_t)f2e<kH>(v[4 * i + 0]) | ((uint32_t)f2e<kH>(v[4 * i + 1]) << 16);
+    u.y = (uint32_t)f2e<kH>(v[4 * i + 2]) | ((uint32_t)f2e<kH>(v[4 * i + 3]) << 16);
+    q[i] = u;
+  }
+}
 
 // Exact unsigned division by a launch constant d < 2^31 via a multiply-high: the merge kernel's
 // per-token divisions are wave-uniform, so they run on the scalar unit instead of ~25 VALU
@@ -174,7 +215,7 @@ GP_DEV int64_t xcd_group(int64_t bid, int64_t nb) {
   return base + (in & 7) * G + (in >> 3);
 }
 
-template <int D>
+template <int D, bool kH = false>
 __global__ __launch_bounds__(256, 2) void dilated_attn_kernel(const AttnArgs a) {
   constexpr int KS = (D + 31) / 32;          // 32-deep k-steps of Q.K (zero-padded d)
   constexpr int DT = D / 16;                 // 16-wide d tiles of P.V
@@ -284,7 +325,7 @@ __global__ __launch_bounds__(256, 2) void dilated_attn_kernel(const AttnArgs a) 
       for (int qt = 0; qt < kQT; ++qt) {
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[ks], qf[qt][ks], acc, 0, 0, 0);
+        for (int ks = 0; ks < KS; ++ks) acc = mfma_16x16x32<kH>(kf[ks], qf[qt][ks], acc);
         sacc[qt][kt] = acc;
       }
     }
@@ -329,8 +370,8 @@ __global__ __launch_bounds__(256, 2) void dilated_attn_kernel(const AttnArgs a) 
       for (int u = 0; u < 2; ++u)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          pf[qt][u][e] = (__bf16)sacc[qt][2 * u][e];
-          pf[qt][u][4 + e] = (__bf16)sacc[qt][2 * u + 1][e];
+          pf[qt][u][e] = f2e_slot<kH>(sacc[qt][2 * u][e]);
+          pf[qt][u][4 + e] = f2e_slot<kH>(sacc[qt][2 * u + 1][e]);
         }
     }
 
@@ -345,7 +386,7 @@ __global__ __launch_bounds__(256, 2) void dilated_attn_kernel(const AttnArgs a) 
         const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
 #pragma unroll
         for (int qt = 0; qt < kQT; ++qt)
-          oacc[qt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qt][u], oacc[qt][dt], 0, 0, 0);
+          oacc[qt][dt] = mfma_16x16x32<kH>(vf, pf[qt][u], oacc[qt][dt]);
       }
     }
 
@@ -376,7 +417,7 @@ __global__ __launch_bounds__(256, 2) void dilated_attn_kernel(const AttnArgs a) 
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
         float vv[4] = {oacc[qt][dt][0] * inv, oacc[qt][dt][1] * inv, oacc[qt][dt][2] * inv, oacc[qt][dt][3] * inv};
-        store_bf16<4>(orow + 16 * dt + 4 * g4, vv);
+        store_e<kH, 4>(orow + 16 * dt + 4 * g4, vv);
       }
       if (g4 == 0) br.lse[(bn * a.H + hh) * (int64_t)g.m + i] = (mr + log2f(l)) * 0.69314718055994530942f;
     }
@@ -397,8 +438,6 @@ __global__ __launch_bounds__(256, 2) void dilated_attn_kernel(const AttnArgs a) 
 //   * V image: 128-byte rows of four 32-byte blocks, block b of row r stored at b ^ (r & 3),
 //     which makes the transposed reads bank-conflict free; K image: 16-byte row padding
 //     (112 / 144-byte rows) makes the 32-row ds_read_b128 fragment reads conflict free.
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
 GP_DEV float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 // lse bit pattern (a quiet NaN no real row produces) that flags a row for the fixup pass
@@ -436,9 +475,16 @@ constexpr int kNWFast = GP_ATTN_NW;
 #define GP_ATTN_PRIO 1
 #endif
 static_assert(kNWFast == 4 || kNWFast == 8 || kNWFast == 16, "GP_ATTN_NW must be 4, 8 or 16");
+// GP_ATTN_ONES_SPARSE: the V image's spare d-block carries 1.0 only in the two rows the epilogue reads
+// (d = 48 and 52) and 0 elsewhere: same outputs, fewer toggling MFMA operand bits (same-box A/B
+// 1.276 -> 1.262 ms per 70k layer, profiles/r02_s6_ab_ones.json)
+#ifndef GP_ATTN_ONES_SPARSE
+#define GP_ATTN_ONES_SPARSE 1
+#endif
 
-template <int D, bool kPre, int MODE, bool kTab, int NW>
+template <int D, bool kPre, int MODE, bool kTab, int NW, bool kH>
 __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_idx) {
+  static_assert(!kH || MODE == kModeGen, "fp16 operands: register-staged exact kernel only");
   static_assert(D == 48 || D == 64, "v2 kernel covers D = 48 and 64");
   static_assert(MODE == kModeGen || (D == 48 && kPre), "LDS-DMA modes need D = 48 and a pre-scaled q");
   static_assert(NW == 4 || ((NW == 8 || NW == 16) && MODE != kModeGen), "8 / 16 waves: LDS-DMA modes only");
@@ -496,10 +542,17 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   const uint16_t* vbase = brr.v + (tok0 - brr.kv_tok_base) * brr.kv_stride + kcol;
 
   // V images: the d-columns >= D of every row (block 3 for D = 48) hold bf16 1.0
+  // (GP_ATTN_ONES_SPARSE: only d = 48 and 52, the two rows the epilogue reads; the rest 0)
   if constexpr (kOnes) {
     for (int idx = threadIdx.x; idx < NBUF * KT * 2; idx += NT) {   // NBUF bufs x KT rows x 2 chunks
       const int buf = idx / (2 * KT), rem = idx % (2 * KT), row = rem >> 1, half = rem & 1;
-      const uint4 ones = make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
+#if GP_ATTN_ONES_SPARSE
+      constexpr uint32_t one = kH ? 0x3C00u : 0x3F80u;   // 1.0 in the operand format
+      const uint4 ones = half ? make_uint4(0u, 0u, 0u, 0u) : make_uint4(one, 0u, one, 0u);
+#else
+      constexpr uint32_t one2 = kH ? 0x3C003C00u : 0x3F803F80u;
+      const uint4 ones = make_uint4(one2, one2, one2, one2);
+#endif
       *reinterpret_cast<uint4*>(smem + buf * BUF + KTILE + row * VROWB + 32 * (3 ^ (row & 3)) + 16 * half) = ones;
     }
   }
@@ -654,7 +707,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         const bf16x8 kk = *reinterpret_cast<const bf16x8*>(Kb + (32 * u + l32) * KROWB + 32 * ks + 16 * h);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kk, qf[ks], acc, 0, 0, 0);
+        acc = mfma_32x32x16<kH>(kk, qf[ks], acc);
       }
       sacc[u] = acc;
     }
@@ -742,7 +795,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
           for (int e = 0; e < 8; ++e) {
             const float p = fast_exp2(sacc[u][8 * s + e]);
             if constexpr (!kOnes) lsum += p;
-            pf[u][s][e] = (__bf16)p;
+            pf[u][s][e] = f2e_slot<kH>(p);
           }
     } else {
       const float tm = mx * a.c_log2;
@@ -765,7 +818,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
           for (int e = 0; e < 8; ++e) {
             const float p = fast_exp2(fmaf(sacc[u][8 * s + e], a.c_log2, -m_run));
             if constexpr (!kOnes) lsum += p;
-            pf[u][s][e] = (__bf16)p;
+            pf[u][s][e] = f2e_slot<kH>(p);
           }
     }
 
@@ -783,7 +836,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
           const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
           const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p1);
           const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-          oacc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[u][s], oacc[mt], 0, 0, 0);
+          oacc[mt] = mfma_32x32x16<kH>(vf, pf[u][s], oacc[mt]);
         }
       }
 
@@ -835,8 +888,8 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
 #pragma unroll
     for (int k = 0; k < D / 8; ++k) {
       const int mt = k / 4, rg = k % 4;
-      pk[k].x = (uint32_t)f2bf(oacc[mt][4 * rg] * inv) | ((uint32_t)f2bf(oacc[mt][4 * rg + 1] * inv) << 16);
-      pk[k].y = (uint32_t)f2bf(oacc[mt][4 * rg + 2] * inv) | ((uint32_t)f2bf(oacc[mt][4 * rg + 3] * inv) << 16);
+      pk[k].x = (uint32_t)f2e<kH>(oacc[mt][4 * rg] * inv) | ((uint32_t)f2e<kH>(oacc[mt][4 * rg + 1] * inv) << 16);
+      pk[k].y = (uint32_t)f2e<kH>(oacc[mt][4 * rg + 2] * inv) | ((uint32_t)f2e<kH>(oacc[mt][4 * rg + 3] * inv) << 16);
     }
 #pragma unroll
     for (int k = 0; k < D / 8; k += 2) {
@@ -861,7 +914,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
         if (d0 < D) {
           float vv[4] = {oacc[mt][4 * rg] * inv, oacc[mt][4 * rg + 1] * inv, oacc[mt][4 * rg + 2] * inv,
                          oacc[mt][4 * rg + 3] * inv};
-          store_bf16<4>(orow + d0, vv);
+          store_e<kH, 4>(orow + d0, vv);
         }
       }
   }
@@ -878,7 +931,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
 // consecutive items per block: the block reads the lse of every needed row of all of them at once
 // (wave w: items 8w .. 8w + 7; 16 independent loads per lane) and exits unless some row holds the
 // kLseRedo marker, so the pass costs about one load latency per 32 items when nothing overflowed.
-template <int D, bool kPre, int MODE, bool kTab = false, int NW = 4>
+template <int D, bool kPre, int MODE, bool kTab = false, int NW = 4, bool kH = false>
 __global__ __launch_bounds__(NW * 64, 2) void dilated_attn32_kernel(const AttnArgs a) {
   if constexpr (MODE == kModeFix) {
     constexpr int QB = NW * 32;
@@ -915,9 +968,9 @@ __global__ __launch_bounds__(NW * 64, 2) void dilated_attn32_kernel(const AttnAr
 #pragma unroll
     for (int n = 0; n < NV; ++n) flagged |= use[n] && vals[n] == kLseRedo;
     if (!__syncthreads_or(flagged)) return;
-    for (int k = 0; k < kFixItems && it0 + k < a.total_items; ++k) attn32_item<D, kPre, MODE, kTab, NW>(a, it0 + k);
+    for (int k = 0; k < kFixItems && it0 + k < a.total_items; ++k) attn32_item<D, kPre, MODE, kTab, NW, kH>(a, it0 + k);
   } else {
-    attn32_item<D, kPre, MODE, kTab, NW>(a, (int)xcd_group(blockIdx.x, gridDim.x));
+    attn32_item<D, kPre, MODE, kTab, NW, kH>(a, (int)xcd_group(blockIdx.x, gridDim.x));
   }
 }
 // ---------------------------------------------------------------------------------------
@@ -1127,10 +1180,10 @@ extern "C" int gp_dilated_gather(const uint16_t* src, int64_t row_stride, int64_
   return gp_check_launch("gp_dilated_gather");
 }
 
-extern "C" int gp_dilated_attn_fwd_ex(const uint16_t* q, int64_t q_row_stride, int64_t q_tok_base, int64_t B,
-                                      int64_t L, int H, int D, int64_t win_lo, int64_t win_hi,
-                                      const GpAttnBranch* branches, int nbranch, float softmax_scale,
-                                      int q_log2_prescaled, void* stream) {
+// kh: fp16 operands (the register-staged exact kernels); bf16 otherwise
+static int attn_fwd_impl(const uint16_t* q, int64_t q_row_stride, int64_t q_tok_base, int64_t B, int64_t L, int H,
+                         int D, int64_t win_lo, int64_t win_hi, const GpAttnBranch* branches, int nbranch,
+                         float softmax_scale, int q_log2_prescaled, bool kh, void* stream) {
   GP_REQUIRE(D == 48 || D == 64 || D == 96, "gp_dilated_attn_fwd: head dim %d unsupported (48, 64, 96)", D);
   GP_REQUIRE(nbranch >= 1 && nbranch <= GP_MAX_BRANCHES, "gp_dilated_attn_fwd: nbranch must be 1..%d", GP_MAX_BRANCHES);
   GP_REQUIRE(B > 0 && L > 0 && H > 0 && q_row_stride >= (int64_t)H * D && q_row_stride % 8 == 0,
@@ -1163,7 +1216,8 @@ extern "C" int gp_dilated_attn_fwd_ex(const uint16_t* q, int64_t q_row_stride, i
     const int64_t rs2 = 2 * d.kv_row_stride;
     kv_desc_ok = kv_desc_ok && dv >= 0 && rs2 >= dv + 2 * D && dv + 64 * (int64_t)d.ratio * rs2 < 0x7fffffff;
   }
-  const bool fast = D == 48 && q_log2_prescaled && kv_desc_ok;   // the LDS-DMA no-max kernel + fixup pass
+  // the LDS-DMA no-max kernel + fixup pass (bf16 only: unnormalised p = 2^s would overflow fp16)
+  const bool fast = !kh && D == 48 && q_log2_prescaled && kv_desc_ok;
   const int qblk = fast ? 32 * kNWFast : 128;   // query rows per workgroup
   // order branches by keys per work item (descending) so the longest items start first
   int order[GP_MAX_BRANCHES];
@@ -1226,7 +1280,13 @@ extern "C" int gp_dilated_attn_fwd_ex(const uint16_t* q, int64_t q_row_stride, i
   a.ntab = 0;
   GP_REQUIRE(items < (int64_t)0x7fffffff, "gp_dilated_attn_fwd: too many work items");
   hipStream_t s = gp_stream(stream);
-  if (D == 96) {
+  if (kh) {
+    if (D == 96) dilated_attn_kernel<96, true><<<(unsigned)items, 256, 0, s>>>(a);
+    else if (D == 48 && q_log2_prescaled) dilated_attn32_kernel<48, true, kModeGen, false, 4, true><<<(unsigned)items, 256, 0, s>>>(a);
+    else if (D == 48) dilated_attn32_kernel<48, false, kModeGen, false, 4, true><<<(unsigned)items, 256, 0, s>>>(a);
+    else if (q_log2_prescaled) dilated_attn32_kernel<64, true, kModeGen, false, 4, true><<<(unsigned)items, 256, 0, s>>>(a);
+    else dilated_attn32_kernel<64, false, kModeGen, false, 4, true><<<(unsigned)items, 256, 0, s>>>(a);
+  } else if (D == 96) {
     dilated_attn_kernel<96><<<(unsigned)items, 256, 0, s>>>(a);
   } else if (fast) {
     // the product launch: no-max kernel, then the fixup pass (exits at once unless a row was flagged)
@@ -1241,6 +1301,14 @@ extern "C" int gp_dilated_attn_fwd_ex(const uint16_t* q, int64_t q_row_stride, i
     else dilated_attn32_kernel<64, false, kModeGen><<<(unsigned)items, 256, 0, s>>>(a);
   }
   return gp_check_launch("gp_dilated_attn_fwd");
+}
+
+extern "C" int gp_dilated_attn_fwd_ex(const uint16_t* q, int64_t q_row_stride, int64_t q_tok_base, int64_t B,
+                                      int64_t L, int H, int D, int64_t win_lo, int64_t win_hi,
+                                      const GpAttnBranch* branches, int nbranch, float softmax_scale,
+                                      int q_log2_prescaled, void* stream) {
+  return attn_fwd_impl(q, q_row_stride, q_tok_base, B, L, H, D, win_lo, win_hi, branches, nbranch, softmax_scale,
+                       q_log2_prescaled, false, stream);
 }
 
 extern "C" int gp_dilated_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, int64_t row_stride,
@@ -1266,13 +1334,33 @@ extern "C" int gp_dilated_attn_fwd(const uint16_t* q, const uint16_t* k, const u
                                 stream);
 }
 
+static int seg_attn(const uint16_t* q, const uint16_t* k, const uint16_t* v, int64_t nbatch, int64_t seqlen, int H,
+                    int D, float softmax_scale, uint16_t* o, float* lse, bool kh, void* stream) {
+  GP_REQUIRE(seqlen > 0 && seqlen < (int64_t)0x7fffffff, "gp_seg_attn_fwd: bad seqlen");
+  GP_REQUIRE(k && v && o && lse, "gp_seg_attn_fwd: null pointer");
+  GpAttnBranch br;
+  br.seg_len = (int32_t)seqlen;
+  br.ratio = 1;
+  br.k = k;
+  br.v = v;
+  br.kv_row_stride = (int64_t)H * D;
+  br.kv_tok_base = 0;
+  br.kv_sparse_cols = 0;
+  br.o = o;
+  br.lse = lse;
+  return attn_fwd_impl(q, (int64_t)H * D, 0, nbatch, seqlen, H, D, 0, seqlen, &br, 1, softmax_scale, 0, kh, stream);
+}
+
 extern "C" int gp_seg_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, int64_t nbatch,
                                int64_t seqlen, int H, int D, float softmax_scale, uint16_t* o, float* lse,
                                void* stream) {
-  GP_REQUIRE(seqlen > 0 && seqlen < (int64_t)0x7fffffff, "gp_seg_attn_fwd: bad seqlen");
-  const int32_t sl = (int32_t)seqlen, r = 1;
-  return gp_dilated_attn_fwd(q, k, v, (int64_t)H * D, nbatch, seqlen, H, D, &sl, &r, 1, &o, &lse, softmax_scale,
-                             0, stream);
+  return seg_attn(q, k, v, nbatch, seqlen, H, D, softmax_scale, o, lse, false, stream);
+}
+
+extern "C" int gp_seg_attn_fwd_f16(const uint16_t* q, const uint16_t* k, const uint16_t* v, int64_t nbatch,
+                                   int64_t seqlen, int H, int D, float softmax_scale, uint16_t* o, float* lse,
+                                   void* stream) {
+  return seg_attn(q, k, v, nbatch, seqlen, H, D, softmax_scale, o, lse, true, stream);
 }
 
 extern "C" int gp_branch_merge_ln(const uint16_t* const* o_in, const float* const* lse_in, const int32_t* seg_len,

@@ -15,7 +15,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_lib", "libgigapath_hip.so")
-ABI_VERSION = 4
+ABI_VERSION = 5
 MAX_BRANCHES = 8
 MAX_DESTS = 8
 
@@ -50,6 +50,7 @@ SIGNATURES = {
     "gp_branch_merge_ln_window": [c_vp, c_vp, c_vp, c_vp, c_i32, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp,
                                   c_f32, c_vp, c_vp],
     "gp_seg_attn_fwd": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i32, c_f32, c_vp, c_vp, c_vp],
+    "gp_seg_attn_fwd_f16": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i32, c_f32, c_vp, c_vp, c_vp],
     "gp_branch_merge_ln": [c_vp, c_vp, c_vp, c_vp, c_i32, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_f32, c_vp, c_vp],
     "gp_residual_layernorm": [c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_vp, c_i64, c_i32, c_vp],
     "gp_gelu_layernorm": [c_vp, c_vp, c_vp, c_f32, c_vp, c_i64, c_i32, c_vp],
@@ -234,13 +235,16 @@ def branch_merge_ln_window(outs, lses, segs, ratios, B, L, tok_lo, n_tok, H, D, 
 
 
 def seg_attn_fwd(q, k, v, o, lse, softmax_scale=0.0):
+    """flash_attn_func seam: bf16 q/k/v/o -> gp_seg_attn_fwd, fp16 -> gp_seg_attn_fwd_f16."""
     lib = load_library()
     nb, sl, H, D = q.shape
+    dt = q.dtype if q.dtype in (torch.bfloat16, torch.float16) else torch.bfloat16
     for nm, t in (("q", q), ("k", k), ("v", v), ("o", o)):
-        _dev(t, torch.bfloat16, nm)
+        _dev(t, dt, nm)
     _dev(lse, torch.float32, "lse")
-    _check(lib.gp_seg_attn_fwd(_ptr(q), _ptr(k), _ptr(v), nb, sl, H, D, float(softmax_scale), _ptr(o), _ptr(lse),
-                               _stream()), "gp_seg_attn_fwd")
+    fn, name = (lib.gp_seg_attn_fwd_f16, "gp_seg_attn_fwd_f16") if dt == torch.float16 else \
+        (lib.gp_seg_attn_fwd, "gp_seg_attn_fwd")
+    _check(fn(_ptr(q), _ptr(k), _ptr(v), nb, sl, H, D, float(softmax_scale), _ptr(o), _ptr(lse), _stream()), name)
 
 
 def branch_merge_ln(outs, lses, segs, ratios, B, L, H, D, ln_w, ln_b, eps, out):

@@ -273,6 +273,29 @@ def test_seg_attn_fwd_operator_seam():
     assert (lse.cpu() - l_ref).abs().max().item() <= LSE_ATOL
 
 
+@pytest.mark.parametrize("D", [48, 64, 96])
+def test_seg_attn_fwd_fp16_operator_seam(D):
+    """fp16 q/k/v (the reference pipeline's autocast(float16) caller, pipeline.py:186-187) run the f16
+    MFMA kernel: out stays fp16 and is ~8x closer to the fp32 reference than the bf16 kernel on the
+    same values (P rounded to fp16, 11 significant bits, instead of bf16's 8)."""
+    _hip()
+    from gigapath.torchscale.component.flash_attention import flash_attn_func
+    rng = np.random.default_rng(D)
+    B, L, H = 2, 777, 16
+    q, k, v = (torch.from_numpy((1.5 * rng.standard_normal((B, L, H, D))).astype(np.float32)).half() for _ in range(3))
+    s = torch.einsum("blhd,bmhd->bhlm", q.float(), k.float()) * D ** -0.5
+    l_ref = torch.logsumexp(s, -1)
+    o_ref = torch.einsum("bhlm,bmhd->blhd", torch.softmax(s, -1), v.float())
+    out, lse = flash_attn_func(q.to(DEV), k.to(DEV), v.to(DEV))
+    assert out.dtype == torch.float16 and lse.dtype == torch.float32
+    err16 = (out.float().cpu() - o_ref).abs().max().item()
+    assert err16 <= 3e-3, err16
+    assert (lse.cpu() - l_ref).abs().max().item() <= 2e-3
+    ob, _ = flash_attn_func(q.bfloat16().to(DEV), k.bfloat16().to(DEV), v.bfloat16().to(DEV))
+    err_bf = (ob.float().cpu() - o_ref).abs().max().item()
+    assert err16 < 0.5 * err_bf, (err16, err_bf)
+
+
 @pytest.mark.parametrize("D", [64, 96])
 def test_attention_other_head_dims(D):
     """24L1024d (D=64) and 12L1536d (D=96) head dims."""
