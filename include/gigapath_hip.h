@@ -5,7 +5,8 @@
  * Conventions (all entry points):
  *   - extern "C", plain pointers and sizes, no framework types.
  *   - Every tensor pointer is a DEVICE pointer to caller-allocated, contiguous memory;
- *     the library never allocates.  "bf16" buffers are uint16_t bit patterns.
+ *     the library never allocates.  16-bit buffers ("act": bf16 or fp16 per the entry's fmt
+ *     argument) are uint16_t bit patterns.
  *   - Work is enqueued on `stream` (a hipStream_t passed as void*; NULL = default stream)
  *     and is stream-ordered; nothing synchronises the host.
  *   - Return value: 0 = ok, GP_EARG (-1) = bad argument, otherwise a hipError_t.
@@ -30,6 +31,13 @@ extern "C" {
 #define GP_MAX_BRANCHES 8
 #define GP_MAX_DESTS 8
 
+/* 16-bit activation format (the `fmt` argument of every entry point with 16-bit activations):
+ * bf16 (BASELINE's compute dtype) or fp16 (the reference pipeline's
+ * torch.cuda.amp.autocast(dtype=torch.float16), pipeline.py:186-187).  Residual stream, LN
+ * parameters, LSEs and readouts stay fp32 in both. */
+#define GP_FMT_BF16 0
+#define GP_FMT_F16 1
+
 /* ABI version of the loaded library (== GP_ABI_VERSION). */
 int gp_abi_version(void);
 
@@ -50,21 +58,21 @@ int gp_coords_to_pos(const void* coords, int coords_is_f64, int64_t n_tiles, int
  *   x_out[b, 0, :]   = cls                                  (pos_embed row 0 is zero)
  *   x_out[b, 1+t, :] = xp[b, t, :] + [tab[(p-1) % G] | tab[(p-1) / G]],  p = pos[b, t]
  *   ln_out           = LayerNorm(x_out; ln_w, ln_b, eps)    (skipped if ln_w == NULL)
- * xp: [B, N, E] bf16 (patch projection incl. bias); tab: [G, E/2] fp32 one-axis sin-cos
- * table (fp64-built); cls: [E] fp32; x_out: [B, N+1, E] fp32; ln_out: [B, N+1, E] bf16.
+ * xp: [B, N, E] act (patch projection incl. bias); tab: [G, E/2] fp32 one-axis sin-cos
+ * table (fp64-built); cls: [E] fp32; x_out: [B, N+1, E] fp32; ln_out: [B, N+1, E] act.
  * cls == NULL: no CLS row (a sequence-parallel shard that does not hold token 0):
  *   x_out[b, t, :] = xp[b, t, :] + pos row, t < N  (x_out, ln_out: [B, N, E]).
  * E must be 64 * {12, 16, 24}. */
 int gp_posembed_cls_ln(const uint16_t* xp, const int64_t* pos, const float* tab, const float* cls,
                        int64_t B, int64_t N, int E, int G, const float* ln_w, const float* ln_b,
-                       float eps, float* x_out, uint16_t* ln_out, void* stream);
+                       float eps, float* x_out, uint16_t* ln_out, int fmt, void* stream);
 
 /* Dilated sparsify of one branch (DilatedAttention.gathering / dense_to_sparse,
  * torchscale/component/dilated_attention.py:16-31, 76-98), bit-exact:
  *   dst[((b*nseg + n)*H + h)*m + i, :] = src[b*L + n*s + i*r + h/(Hp/r), col_off + h*D + :]
  *   or zeros where the reference pads (i*r + j >= s, or the token >= L).
  * s = min(sl, L), nseg = ceil(L/s), m = ceil(s/r), Hp = H rounded up to a multiple of r.
- * src: [B*L, row_stride] bf16; dst: [B*nseg*H*m, D] bf16.  D % 8 == 0. */
+ * src: [B*L, row_stride] 16-bit; dst: [B*nseg*H*m, D] same (a copy: any 16-bit format).  D % 8 == 0. */
 int gp_dilated_gather(const uint16_t* src, int64_t row_stride, int64_t col_off, int64_t B, int64_t L,
                       int H, int D, int sl, int r, uint16_t* dst, void* stream);
 
@@ -72,10 +80,10 @@ int gp_dilated_gather(const uint16_t* src, int64_t row_stride, int64_t col_off, 
  * folded into the attention addressing, and zero-padded keys are added analytically
  * (replaces gathering x3 + flash_attn_func per branch: dilated_attention.py:199-208,
  * multihead_attention.py:97-107, flash_attention.py:13-16).
- * q/k/v: [B*L, row_stride] bf16 (head h at columns h*D .. h*D+D-1 of each pointer; a fused
+ * q/k/v: [B*L, row_stride] act (head h at columns h*D .. h*D+D-1 of each pointer; a fused
  *   QKV buffer passes q = base, k = base + E, v = base + 2E, row_stride = 3E).
  * Branch b (sl = seg_len[b], r = ratios[b]) writes
- *   o_out[b]:   [B*nseg_b, m_b, H, D] bf16   (flash_attn's "out" layout per segment)
+ *   o_out[b]:   [B*nseg_b, m_b, H, D] act    (flash_attn's "out" layout per segment)
  *   lse_out[b]: [B*nseg_b, H, m_b]    fp32   (natural-log LSE, flash_attn's softmax_lse)
  * Rows whose values the merge can never read (beyond the last segment's tokens) are left
  * unwritten.  softmax_scale <= 0 selects D^-0.5.  D in {48, 64, 96}.
@@ -86,7 +94,7 @@ int gp_dilated_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v,
                         int64_t B, int64_t L, int H, int D, const int32_t* seg_len,
                         const int32_t* ratios, int nbranch, uint16_t* const* o_out,
                         float* const* lse_out, float softmax_scale, int q_log2_prescaled,
-                        void* stream);
+                        int fmt, void* stream);
 
 /* One branch of gp_dilated_attn_fwd_ex: where its keys/values live and where its outputs go. */
 typedef struct GpAttnBranch {
@@ -100,7 +108,7 @@ typedef struct GpAttnBranch {
                                 1: head h at columns (h % (H/r))*D (token-major sparsified rows
                                    written by gp_dilated_sparsify, where K is at column 0 and V at
                                    column (H/r)*D of each row; pass v = k + (H/r)*D) */
-  uint16_t* o;               /* [B*nseg, m, H, D] bf16 */
+  uint16_t* o;               /* [B*nseg, m, H, D] act */
   float* lse;                /* [B*nseg, H, m] fp32 */
 } GpAttnBranch;
 
@@ -115,7 +123,7 @@ typedef struct GpAttnBranch {
 int gp_dilated_attn_fwd_ex(const uint16_t* q, int64_t q_row_stride, int64_t q_tok_base, int64_t B,
                            int64_t L, int H, int D, int64_t win_lo, int64_t win_hi,
                            const GpAttnBranch* branches, int nbranch, float softmax_scale,
-                           int q_log2_prescaled, void* stream);
+                           int q_log2_prescaled, int fmt, void* stream);
 
 /* Token-major sparsified K/V rows for sequence parallelism (one rank's share of
  * DilatedAttention.gathering, dilated_attention.py:16-31,76-98).  For tokens
@@ -123,7 +131,7 @@ int gp_dilated_attn_fwd_ex(const uint16_t* q, int64_t q_row_stride, int64_t q_to
  * s = min(sl, L), j = (p % s) % r, C = (H/r)*D:
  *   dst[b][p - base_b, 0:C]  = src[p - tok_lo, k_col + j*C : k_col + (j+1)*C]
  *   dst[b][p - base_b, C:2C] = src[p - tok_lo, v_col + j*C : v_col + (j+1)*C]
- * dst[b]: [rows, 2C] bf16 whose row 0 holds token base_b = dst_tok_base[b] (NULL: all 0,
+ * dst[b]: [rows, 2C] 16-bit (a copy of src's format) whose row 0 holds token base_b = dst_tok_base[b] (NULL: all 0,
  * i.e. full-length [L, 2C] buffers); base_b <= tok_lo.  B = 1.  H % r == 0 for every branch. */
 int gp_dilated_sparsify(const uint16_t* src, int64_t src_row_stride, int64_t k_col, int64_t v_col,
                         int64_t tok_lo, int64_t n_tok, int64_t L, int H, int D, const int32_t* seg_len,
@@ -167,11 +175,11 @@ int gp_seg_attn_fwd_f16(const uint16_t* q, const uint16_t* k, const uint16_t* v,
  *   per (token p, head h): lse_b = covered ? lse_b[..] : -1e8, lse_b == 0 -> -1e8,
  *   w_b = softmax_b(lse_b) in fp32, out = sum_b w_b * o_b, then LayerNorm over H*D
  *   (skipped if ln_w == NULL).  Inputs are gp_dilated_attn_fwd's outputs.
- * out: [B*L, H*D] bf16. */
+ * out: [B*L, H*D] act (the o_in format). */
 int gp_branch_merge_ln(const uint16_t* const* o_in, const float* const* lse_in,
                        const int32_t* seg_len, const int32_t* ratios, int nbranch, int64_t B,
                        int64_t L, int H, int D, const float* ln_w, const float* ln_b, float eps,
-                       uint16_t* out, void* stream);
+                       uint16_t* out, int fmt, void* stream);
 
 /* gp_branch_merge_ln restricted to tokens [tok_lo, tok_lo + n_tok) of each batch (a
  * sequence-parallel shard): out row b*n_tok + (p - tok_lo).  Reads only the branch rows
@@ -179,7 +187,7 @@ int gp_branch_merge_ln(const uint16_t* const* o_in, const float* const* lse_in,
 int gp_branch_merge_ln_window(const uint16_t* const* o_in, const float* const* lse_in,
                               const int32_t* seg_len, const int32_t* ratios, int nbranch, int64_t B,
                               int64_t L, int64_t tok_lo, int64_t n_tok, int H, int D, const float* ln_w,
-                              const float* ln_b, float eps, uint16_t* out, void* stream);
+                              const float* ln_b, float eps, uint16_t* out, int fmt, void* stream);
 
 /* ---- Varlen packing (config C5, SURVEY §8e: "concatenate slides with per-slide segment
  * tables, no cross-slide attention").  nslide slides packed token-major in one qkv buffer
@@ -197,29 +205,30 @@ int gp_branch_merge_ln_window(const uint16_t* const* o_in, const float* const* l
  * gp_dilated_attn_fwd_varlen: every slide's five-branch attention in one launch (D = 48,
  *   q pre-scaled by D^-1/2 * log2 e).
  * gp_branch_merge_ln_varlen: every packed token's LSE merge + inner LN (E = 768, D = 48);
- *   out: [T, E] bf16, row = packed token. */
+ *   out: [T, E] act (the plan's qkv format), row = packed token. */
 int64_t gp_varlen_plan_bytes(int nslide, int nbranch);
 int gp_varlen_plan(const int64_t* L, int nslide, int H, int D, const int32_t* seg_len,
                    const int32_t* ratios, int nbranch, const uint16_t* qkv, int64_t qkv_row_stride,
                    uint16_t* const* o_out, float* const* lse_out, void* plan_host, int64_t plan_bytes,
                    int64_t* o_elems, int64_t* lse_elems);
 int gp_dilated_attn_fwd_varlen(const void* plan_host, const void* plan_dev, int q_log2_prescaled,
-                               void* stream);
+                               int fmt, void* stream);
 int gp_branch_merge_ln_varlen(const void* plan_host, const void* plan_dev, const float* ln_w,
-                              const float* ln_b, float eps, uint16_t* out, void* stream);
+                              const float* ln_b, float eps, uint16_t* out, int fmt, void* stream);
 
 /* Residual add fused with the next pre-LN (encoder.py:141,147 / :159,126):
  *   x += y + bias (fp32 residual stream, in place);  ln_out = LayerNorm(x) (skipped if ln_w == NULL).
- * x: [rows, cols] fp32; y: [rows, cols] bf16 (GEMM output without bias); bias: [cols] fp32 or NULL;
- * ln_out: [rows, cols] bf16.  cols = 64 * {12, 16, 24}. */
+ * x: [rows, cols] fp32; y: [rows, cols] act (GEMM output without bias); bias: [cols] fp32 or NULL;
+ * ln_out: [rows, cols] act.  cols = 64 * {12, 16, 24}. */
 int gp_residual_layernorm(float* x, const uint16_t* y, const float* bias, const float* ln_w,
                           const float* ln_b, float eps, uint16_t* ln_out, int64_t rows, int cols,
-                          void* stream);
+                          int fmt, void* stream);
 
 /* FFN middle (feedforward_network.py:131-137): out = LayerNorm(gelu_erf(h)) in fp32.
- * h, out: [rows, cols] bf16 (in place allowed); cols = 64 * {48, 64, 96}. */
+ * h, out: [rows, cols] act (in place allowed); cols = 64 * {48, 64, 96}.  GELU is rounded to act
+ * before the LN (gelu(x.float()).type_as(x), feedforward_network.py:135). */
 int gp_gelu_layernorm(const uint16_t* h, const float* ln_w, const float* ln_b, float eps,
-                      uint16_t* out, int64_t rows, int cols, void* stream);
+                      uint16_t* out, int64_t rows, int cols, int fmt, void* stream);
 
 /* Plain fp32 LayerNorm over rows with a row stride (readout: encoder.py:387-388,
  * slide_encoder.py:213-221).  out: [rows, cols] fp32 contiguous.  cols = 64 * {12, 16, 24}. */

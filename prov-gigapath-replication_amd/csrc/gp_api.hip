@@ -24,6 +24,12 @@ int gp_check_launch(const char* what) {
   return 0;
 }
 
+// GP_ABI_VERSION_OVERRIDE: a lab build whose entry points predate the current header (tools/attn_lab
+// liblab_r01.so: the round-1 sources, ABI 4) reports its own version, so the ctypes binding refuses it
+#ifdef GP_ABI_VERSION_OVERRIDE
+extern "C" int gp_abi_version(void) { return GP_ABI_VERSION_OVERRIDE; }
+#else
 extern "C" int gp_abi_version(void) { return GP_ABI_VERSION; }
+#endif
 
 extern "C" const char* gp_last_error_string(void) { return g_err; }

@@ -32,10 +32,10 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
-// 16-bit element format of q / k / v / o: kH = false is bf16 (the forward), kH = true is fp16 (the
-// operator seam called under the reference pipeline's fp16 autocast, pipeline.py:186-187, whose
-// flash-attn computes in fp16).  Operands travel as raw 16-bit containers (bf16x8); only the MFMA
-// opcode, the P rounding and the output rounding depend on the format.
+// 16-bit element format of q / k / v / o: kH = false is bf16 (BASELINE's dtype), kH = true is fp16
+// (the forward and the operator seam under the reference pipeline's fp16 autocast,
+// pipeline.py:186-187, whose flash-attn computes in fp16).  Operands travel as raw 16-bit containers
+// (bf16x8); only the MFMA opcode, the P rounding and the output rounding depend on the format.
 template <bool kH>
 GP_DEV f32x16 mfma_32x32x16(bf16x8 a, bf16x8 b, f32x16 c) {
   if constexpr (kH)
@@ -50,26 +50,8 @@ GP_DEV f32x4 mfma_16x16x32(bf16x8 a, bf16x8 b, f32x4 c) {
   else
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
-// fp32 -> the format's 16-bit pattern, round to nearest even
-template <bool kH>
-GP_DEV uint16_t f2e(float f) {
-  if constexpr (kH) return __builtin_bit_cast(uint16_t, (_Float16)f);
-  else return f2bf(f);
-}
 template <bool kH>
 GP_DEV __bf16 f2e_slot(float f) { return __builtin_bit_cast(__bf16, f2e<kH>(f)); }
-template <bool kH, int N>
-GP_DEV void store_e(uint16_t* p, const float* v) {
-  static_assert(N % 4 == 0, "");
-  uint2* q = reinterpret_cast<uint2*>(p);
-#pragma unroll
-  for (int i = 0; i < N / 4; ++i) {
-    uint2 u;
-    u.x = (uint32_t)f2e<kH>(v[4 * i + 0]) | ((uint32_t)f2e<kH>(v[4 * i + 1]) << 16);
-    u.y = (uint32_t)f2e<kH>(v[4 * i + 2]) | ((uint32_t)f2e<kH>(v[4 * i + 3]) << 16);
-    q[i] = u;
-  }
-}
 
 // Exact unsigned division by a launch constant d < 2^31 via a multiply-high: the merge kernel's
 // per-token divisions are wave-uniform, so they run on the scalar unit instead of ~25 VALU
@@ -459,7 +441,10 @@ constexpr uint32_t kLseRedo = 0x7fc0dead;
 //   kModeGen (D = 48 / 64, q pre-scaled or not): the same exact arithmetic with register-staged
 //     K/V tiles (global loads, addresses computed once), for k / v layouts the descriptor cannot
 //     cover (the operator seam's separate q / k / v tensors) and for D = 64.
-enum AttnMode { kModeFast = 0, kModeFix = 1, kModeGen = 2 };
+//   kModeExact (fp16 operands, D = 48, q pre-scaled): the LDS-DMA staging and work decomposition of
+//     kModeFast with the exact running-max arithmetic (no-max p = 2^s would overflow fp16), the
+//     -m start as the accumulator's initial value
+enum AttnMode { kModeFast = 0, kModeFix = 1, kModeGen = 2, kModeExact = 3 };
 constexpr int kFixItems = 32;
 
 // Waves per workgroup of the LDS-DMA kernels (each wave 32 queries; the K/V tile is shared by all):
@@ -484,7 +469,7 @@ static_assert(kNWFast == 4 || kNWFast == 8 || kNWFast == 16, "GP_ATTN_NW must be
 
 template <int D, bool kPre, int MODE, bool kTab, int NW, bool kH>
 __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_idx) {
-  static_assert(!kH || MODE == kModeGen, "fp16 operands: register-staged exact kernel only");
+  static_assert(!kH || MODE == kModeGen || MODE == kModeExact, "fp16 operands: exact kernels only");
   static_assert(D == 48 || D == 64, "v2 kernel covers D = 48 and 64");
   static_assert(MODE == kModeGen || (D == 48 && kPre), "LDS-DMA modes need D = 48 and a pre-scaled q");
   static_assert(NW == 4 || ((NW == 8 || NW == 16) && MODE != kModeGen), "8 / 16 waves: LDS-DMA modes only");
@@ -1014,7 +999,7 @@ constexpr int kTPW = 1;
 // NBR < GP_MAX_BRANCHES: the launch guarantees a.nbranch == NBR, so the branch loops have a
 // compile-time trip count (the 5-branch schedule of every registered arch: 3 dead branches of
 // position stepping, address math and exp fewer per token)
-template <int EPL, int D, bool kTab = false, int NBR = GP_MAX_BRANCHES>
+template <int EPL, int D, bool kTab = false, int NBR = GP_MAX_BRANCHES, bool kH = false>
 __global__ __launch_bounds__(256) void branch_merge_kernel(const MergeArgs a) {
   const int nbr = NBR < GP_MAX_BRANCHES ? NBR : a.nbranch;
   const int lane = threadIdx.x & 63;
@@ -1127,15 +1112,15 @@ __global__ __launch_bounds__(256) void branch_merge_kernel(const MergeArgs a) {
 #pragma unroll
         for (int q = 0; q < EPL / 4; ++q) {
           // explicit fma: every instantiation (and the varlen path) rounds identically
-          acc[4 * q + 0] = __builtin_fmaf(__uint_as_float(ob[b][q].x << 16), wb, acc[4 * q + 0]);
-          acc[4 * q + 1] = __builtin_fmaf(__uint_as_float(ob[b][q].x & 0xffff0000u), wb, acc[4 * q + 1]);
-          acc[4 * q + 2] = __builtin_fmaf(__uint_as_float(ob[b][q].y << 16), wb, acc[4 * q + 2]);
-          acc[4 * q + 3] = __builtin_fmaf(__uint_as_float(ob[b][q].y & 0xffff0000u), wb, acc[4 * q + 3]);
+          acc[4 * q + 0] = __builtin_fmaf(e2f<kH>(ob[b][q].x), wb, acc[4 * q + 0]);
+          acc[4 * q + 1] = __builtin_fmaf(e2f_hi<kH>(ob[b][q].x), wb, acc[4 * q + 1]);
+          acc[4 * q + 2] = __builtin_fmaf(e2f<kH>(ob[b][q].y), wb, acc[4 * q + 2]);
+          acc[4 * q + 3] = __builtin_fmaf(e2f_hi<kH>(ob[b][q].y), wb, acc[4 * q + 3]);
         }
       }
     }
     if (a.ln_w != nullptr) wave_layernorm_regs<EPL>(acc, E, wv, bv, a.eps);
-    store_bf16<EPL>(a.out + (int64_t)row * E + col0, acc);
+    store_e<kH, EPL>(a.out + (int64_t)row * E + col0, acc);
   }
 }
 
@@ -1184,6 +1169,8 @@ extern "C" int gp_dilated_gather(const uint16_t* src, int64_t row_stride, int64_
 static int attn_fwd_impl(const uint16_t* q, int64_t q_row_stride, int64_t q_tok_base, int64_t B, int64_t L, int H,
                          int D, int64_t win_lo, int64_t win_hi, const GpAttnBranch* branches, int nbranch,
                          float softmax_scale, int q_log2_prescaled, bool kh, void* stream) {
+  // bf16: the no-max LDS-DMA kernel + fixup pass (kModeFast / kModeFix) when the layout allows LDS-DMA
+  // staging, else the register-staged exact kernel; fp16: kModeExact / kModeGen likewise
   GP_REQUIRE(D == 48 || D == 64 || D == 96, "gp_dilated_attn_fwd: head dim %d unsupported (48, 64, 96)", D);
   GP_REQUIRE(nbranch >= 1 && nbranch <= GP_MAX_BRANCHES, "gp_dilated_attn_fwd: nbranch must be 1..%d", GP_MAX_BRANCHES);
   GP_REQUIRE(B > 0 && L > 0 && H > 0 && q_row_stride >= (int64_t)H * D && q_row_stride % 8 == 0,
@@ -1216,8 +1203,7 @@ static int attn_fwd_impl(const uint16_t* q, int64_t q_row_stride, int64_t q_tok_
     const int64_t rs2 = 2 * d.kv_row_stride;
     kv_desc_ok = kv_desc_ok && dv >= 0 && rs2 >= dv + 2 * D && dv + 64 * (int64_t)d.ratio * rs2 < 0x7fffffff;
   }
-  // the LDS-DMA no-max kernel + fixup pass (bf16 only: unnormalised p = 2^s would overflow fp16)
-  const bool fast = !kh && D == 48 && q_log2_prescaled && kv_desc_ok;
+  const bool fast = D == 48 && q_log2_prescaled && kv_desc_ok;   // LDS-DMA staging (8 waves x 32 queries)
   const int qblk = fast ? 32 * kNWFast : 128;   // query rows per workgroup
   // order branches by keys per work item (descending) so the longest items start first
   int order[GP_MAX_BRANCHES];
@@ -1281,7 +1267,8 @@ static int attn_fwd_impl(const uint16_t* q, int64_t q_row_stride, int64_t q_tok_
   GP_REQUIRE(items < (int64_t)0x7fffffff, "gp_dilated_attn_fwd: too many work items");
   hipStream_t s = gp_stream(stream);
   if (kh) {
-    if (D == 96) dilated_attn_kernel<96, true><<<(unsigned)items, 256, 0, s>>>(a);
+    if (fast) dilated_attn32_kernel<48, true, kModeExact, false, kNWFast, true><<<(unsigned)items, 64 * kNWFast, 0, s>>>(a);
+    else if (D == 96) dilated_attn_kernel<96, true><<<(unsigned)items, 256, 0, s>>>(a);
     else if (D == 48 && q_log2_prescaled) dilated_attn32_kernel<48, true, kModeGen, false, 4, true><<<(unsigned)items, 256, 0, s>>>(a);
     else if (D == 48) dilated_attn32_kernel<48, false, kModeGen, false, 4, true><<<(unsigned)items, 256, 0, s>>>(a);
     else if (q_log2_prescaled) dilated_attn32_kernel<64, true, kModeGen, false, 4, true><<<(unsigned)items, 256, 0, s>>>(a);
@@ -1306,15 +1293,16 @@ static int attn_fwd_impl(const uint16_t* q, int64_t q_row_stride, int64_t q_tok_
 extern "C" int gp_dilated_attn_fwd_ex(const uint16_t* q, int64_t q_row_stride, int64_t q_tok_base, int64_t B,
                                       int64_t L, int H, int D, int64_t win_lo, int64_t win_hi,
                                       const GpAttnBranch* branches, int nbranch, float softmax_scale,
-                                      int q_log2_prescaled, void* stream) {
+                                      int q_log2_prescaled, int fmt, void* stream) {
+  GP_REQUIRE(fmt == GP_FMT_BF16 || fmt == GP_FMT_F16, "gp_dilated_attn_fwd: bad fmt %d", fmt);
   return attn_fwd_impl(q, q_row_stride, q_tok_base, B, L, H, D, win_lo, win_hi, branches, nbranch, softmax_scale,
-                       q_log2_prescaled, false, stream);
+                       q_log2_prescaled, fmt == GP_FMT_F16, stream);
 }
 
 extern "C" int gp_dilated_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, int64_t row_stride,
                                    int64_t B, int64_t L, int H, int D, const int32_t* seg_len, const int32_t* ratios,
                                    int nbranch, uint16_t* const* o_out, float* const* lse_out, float softmax_scale,
-                                   int q_log2_prescaled, void* stream) {
+                                   int q_log2_prescaled, int fmt, void* stream) {
   GP_REQUIRE(D == 48 || D == 64 || D == 96, "gp_dilated_attn_fwd: head dim %d unsupported (48, 64, 96)", D);
   GP_REQUIRE(nbranch >= 1 && nbranch <= GP_MAX_BRANCHES, "gp_dilated_attn_fwd: nbranch must be 1..%d", GP_MAX_BRANCHES);
   GP_REQUIRE(k && v && seg_len && ratios && o_out && lse_out, "gp_dilated_attn_fwd: null pointer");
@@ -1331,7 +1319,7 @@ extern "C" int gp_dilated_attn_fwd(const uint16_t* q, const uint16_t* k, const u
     br[b].lse = lse_out[b];
   }
   return gp_dilated_attn_fwd_ex(q, row_stride, 0, B, L, H, D, 0, L, br, nbranch, softmax_scale, q_log2_prescaled,
-                                stream);
+                                fmt, stream);
 }
 
 static int seg_attn(const uint16_t* q, const uint16_t* k, const uint16_t* v, int64_t nbatch, int64_t seqlen, int H,
@@ -1365,16 +1353,39 @@ extern "C" int gp_seg_attn_fwd_f16(const uint16_t* q, const uint16_t* k, const u
 
 extern "C" int gp_branch_merge_ln(const uint16_t* const* o_in, const float* const* lse_in, const int32_t* seg_len,
                                   const int32_t* ratios, int nbranch, int64_t B, int64_t L, int H, int D,
-                                  const float* ln_w, const float* ln_b, float eps, uint16_t* out, void* stream) {
+                                  const float* ln_w, const float* ln_b, float eps, uint16_t* out, int fmt,
+                                  void* stream) {
   return gp_branch_merge_ln_window(o_in, lse_in, seg_len, ratios, nbranch, B, L, 0, L, H, D, ln_w, ln_b, eps, out,
-                                   stream);
+                                   fmt, stream);
+}
+
+template <bool kH>
+static void launch_merge(const MergeArgs& a, int E, int D, int nbranch, unsigned nb, hipStream_t s) {
+  switch (E) {
+    case 768:
+      if (D == 48 && nbranch == 5) branch_merge_kernel<12, 48, false, 5, kH><<<nb, 256, 0, s>>>(a);
+      else if (D == 48) branch_merge_kernel<12, 48, false, GP_MAX_BRANCHES, kH><<<nb, 256, 0, s>>>(a);
+      else if (D == 96) branch_merge_kernel<12, 96, false, GP_MAX_BRANCHES, kH><<<nb, 256, 0, s>>>(a);
+      else branch_merge_kernel<12, 12, false, GP_MAX_BRANCHES, kH><<<nb, 256, 0, s>>>(a);
+      break;
+    case 1024:
+      if (D == 64) branch_merge_kernel<16, 64, false, GP_MAX_BRANCHES, kH><<<nb, 256, 0, s>>>(a);
+      else branch_merge_kernel<16, 16, false, GP_MAX_BRANCHES, kH><<<nb, 256, 0, s>>>(a);
+      break;
+    case 1536:
+      if (D == 96) branch_merge_kernel<24, 96, false, GP_MAX_BRANCHES, kH><<<nb, 256, 0, s>>>(a);
+      else if (D == 48) branch_merge_kernel<24, 48, false, GP_MAX_BRANCHES, kH><<<nb, 256, 0, s>>>(a);
+      else branch_merge_kernel<24, 24, false, GP_MAX_BRANCHES, kH><<<nb, 256, 0, s>>>(a);
+      break;
+  }
 }
 
 extern "C" int gp_branch_merge_ln_window(const uint16_t* const* o_in, const float* const* lse_in,
                                          const int32_t* seg_len, const int32_t* ratios, int nbranch, int64_t B,
                                          int64_t L, int64_t tok_lo, int64_t n_tok, int H, int D, const float* ln_w,
-                                         const float* ln_b, float eps, uint16_t* out, void* stream) {
+                                         const float* ln_b, float eps, uint16_t* out, int fmt, void* stream) {
   const int E = H * D;
+  GP_REQUIRE(fmt == GP_FMT_BF16 || fmt == GP_FMT_F16, "gp_branch_merge_ln: bad fmt %d", fmt);
   GP_REQUIRE(nbranch >= 1 && nbranch <= GP_MAX_BRANCHES, "gp_branch_merge_ln: nbranch must be 1..%d", GP_MAX_BRANCHES);
   GP_REQUIRE((E == 768 && (D == 48 || D == 96 || D == 12)) || (E == 1024 && (D == 64 || D == 16)) ||
                  (E == 1536 && (D == 96 || D == 48 || D == 24)),
@@ -1398,24 +1409,8 @@ extern "C" int gp_branch_merge_ln_window(const uint16_t* const* o_in, const floa
   for (int b = nbranch; b < GP_MAX_BRANCHES; ++b) a.br[b] = a.br[nbranch - 1];
   a.ln_w = ln_w; a.ln_b = ln_b; a.eps = eps; a.out = out;
   const unsigned nb = (unsigned)((B * n_tok + 4 * kTPW - 1) / (4 * kTPW));   // kTPW tokens per wave
-  hipStream_t s = gp_stream(stream);
-  switch (E) {
-    case 768:
-      if (D == 48 && nbranch == 5) branch_merge_kernel<12, 48, false, 5><<<nb, 256, 0, s>>>(a);
-      else if (D == 48) branch_merge_kernel<12, 48><<<nb, 256, 0, s>>>(a);
-      else if (D == 96) branch_merge_kernel<12, 96><<<nb, 256, 0, s>>>(a);
-      else branch_merge_kernel<12, 12><<<nb, 256, 0, s>>>(a);
-      break;
-    case 1024:
-      if (D == 64) branch_merge_kernel<16, 64><<<nb, 256, 0, s>>>(a);
-      else branch_merge_kernel<16, 16><<<nb, 256, 0, s>>>(a);
-      break;
-    case 1536:
-      if (D == 96) branch_merge_kernel<24, 96><<<nb, 256, 0, s>>>(a);
-      else if (D == 48) branch_merge_kernel<24, 48><<<nb, 256, 0, s>>>(a);
-      else branch_merge_kernel<24, 24><<<nb, 256, 0, s>>>(a);
-      break;
-  }
+  if (fmt == GP_FMT_F16) launch_merge<true>(a, E, D, nbranch, nb, gp_stream(stream));
+  else launch_merge<false>(a, E, D, nbranch, nb, gp_stream(stream));
   return gp_check_launch("gp_branch_merge_ln");
 }
 
@@ -1549,7 +1544,8 @@ static int varlen_header(const void* plan_host, const void* plan_dev, const char
 }
 
 extern "C" int gp_dilated_attn_fwd_varlen(const void* plan_host, const void* plan_dev, int q_log2_prescaled,
-                                          void* stream) {
+                                          int fmt, void* stream) {
+  GP_REQUIRE(fmt == GP_FMT_BF16 || fmt == GP_FMT_F16, "gp_dilated_attn_fwd_varlen: bad fmt %d", fmt);
   VarlenHdr h;
   if (int rc = varlen_header(plan_host, plan_dev, "gp_dilated_attn_fwd_varlen", h)) return rc;
   GP_REQUIRE(h.D == 48 && q_log2_prescaled, "gp_dilated_attn_fwd_varlen: needs D = 48 and a pre-scaled q (D=%d)", h.D);
@@ -1565,6 +1561,11 @@ extern "C" int gp_dilated_attn_fwd_varlen(const void* plan_host, const void* pla
   a.ntab = h.ntab;
   a.d_H = make_div_magic((uint32_t)h.H);
   // the single-slide default's variant, so each packed slide's outputs equal its own launch's
+  if (fmt == GP_FMT_F16) {
+    dilated_attn32_kernel<48, true, kModeExact, true, kNWFast, true>
+        <<<(unsigned)h.total_items, 64 * kNWFast, 0, gp_stream(stream)>>>(a);
+    return gp_check_launch("gp_dilated_attn_fwd_varlen");
+  }
   dilated_attn32_kernel<48, true, kModeFast, true, kNWFast><<<(unsigned)h.total_items, 64 * kNWFast, 0, gp_stream(stream)>>>(a);
   dilated_attn32_kernel<48, true, kModeFix, true, kNWFast>
       <<<(unsigned)((h.total_items + kFixItems - 1) / kFixItems), 64 * kNWFast, 0, gp_stream(stream)>>>(a);
@@ -1572,7 +1573,8 @@ extern "C" int gp_dilated_attn_fwd_varlen(const void* plan_host, const void* pla
 }
 
 extern "C" int gp_branch_merge_ln_varlen(const void* plan_host, const void* plan_dev, const float* ln_w,
-                                         const float* ln_b, float eps, uint16_t* out, void* stream) {
+                                         const float* ln_b, float eps, uint16_t* out, int fmt, void* stream) {
+  GP_REQUIRE(fmt == GP_FMT_BF16 || fmt == GP_FMT_F16, "gp_branch_merge_ln_varlen: bad fmt %d", fmt);
   VarlenHdr h;
   if (int rc = varlen_header(plan_host, plan_dev, "gp_branch_merge_ln_varlen", h)) return rc;
   GP_REQUIRE(h.H * h.D == 768 && h.D == 48, "gp_branch_merge_ln_varlen: needs H*D = 768, D = 48");
@@ -1586,7 +1588,8 @@ extern "C" int gp_branch_merge_ln_varlen(const void* plan_host, const void* plan
   a.tok_off = reinterpret_cast<const int64_t*>(static_cast<const char*>(plan_dev) + h.tok_off_off);
   a.nslide = h.nslide;
   const unsigned nb = (unsigned)((h.T + 4 * kTPW - 1) / (4 * kTPW));
-  branch_merge_kernel<12, 48, true><<<nb, 256, 0, gp_stream(stream)>>>(a);
+  if (fmt == GP_FMT_F16) branch_merge_kernel<12, 48, true, GP_MAX_BRANCHES, true><<<nb, 256, 0, gp_stream(stream)>>>(a);
+  else branch_merge_kernel<12, 48, true><<<nb, 256, 0, gp_stream(stream)>>>(a);
   return gp_check_launch("gp_branch_merge_ln_varlen");
 }
 

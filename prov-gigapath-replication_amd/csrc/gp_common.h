@@ -16,6 +16,48 @@ GP_DEV uint16_t f2bf(float f) {
   return __builtin_bit_cast(uint16_t, h);
 }
 
+// 16-bit activation formats: kH = false is bf16 (BASELINE's dtype), kH = true is fp16 (the compute
+// format under the reference pipeline's torch.cuda.amp.autocast(float16), pipeline.py:186-187).
+// Raw 16-bit patterns in and out; conversions round to nearest even.
+template <bool kH>
+GP_DEV float e2f(uint32_t b16) {                 // the low 16 bits of b16
+  if constexpr (kH) return (float)__builtin_bit_cast(_Float16, (uint16_t)b16);
+  else return __uint_as_float(b16 << 16);
+}
+template <bool kH>
+GP_DEV float e2f_hi(uint32_t w) {                // the high 16 bits of w
+  if constexpr (kH) return (float)__builtin_bit_cast(_Float16, (uint16_t)(w >> 16));
+  else return __uint_as_float(w & 0xffff0000u);
+}
+template <bool kH>
+GP_DEV uint16_t f2e(float f) {
+  if constexpr (kH) return __builtin_bit_cast(uint16_t, (_Float16)f);
+  else return f2bf(f);
+}
+template <bool kH>
+GP_DEV uint32_t pack2e(float lo, float hi) { return (uint32_t)f2e<kH>(lo) | ((uint32_t)f2e<kH>(hi) << 16); }
+
+template <bool kH, int N>
+GP_DEV void load_e(const uint16_t* p, float* out) {
+  static_assert(N % 4 == 0, "");
+  const uint2* q = reinterpret_cast<const uint2*>(p);
+#pragma unroll
+  for (int i = 0; i < N / 4; ++i) {
+    const uint2 u = q[i];
+    out[4 * i + 0] = e2f<kH>(u.x);
+    out[4 * i + 1] = e2f_hi<kH>(u.x);
+    out[4 * i + 2] = e2f<kH>(u.y);
+    out[4 * i + 3] = e2f_hi<kH>(u.y);
+  }
+}
+template <bool kH, int N>
+GP_DEV void store_e(uint16_t* p, const float* v) {
+  static_assert(N % 4 == 0, "");
+  uint2* q = reinterpret_cast<uint2*>(p);
+#pragma unroll
+  for (int i = 0; i < N / 4; ++i) q[i] = make_uint2(pack2e<kH>(v[4 * i], v[4 * i + 1]), pack2e<kH>(v[4 * i + 2], v[4 * i + 3]));
+}
+
 GP_DEV float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -98,6 +140,16 @@ template <int EPL>
 GP_DEV void st_x4_bf16(uint16_t* row, int lane, const float* v) {
 #pragma unroll
   for (int k = 0; k < EPL / 4; ++k) store_bf16<4>(row + k * 256 + 4 * lane, v + 4 * k);
+}
+template <bool kH, int EPL>
+GP_DEV void ld_x4_e(const uint16_t* row, int lane, float* v) {
+#pragma unroll
+  for (int k = 0; k < EPL / 4; ++k) load_e<kH, 4>(row + k * 256 + 4 * lane, v + 4 * k);
+}
+template <bool kH, int EPL>
+GP_DEV void st_x4_e(uint16_t* row, int lane, const float* v) {
+#pragma unroll
+  for (int k = 0; k < EPL / 4; ++k) store_e<kH, 4>(row + k * 256 + 4 * lane, v + 4 * k);
 }
 template <int EPL>
 GP_DEV void ld_x8_bf16(const uint16_t* row, int lane, float* v) {

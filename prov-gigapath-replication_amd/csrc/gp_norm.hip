@@ -50,7 +50,7 @@ inline unsigned row_grid(int64_t rows) {
   return (unsigned)(nb < kMaxRowBlocks ? nb : kMaxRowBlocks);
 }
 
-template <int EPL>
+template <int EPL, bool kH>
 __global__ __launch_bounds__(256) void posembed_cls_ln_kernel(
     const uint16_t* __restrict__ xp, const int64_t* __restrict__ pos, const float* __restrict__ tab,
     const float* __restrict__ cls, int64_t B, int64_t N, int E, int G, const float* __restrict__ ln_w,
@@ -72,7 +72,7 @@ __global__ __launch_bounds__(256) void posembed_cls_ln_kernel(
     if (t < 0) {
       ld_x4_f32<EPL>(cls, lane, v);
     } else {
-      ld_x4_bf16<EPL>(xp + (b * N + t) * E, lane, v);
+      ld_x4_e<kH, EPL>(xp + (b * N + t) * E, lane, v);
       int64_t p = pos[b * N + t];
       const int64_t nrows = (int64_t)G * G + 1;
       if (p < 0) p += nrows;
@@ -91,13 +91,13 @@ __global__ __launch_bounds__(256) void posembed_cls_ln_kernel(
     st_x4_f32<EPL>(x_out + row * E, lane, v);
     if (ln_w != nullptr) {
       wave_layernorm_regs<EPL>(v, E, wv, bv, eps);
-      st_x4_bf16<EPL>(ln_out + row * E, lane, v);
+      st_x4_e<kH, EPL>(ln_out + row * E, lane, v);
     }
   }
 }
 
 // ---------------------------------------------------------------------------------------
-template <int EPL>
+template <int EPL, bool kH>
 __global__ __launch_bounds__(256) void residual_ln_kernel(float* __restrict__ x, const uint16_t* __restrict__ y,
                                                           const float* __restrict__ bias,
                                                           const float* __restrict__ ln_w,
@@ -118,13 +118,13 @@ __global__ __launch_bounds__(256) void residual_ln_kernel(float* __restrict__ x,
        row += (int64_t)gridDim.x * kRowsPerBlock) {
     float v[EPL], yv[EPL];
     ld_x4_f32<EPL>(x + row * cols, lane, v);
-    ld_x4_bf16<EPL>(y + row * cols, lane, yv);
+    ld_x4_e<kH, EPL>(y + row * cols, lane, yv);
 #pragma unroll
     for (int i = 0; i < EPL; ++i) v[i] += yv[i] + bb[i];
     st_x4_f32<EPL>(x + row * cols, lane, v);
     if (ln_w != nullptr) {
       wave_layernorm_regs<EPL>(v, cols, wv, bv, eps);
-      st_x4_bf16<EPL>(out + row * cols, lane, v);
+      st_x4_e<kH, EPL>(out + row * cols, lane, v);
     }
   }
 }
@@ -154,24 +154,21 @@ GP_DEV float gelu_erf(float x) {
 // registers allow).  The GELU outputs are rounded to bf16 in place -- as the reference's
 // gelu(x.float()).type_as(x) does before ffn_layernorm (feedforward_network.py:135-137) -- so
 // a row lives in EPL/2 registers, and the LN statistics are taken over those rounded values.
+template <bool kH>
 GP_DEV void unpack8(const uint4 u, float* v) {
   const uint32_t w4[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    v[2 * i] = __uint_as_float(w4[i] << 16);
-    v[2 * i + 1] = __uint_as_float(w4[i] & 0xffff0000u);
+    v[2 * i] = e2f<kH>(w4[i]);
+    v[2 * i + 1] = e2f_hi<kH>(w4[i]);
   }
 }
+template <bool kH>
 GP_DEV uint4 pack8(const float* v) {
-  uint4 u;
-  u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-  u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-  u.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
-  u.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
-  return u;
+  return make_uint4(pack2e<kH>(v[0], v[1]), pack2e<kH>(v[2], v[3]), pack2e<kH>(v[4], v[5]), pack2e<kH>(v[6], v[7]));
 }
 
-template <int EPL>
+template <int EPL, bool kH>
 __global__ __launch_bounds__(256) void gelu_ln_wave2_kernel(const uint16_t* h, const float* __restrict__ ln_w,
                                                             const float* __restrict__ ln_b, float eps,
                                                             uint16_t* out, int64_t rows) {
@@ -202,11 +199,11 @@ __global__ __launch_bounds__(256) void gelu_ln_wave2_kernel(const uint16_t* h, c
 #pragma unroll
     for (int k = 0; k < NK; ++k) {
       float v[8];
-      unpack8(cur[k], v);
+      unpack8<kH>(cur[k], v);
 #pragma unroll
       for (int i = 0; i < 8; ++i) v[i] = gelu_erf(v[i]);
-      cur[k] = pack8(v);
-      unpack8(cur[k], v);
+      cur[k] = pack8<kH>(v);
+      unpack8<kH>(cur[k], v);
 #pragma unroll
       for (int i = 0; i < 8; ++i) s += v[i];
       __builtin_amdgcn_sched_barrier(0);   // one chunk's GELU temporaries live at a time
@@ -216,7 +213,7 @@ __global__ __launch_bounds__(256) void gelu_ln_wave2_kernel(const uint16_t* h, c
 #pragma unroll
     for (int k = 0; k < NK; ++k) {
       float v[8];
-      unpack8(cur[k], v);
+      unpack8<kH>(cur[k], v);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const float d = v[i] - mean;
@@ -227,14 +224,14 @@ __global__ __launch_bounds__(256) void gelu_ln_wave2_kernel(const uint16_t* h, c
 #pragma unroll
     for (int k = 0; k < NK; ++k) {
       float v[8], wv[8], bv[8];
-      unpack8(cur[k], v);
+      unpack8<kH>(cur[k], v);
       *reinterpret_cast<float4*>(wv) = *reinterpret_cast<const float4*>(sw + k * 512 + 8 * lane);
       *reinterpret_cast<float4*>(wv + 4) = *reinterpret_cast<const float4*>(sw + k * 512 + 8 * lane + 4);
       *reinterpret_cast<float4*>(bv) = *reinterpret_cast<const float4*>(sb + k * 512 + 8 * lane);
       *reinterpret_cast<float4*>(bv + 4) = *reinterpret_cast<const float4*>(sb + k * 512 + 8 * lane + 4);
 #pragma unroll
       for (int i = 0; i < 8; ++i) v[i] = (v[i] - mean) * rstd * wv[i] + bv[i];
-      *reinterpret_cast<uint4*>(out + row * C + k * 512 + 8 * lane) = pack8(v);
+      *reinterpret_cast<uint4*>(out + row * C + k * 512 + 8 * lane) = pack8<kH>(v);
     }
 #pragma unroll
     for (int k = 0; k < NK; ++k) cur[k] = nxt[k];
@@ -252,17 +249,19 @@ __global__ __launch_bounds__(256) void gelu_ln_wave2_kernel(const uint16_t* h, c
 // kCopy: the table is copied into LDS from g_gelu_tab (filled once per device by gelu_tab_fill_kernel,
 // the same arithmetic, so the entries are bit-identical) -- 128 KiB from L2 instead of 65,536 gelu_erf
 // evaluations per block (~8 % of the launch at 70k rows).  Without kCopy each block evaluates the table.
-__device__ __attribute__((aligned(16))) uint16_t g_gelu_tab[65536];
+// One table per format (index: the input's 16 bits; entry: gelu_erf rounded to the same format).
+__device__ __attribute__((aligned(16))) uint16_t g_gelu_tab[2][65536];
 
+template <bool kH>
 __global__ __launch_bounds__(256) void gelu_tab_fill_kernel() {
   const int g = (int)blockIdx.x * 256 + (int)threadIdx.x;   // 8192 groups of 8 consecutive entries
   float v[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) v[i] = gelu_erf(__uint_as_float((uint32_t)(8 * g + i) << 16));
-  *reinterpret_cast<uint4*>(g_gelu_tab + 8 * g) = pack8(v);
+  for (int i = 0; i < 8; ++i) v[i] = gelu_erf(e2f<kH>((uint32_t)(8 * g + i)));
+  *reinterpret_cast<uint4*>(g_gelu_tab[kH] + 8 * g) = pack8<kH>(v);
 }
 
-template <int EPL, int NW = 8, bool kCopy = false>
+template <int EPL, int NW, bool kCopy, bool kH>
 __global__ __launch_bounds__(NW * 64) void gelu_ln_lut_kernel(const uint16_t* h, const float* __restrict__ ln_w,
                                                           const float* __restrict__ ln_b, float eps,
                                                           uint16_t* out, int64_t rows) {
@@ -271,13 +270,13 @@ __global__ __launch_bounds__(NW * 64) void gelu_ln_lut_kernel(const uint16_t* h,
   __shared__ __attribute__((aligned(16))) float sw[C], sb[C];
   if constexpr (kCopy) {
     for (int g = threadIdx.x; g < 65536 / 8; g += NW * 64)
-      *reinterpret_cast<uint4*>(tab + 8 * g) = *reinterpret_cast<const uint4*>(g_gelu_tab + 8 * g);
+      *reinterpret_cast<uint4*>(tab + 8 * g) = *reinterpret_cast<const uint4*>(g_gelu_tab[kH] + 8 * g);
   } else {
     for (int g = threadIdx.x; g < 65536 / 8; g += NW * 64) {   // 8 consecutive entries per step
       float v[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = gelu_erf(__uint_as_float((uint32_t)(8 * g + i) << 16));
-      *reinterpret_cast<uint4*>(tab + 8 * g) = pack8(v);
+      for (int i = 0; i < 8; ++i) v[i] = gelu_erf(e2f<kH>((uint32_t)(8 * g + i)));
+      *reinterpret_cast<uint4*>(tab + 8 * g) = pack8<kH>(v);
       __builtin_amdgcn_sched_barrier(0);
     }
   }
@@ -294,7 +293,7 @@ __global__ __launch_bounds__(NW * 64) void gelu_ln_lut_kernel(const uint16_t* h,
 #pragma unroll
     for (int k = 0; k < NK; ++k) cur[k] = *reinterpret_cast<const uint4*>(h + row * C + k * 512 + 8 * lane);
   }
-  auto look2 = [&](uint32_t w) -> uint32_t {   // two bf16 inputs -> two bf16 GELU outputs
+  auto look2 = [&](uint32_t w) -> uint32_t {   // two 16-bit inputs -> two GELU outputs
     return (uint32_t)tab[w & 0xffffu] | ((uint32_t)tab[w >> 16] << 16);
   };
   for (; row < rows; row += stride) {
@@ -308,7 +307,7 @@ __global__ __launch_bounds__(NW * 64) void gelu_ln_lut_kernel(const uint16_t* h,
     for (int k = 0; k < NK; ++k) {
       cur[k] = make_uint4(look2(cur[k].x), look2(cur[k].y), look2(cur[k].z), look2(cur[k].w));
       float v[8];
-      unpack8(cur[k], v);
+      unpack8<kH>(cur[k], v);
 #pragma unroll
       for (int i = 0; i < 8; ++i) s += v[i];
       __builtin_amdgcn_sched_barrier(0);   // bounds the lookups in flight (registers: 1024-thread block)
@@ -318,7 +317,7 @@ __global__ __launch_bounds__(NW * 64) void gelu_ln_lut_kernel(const uint16_t* h,
 #pragma unroll
     for (int k = 0; k < NK; ++k) {
       float v[8];
-      unpack8(cur[k], v);
+      unpack8<kH>(cur[k], v);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const float d = v[i] - mean;
@@ -330,14 +329,14 @@ __global__ __launch_bounds__(NW * 64) void gelu_ln_lut_kernel(const uint16_t* h,
 #pragma unroll
     for (int k = 0; k < NK; ++k) {
       float v[8], wv[8], bv[8];
-      unpack8(cur[k], v);
+      unpack8<kH>(cur[k], v);
       *reinterpret_cast<float4*>(wv) = *reinterpret_cast<const float4*>(sw + k * 512 + wo);
       *reinterpret_cast<float4*>(wv + 4) = *reinterpret_cast<const float4*>(sw + k * 512 + wo + 4);
       *reinterpret_cast<float4*>(bv) = *reinterpret_cast<const float4*>(sb + k * 512 + wo);
       *reinterpret_cast<float4*>(bv + 4) = *reinterpret_cast<const float4*>(sb + k * 512 + wo + 4);
 #pragma unroll
       for (int i = 0; i < 8; ++i) v[i] = (v[i] - mean) * rstd * wv[i] + bv[i];
-      *reinterpret_cast<uint4*>(out + row * C + k * 512 + 8 * lane) = pack8(v);
+      *reinterpret_cast<uint4*>(out + row * C + k * 512 + 8 * lane) = pack8<kH>(v);
     }
 #pragma unroll
     for (int k = 0; k < NK; ++k) cur[k] = nxt[k];
@@ -369,18 +368,19 @@ static int gp_num_cus(hipStream_t s) {       // per-device cache of the CU count
 // the stream is being captured into a graph the fill cannot be synchronised: the caller then takes the
 // self-filling kernel until an eager call has filled the table.  Two threads filling at once write the
 // same bytes.
-static bool gelu_tab_ready(hipStream_t s) {
-  static std::atomic<bool> ready[64];
+static bool gelu_tab_ready(hipStream_t s, bool kh) {
+  static std::atomic<bool> ready[2][64];
   const int dev = stream_device(s);
   if (dev < 0 || dev >= 64) return false;
-  if (ready[dev].load(std::memory_order_acquire)) return true;
+  if (ready[kh][dev].load(std::memory_order_acquire)) return true;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
   // a launch error here is reported by this call only (hipPeekAtLastError leaves earlier errors
   // pending for the caller's own check)
-  gelu_tab_fill_kernel<<<65536 / 8 / 256, 256, 0, s>>>();
+  if (kh) gelu_tab_fill_kernel<true><<<65536 / 8 / 256, 256, 0, s>>>();
+  else gelu_tab_fill_kernel<false><<<65536 / 8 / 256, 256, 0, s>>>();
   if (hipPeekAtLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess) return false;
-  ready[dev].store(true, std::memory_order_release);
+  ready[kh][dev].store(true, std::memory_order_release);
   return true;
 }
 
@@ -447,9 +447,16 @@ static bool epl_ok(int cols) {
   return cols % 64 == 0 && (cols / 64 == 12 || cols / 64 == 16 || cols / 64 == 24);
 }
 
+// fmt (every entry with 16-bit activations): GP_FMT_BF16 or GP_FMT_F16
+#define GP_FMT_DISPATCH(fmt, KERNEL_CALL_H, KERNEL_CALL_B) \
+  do {                                                    \
+    if (fmt == GP_FMT_F16) { KERNEL_CALL_H; } else { KERNEL_CALL_B; } \
+  } while (0)
+
 extern "C" int gp_posembed_cls_ln(const uint16_t* xp, const int64_t* pos, const float* tab, const float* cls,
                                   int64_t B, int64_t N, int E, int G, const float* ln_w, const float* ln_b,
-                                  float eps, float* x_out, uint16_t* ln_out, void* stream) {
+                                  float eps, float* x_out, uint16_t* ln_out, int fmt, void* stream) {
+  GP_REQUIRE(fmt == GP_FMT_BF16 || fmt == GP_FMT_F16, "gp_posembed_cls_ln: bad fmt %d", fmt);
   GP_REQUIRE(epl_ok(E), "gp_posembed_cls_ln: E=%d unsupported (64*{12,16,24})", E);
   GP_REQUIRE(B > 0 && N >= 0 && G > 0, "gp_posembed_cls_ln: bad sizes");
   GP_REQUIRE(tab && x_out && (N == 0 || (xp && pos)), "gp_posembed_cls_ln: null pointer");
@@ -457,33 +464,39 @@ extern "C" int gp_posembed_cls_ln(const uint16_t* xp, const int64_t* pos, const 
   const int64_t rows = B * (N + (cls != nullptr));
   if (rows == 0) return 0;
   hipStream_t s = gp_stream(stream);
+#define GP_POSEMB(EPL, KH) posembed_cls_ln_kernel<EPL, KH><<<row_grid(rows), 256, 0, s>>>(xp, pos, tab, cls, B, N, E, G, ln_w, ln_b, eps, x_out, ln_out)
   switch (E / 64) {
-    case 12: posembed_cls_ln_kernel<12><<<row_grid(rows), 256, 0, s>>>(xp, pos, tab, cls, B, N, E, G, ln_w, ln_b, eps, x_out, ln_out); break;
-    case 16: posembed_cls_ln_kernel<16><<<row_grid(rows), 256, 0, s>>>(xp, pos, tab, cls, B, N, E, G, ln_w, ln_b, eps, x_out, ln_out); break;
-    case 24: posembed_cls_ln_kernel<24><<<row_grid(rows), 256, 0, s>>>(xp, pos, tab, cls, B, N, E, G, ln_w, ln_b, eps, x_out, ln_out); break;
+    case 12: GP_FMT_DISPATCH(fmt, GP_POSEMB(12, true), GP_POSEMB(12, false)); break;
+    case 16: GP_FMT_DISPATCH(fmt, GP_POSEMB(16, true), GP_POSEMB(16, false)); break;
+    case 24: GP_FMT_DISPATCH(fmt, GP_POSEMB(24, true), GP_POSEMB(24, false)); break;
   }
+#undef GP_POSEMB
   return gp_check_launch("gp_posembed_cls_ln");
 }
 
 extern "C" int gp_residual_layernorm(float* x, const uint16_t* y, const float* bias, const float* ln_w,
                                      const float* ln_b, float eps, uint16_t* ln_out, int64_t rows, int cols,
-                                     void* stream) {
+                                     int fmt, void* stream) {
+  GP_REQUIRE(fmt == GP_FMT_BF16 || fmt == GP_FMT_F16, "gp_residual_layernorm: bad fmt %d", fmt);
   GP_REQUIRE(epl_ok(cols), "gp_residual_layernorm: cols=%d unsupported (64*{12,16,24})", cols);
   GP_REQUIRE(rows >= 0, "gp_residual_layernorm: bad rows");
   if (rows == 0) return 0;
   GP_REQUIRE(x && y, "gp_residual_layernorm: null pointer");
   GP_REQUIRE(ln_w == nullptr || (ln_b && ln_out), "gp_residual_layernorm: LN needs ln_b and ln_out");
   hipStream_t s = gp_stream(stream);
+#define GP_RESLN(EPL, KH) residual_ln_kernel<EPL, KH><<<row_grid(rows), 256, 0, s>>>(x, y, bias, ln_w, ln_b, eps, ln_out, rows, cols)
   switch (cols / 64) {
-    case 12: residual_ln_kernel<12><<<row_grid(rows), 256, 0, s>>>(x, y, bias, ln_w, ln_b, eps, ln_out, rows, cols); break;
-    case 16: residual_ln_kernel<16><<<row_grid(rows), 256, 0, s>>>(x, y, bias, ln_w, ln_b, eps, ln_out, rows, cols); break;
-    case 24: residual_ln_kernel<24><<<row_grid(rows), 256, 0, s>>>(x, y, bias, ln_w, ln_b, eps, ln_out, rows, cols); break;
+    case 12: GP_FMT_DISPATCH(fmt, GP_RESLN(12, true), GP_RESLN(12, false)); break;
+    case 16: GP_FMT_DISPATCH(fmt, GP_RESLN(16, true), GP_RESLN(16, false)); break;
+    case 24: GP_FMT_DISPATCH(fmt, GP_RESLN(24, true), GP_RESLN(24, false)); break;
   }
+#undef GP_RESLN
   return gp_check_launch("gp_residual_layernorm");
 }
 
 extern "C" int gp_gelu_layernorm(const uint16_t* h, const float* ln_w, const float* ln_b, float eps,
-                                 uint16_t* out, int64_t rows, int cols, void* stream) {
+                                 uint16_t* out, int64_t rows, int cols, int fmt, void* stream) {
+  GP_REQUIRE(fmt == GP_FMT_BF16 || fmt == GP_FMT_F16, "gp_gelu_layernorm: bad fmt %d", fmt);
   GP_REQUIRE(cols % 64 == 0 && (cols / 64 == 48 || cols / 64 == 64 || cols / 64 == 96),
              "gp_gelu_layernorm: cols=%d unsupported (64*{48,64,96})", cols);
   GP_REQUIRE(rows >= 0, "gp_gelu_layernorm: bad rows");
@@ -497,19 +510,22 @@ extern "C" int gp_gelu_layernorm(const uint16_t* h, const float* ln_w, const flo
     const int64_t want = (rows + 7) / 8;
     const int cus = gp_num_cus(s);
     const unsigned nb = (unsigned)(want < cus ? want : cus);
-    const bool copy = gelu_tab_ready(s);
+    const bool copy = gelu_tab_ready(s, fmt == GP_FMT_F16);
+#define GP_LUT(EPL, CP, KH) gelu_ln_lut_kernel<EPL, 8, CP, KH><<<nb, 512, 0, s>>>(h, ln_w, ln_b, eps, out, rows)
     if (cols == 3072) {
-      if (copy) gelu_ln_lut_kernel<48, 8, true><<<nb, 512, 0, s>>>(h, ln_w, ln_b, eps, out, rows);
-      else gelu_ln_lut_kernel<48><<<nb, 512, 0, s>>>(h, ln_w, ln_b, eps, out, rows);
+      if (copy) GP_FMT_DISPATCH(fmt, GP_LUT(48, true, true), GP_LUT(48, true, false));
+      else GP_FMT_DISPATCH(fmt, GP_LUT(48, false, true), GP_LUT(48, false, false));
     } else {
-      if (copy) gelu_ln_lut_kernel<64, 8, true><<<nb, 512, 0, s>>>(h, ln_w, ln_b, eps, out, rows);
-      else gelu_ln_lut_kernel<64><<<nb, 512, 0, s>>>(h, ln_w, ln_b, eps, out, rows);
+      if (copy) GP_FMT_DISPATCH(fmt, GP_LUT(64, true, true), GP_LUT(64, true, false));
+      else GP_FMT_DISPATCH(fmt, GP_LUT(64, false, true), GP_LUT(64, false, false));
     }
+#undef GP_LUT
   } else {
     // v2 (F = 6144): wave per row, grid-stride with next-row prefetch, bf16-rounded GELU
     const int64_t want = (rows + 3) / 4;
     const unsigned nb = (unsigned)(want < 1024 ? want : 1024);
-    gelu_ln_wave2_kernel<96><<<nb, 256, 0, s>>>(h, ln_w, ln_b, eps, out, rows);
+    GP_FMT_DISPATCH(fmt, (gelu_ln_wave2_kernel<96, true><<<nb, 256, 0, s>>>(h, ln_w, ln_b, eps, out, rows)),
+                    (gelu_ln_wave2_kernel<96, false><<<nb, 256, 0, s>>>(h, ln_w, ln_b, eps, out, rows)));
   }
   return gp_check_launch("gp_gelu_layernorm");
 }

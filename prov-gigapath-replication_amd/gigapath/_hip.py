@@ -37,29 +37,31 @@ SIGNATURES = {
     "gp_abi_version": [],
     "gp_last_error_string": [],
     "gp_coords_to_pos": [c_vp, c_i32, c_i64, c_i32, c_f64, c_vp, c_vp, c_vp],
-    "gp_posembed_cls_ln": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp],
+    "gp_posembed_cls_ln": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_f32, c_vp, c_vp, c_i32,
+                           c_vp],
     "gp_dilated_gather": [c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp],
     "gp_dilated_attn_fwd": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp,
-                            c_f32, c_i32, c_vp],
+                            c_f32, c_i32, c_i32, c_vp],
     "gp_dilated_attn_fwd_ex": [c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i64, c_i64, c_vp, c_i32, c_f32,
-                               c_i32, c_vp],
+                               c_i32, c_i32, c_vp],
     "gp_dilated_sparsify": [c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp,
                             c_vp, c_vp],
     "gp_dilated_sparsify_dests": [c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_i32,
                                   c_vp, c_vp, c_vp],
     "gp_branch_merge_ln_window": [c_vp, c_vp, c_vp, c_vp, c_i32, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp,
-                                  c_f32, c_vp, c_vp],
+                                  c_f32, c_vp, c_i32, c_vp],
     "gp_seg_attn_fwd": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i32, c_f32, c_vp, c_vp, c_vp],
     "gp_seg_attn_fwd_f16": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i32, c_f32, c_vp, c_vp, c_vp],
-    "gp_branch_merge_ln": [c_vp, c_vp, c_vp, c_vp, c_i32, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_f32, c_vp, c_vp],
-    "gp_residual_layernorm": [c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_vp, c_i64, c_i32, c_vp],
-    "gp_gelu_layernorm": [c_vp, c_vp, c_vp, c_f32, c_vp, c_i64, c_i32, c_vp],
+    "gp_branch_merge_ln": [c_vp, c_vp, c_vp, c_vp, c_i32, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_f32, c_vp, c_i32,
+                           c_vp],
+    "gp_residual_layernorm": [c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_vp, c_i64, c_i32, c_i32, c_vp],
+    "gp_gelu_layernorm": [c_vp, c_vp, c_vp, c_f32, c_vp, c_i64, c_i32, c_i32, c_vp],
     "gp_layernorm_f32": [c_vp, c_i64, c_vp, c_vp, c_f32, c_vp, c_i64, c_i32, c_vp],
     "gp_mean_tokens": [c_vp, c_i64, c_i64, c_i32, c_i64, c_vp, c_vp],
     "gp_varlen_plan_bytes": [c_i32, c_i32],
     "gp_varlen_plan": [c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp],
-    "gp_dilated_attn_fwd_varlen": [c_vp, c_vp, c_i32, c_vp],
-    "gp_branch_merge_ln_varlen": [c_vp, c_vp, c_vp, c_vp, c_f32, c_vp, c_vp],
+    "gp_dilated_attn_fwd_varlen": [c_vp, c_vp, c_i32, c_i32, c_vp],
+    "gp_branch_merge_ln_varlen": [c_vp, c_vp, c_vp, c_vp, c_f32, c_vp, c_i32, c_vp],
 }
 _RESTYPES = {"gp_last_error_string": ctypes.c_char_p, "gp_varlen_plan_bytes": c_i64}
 
@@ -120,6 +122,19 @@ def _dev(t: torch.Tensor, dtype=None, name="tensor"):
     return t
 
 
+FMT_BF16, FMT_F16 = 0, 1            # GP_FMT_* (include/gigapath_hip.h)
+ACT_DTYPES = (torch.bfloat16, torch.float16)
+
+
+def fmt_of(dtype: torch.dtype) -> int:
+    """The C ABI's 16-bit activation format of a torch dtype (bf16 or fp16; anything else raises)."""
+    if dtype == torch.bfloat16:
+        return FMT_BF16
+    if dtype == torch.float16:
+        return FMT_F16
+    raise TypeError("gigapath HIP path: 16-bit activations must be bf16 or fp16 (got %s)" % dtype)
+
+
 def _i32_array(vals: Sequence[int]):
     return (ctypes.c_int32 * len(vals))(*[int(v) for v in vals])
 
@@ -145,17 +160,21 @@ def coords_to_pos(coords: torch.Tensor, grid: int, tile_size: float, pos_out: to
 
 def posembed_cls_ln(xp, pos, tab, cls, B, N, E, G, ln_w, ln_b, eps, x_out, ln_out):
     lib = load_library()
-    _dev(xp, torch.bfloat16, "xp"); _dev(pos, torch.int64, "pos"); _dev(tab, torch.float32, "tab")
+    fmt = fmt_of(xp.dtype)
+    _dev(xp, name="xp"); _dev(pos, torch.int64, "pos"); _dev(tab, torch.float32, "tab")
     if cls is not None:
         _dev(cls, torch.float32, "cls")
     _dev(x_out, torch.float32, "x_out")
+    if ln_out is not None:
+        _dev(ln_out, xp.dtype, "ln_out")
     _check(lib.gp_posembed_cls_ln(_ptr(xp), _ptr(pos), _ptr(tab), _ptr(cls), B, N, E, G, _ptr(ln_w), _ptr(ln_b),
-                                  eps, _ptr(x_out), _ptr(ln_out), _stream()), "gp_posembed_cls_ln")
+                                  eps, _ptr(x_out), _ptr(ln_out), fmt, _stream()), "gp_posembed_cls_ln")
 
 
 def dilated_gather(src, row_stride, col_off, B, L, H, D, sl, r, dst):
     lib = load_library()
-    _dev(src, torch.bfloat16, "src"); _dev(dst, torch.bfloat16, "dst")
+    fmt_of(src.dtype)
+    _dev(src, name="src"); _dev(dst, src.dtype, "dst")
     _check(lib.gp_dilated_gather(_ptr(src), row_stride, col_off, B, L, H, D, sl, r, _ptr(dst), _stream()),
            "gp_dilated_gather")
 
@@ -163,13 +182,16 @@ def dilated_gather(src, row_stride, col_off, B, L, H, D, sl, r, dst):
 def dilated_attn_fwd(q, k, v, row_stride, B, L, H, D, segs, ratios, outs, lses, softmax_scale=0.0,
                      q_log2_prescaled=False):
     lib = load_library()
+    fmt = fmt_of(q.dtype)
     for t in (q, k, v):
-        if not t.is_cuda or t.dtype != torch.bfloat16:
-            raise TypeError("q/k/v must be bf16 device tensors")
+        if not t.is_cuda or t.dtype != q.dtype:
+            raise TypeError("q/k/v must be device tensors of one 16-bit dtype")
+    for o in outs:
+        _dev(o, q.dtype, "o")
     oa, la = _ptr_array(outs), _ptr_array(lses)
     _check(lib.gp_dilated_attn_fwd(_ptr(q), _ptr(k), _ptr(v), row_stride, B, L, H, D, _i32_array(segs),
                                    _i32_array(ratios), len(segs), oa, la, float(softmax_scale),
-                                   int(bool(q_log2_prescaled)), _stream()),
+                                   int(bool(q_log2_prescaled)), fmt, _stream()),
            "gp_dilated_attn_fwd")
 
 
@@ -185,19 +207,21 @@ def dilated_attn_fwd_ex(q, q_row_stride, q_tok_base, B, L, H, D, win_lo, win_hi,
                         q_log2_prescaled=False):
     """branches: sequence of GpAttnBranch (attn_branch)."""
     lib = load_library()
-    if not q.is_cuda or q.dtype != torch.bfloat16:
-        raise TypeError("q must be a bf16 device tensor")
+    if not q.is_cuda:
+        raise TypeError("q must be a device tensor")
+    fmt = fmt_of(q.dtype)     # k / v / o of the descriptors are in q's format
     arr = (GpAttnBranch * len(branches))(*branches)
     _check(lib.gp_dilated_attn_fwd_ex(_ptr(q), q_row_stride, q_tok_base, B, L, H, D, win_lo, win_hi,
                                       ctypes.cast(arr, c_vp), len(branches), float(softmax_scale),
-                                      int(bool(q_log2_prescaled)), _stream()), "gp_dilated_attn_fwd_ex")
+                                      int(bool(q_log2_prescaled)), fmt, _stream()), "gp_dilated_attn_fwd_ex")
 
 
 def dilated_sparsify(src, src_row_stride, k_col, v_col, tok_lo, n_tok, L, H, D, segs, ratios, dsts, dst_bases=None):
     lib = load_library()
-    _dev(src, torch.bfloat16, "src")
+    fmt_of(src.dtype)
+    _dev(src, name="src")
     for t in dsts:
-        _dev(t, torch.bfloat16, "dst")
+        _dev(t, src.dtype, "dst")
     bases = None if dst_bases is None else (ctypes.c_int64 * len(dst_bases))(*[int(b) for b in dst_bases])
     _check(lib.gp_dilated_sparsify(_ptr(src), src_row_stride, k_col, v_col, tok_lo, n_tok, L, H, D, _i32_array(segs),
                                    _i32_array(ratios), len(segs), _ptr_array(dsts), bases, _stream()),
@@ -208,7 +232,8 @@ def dilated_sparsify_dests(src, src_row_stride, k_col, v_col, tok_lo, n_tok, L, 
     """dests[b] = list of (tok_lo, tok_hi, tensor, row_offset): token p of branch b is written to
     row row_offset + (p - tok_lo) of that [rows, 2C] bf16 tensor."""
     lib = load_library()
-    _dev(src, torch.bfloat16, "src")
+    fmt_of(src.dtype)
+    _dev(src, name="src")
     arr = (GpRowDest * (MAX_DESTS * len(segs)))()
     nd = (ctypes.c_int32 * len(segs))()
     for b, lst in enumerate(dests):
@@ -216,7 +241,7 @@ def dilated_sparsify_dests(src, src_row_stride, k_col, v_col, tok_lo, n_tok, L, 
             raise ValueError("at most %d destinations per branch" % MAX_DESTS)
         nd[b] = len(lst)
         for d, (lo, hi, t, off) in enumerate(lst):
-            _dev(t, torch.bfloat16, "dst")
+            _dev(t, src.dtype, "dst")
             if off < 0 or off + (hi - lo) > t.shape[0]:
                 raise ValueError("sparsify destination rows [%d, %d) outside a %d-row buffer" % (off, off + hi - lo,
                                                                                                t.shape[0]))
@@ -228,10 +253,13 @@ def dilated_sparsify_dests(src, src_row_stride, k_col, v_col, tok_lo, n_tok, L, 
 
 def branch_merge_ln_window(outs, lses, segs, ratios, B, L, tok_lo, n_tok, H, D, ln_w, ln_b, eps, out):
     lib = load_library()
-    _dev(out, torch.bfloat16, "out")
+    fmt = fmt_of(out.dtype)
+    _dev(out, name="out")
+    for o in outs:
+        _dev(o, out.dtype, "o")
     _check(lib.gp_branch_merge_ln_window(_ptr_array(outs), _ptr_array(lses), _i32_array(segs), _i32_array(ratios),
                                          len(segs), B, L, tok_lo, n_tok, H, D, _ptr(ln_w), _ptr(ln_b), eps, _ptr(out),
-                                         _stream()), "gp_branch_merge_ln_window")
+                                         fmt, _stream()), "gp_branch_merge_ln_window")
 
 
 def seg_attn_fwd(q, k, v, o, lse, softmax_scale=0.0):
@@ -249,23 +277,30 @@ def seg_attn_fwd(q, k, v, o, lse, softmax_scale=0.0):
 
 def branch_merge_ln(outs, lses, segs, ratios, B, L, H, D, ln_w, ln_b, eps, out):
     lib = load_library()
-    _dev(out, torch.bfloat16, "out")
+    fmt = fmt_of(out.dtype)
+    _dev(out, name="out")
+    for o in outs:
+        _dev(o, out.dtype, "o")
     _check(lib.gp_branch_merge_ln(_ptr_array(outs), _ptr_array(lses), _i32_array(segs), _i32_array(ratios),
-                                  len(segs), B, L, H, D, _ptr(ln_w), _ptr(ln_b), eps, _ptr(out), _stream()),
+                                  len(segs), B, L, H, D, _ptr(ln_w), _ptr(ln_b), eps, _ptr(out), fmt, _stream()),
            "gp_branch_merge_ln")
 
 
 def residual_layernorm(x, y, bias, ln_w, ln_b, eps, ln_out, rows, cols):
     lib = load_library()
-    _dev(x, torch.float32, "x"); _dev(y, torch.bfloat16, "y")
+    fmt = fmt_of(y.dtype)
+    _dev(x, torch.float32, "x"); _dev(y, name="y")
+    if ln_out is not None:
+        _dev(ln_out, y.dtype, "ln_out")
     _check(lib.gp_residual_layernorm(_ptr(x), _ptr(y), _ptr(bias), _ptr(ln_w), _ptr(ln_b), eps, _ptr(ln_out),
-                                     rows, cols, _stream()), "gp_residual_layernorm")
+                                     rows, cols, fmt, _stream()), "gp_residual_layernorm")
 
 
 def gelu_layernorm(h, ln_w, ln_b, eps, out, rows, cols):
     lib = load_library()
-    _dev(h, torch.bfloat16, "h"); _dev(out, torch.bfloat16, "out")
-    _check(lib.gp_gelu_layernorm(_ptr(h), _ptr(ln_w), _ptr(ln_b), eps, _ptr(out), rows, cols, _stream()),
+    fmt = fmt_of(h.dtype)
+    _dev(h, name="h"); _dev(out, h.dtype, "out")
+    _check(lib.gp_gelu_layernorm(_ptr(h), _ptr(ln_w), _ptr(ln_b), eps, _ptr(out), rows, cols, fmt, _stream()),
            "gp_gelu_layernorm")
 
 
@@ -313,11 +348,12 @@ class VarlenPlan:
 
     def bind(self, qkv: torch.Tensor, outs: Sequence[torch.Tensor], lses: Sequence[torch.Tensor]):
         lib = load_library()
-        _dev(qkv, torch.bfloat16, "qkv")
+        self.fmt = fmt_of(qkv.dtype)
+        _dev(qkv, name="qkv")
         if qkv.shape[0] < self.tok_off[-1] or qkv.shape[1] != 3 * self.H * self.D:
             raise ValueError("VarlenPlan.bind: qkv must be [>= %d, %d]" % (self.tok_off[-1], 3 * self.H * self.D))
         for b, (o, l) in enumerate(zip(outs, lses)):
-            _dev(o, torch.bfloat16, "o[%d]" % b); _dev(l, torch.float32, "lse[%d]" % b)
+            _dev(o, qkv.dtype, "o[%d]" % b); _dev(l, torch.float32, "lse[%d]" % b)
             if o.numel() < self.o_elems[b] or l.numel() < self.lse_elems[b]:
                 raise ValueError("VarlenPlan.bind: branch %d outputs too small" % b)
         host = (ctypes.c_uint8 * self.nbytes)()
@@ -334,12 +370,14 @@ class VarlenPlan:
 
 def dilated_attn_fwd_varlen(plan: VarlenPlan, q_log2_prescaled: bool = True):
     lib = load_library()
-    _check(lib.gp_dilated_attn_fwd_varlen(plan.host, _ptr(plan.dev), int(bool(q_log2_prescaled)), _stream()),
-           "gp_dilated_attn_fwd_varlen")
+    _check(lib.gp_dilated_attn_fwd_varlen(plan.host, _ptr(plan.dev), int(bool(q_log2_prescaled)), plan.fmt,
+                                          _stream()), "gp_dilated_attn_fwd_varlen")
 
 
 def branch_merge_ln_varlen(plan: VarlenPlan, ln_w, ln_b, eps, out):
     lib = load_library()
-    _dev(out, torch.bfloat16, "out")
+    _dev(out, name="out")
+    if fmt_of(out.dtype) != plan.fmt:
+        raise TypeError("branch_merge_ln_varlen: out must be in the plan's 16-bit format")
     _check(lib.gp_branch_merge_ln_varlen(plan.host, _ptr(plan.dev), _ptr(ln_w), _ptr(ln_b), eps, _ptr(out),
-                                         _stream()), "gp_branch_merge_ln_varlen")
+                                         plan.fmt, _stream()), "gp_branch_merge_ln_varlen")

@@ -15,7 +15,7 @@ Per layer the engine issues 9 launches on torch's current HIP stream (M = B*L to
 which is EncoderLayer.forward (torchscale/architecture/encoder.py:116-162) with
 DilatedAttention.forward (component/dilated_attention.py:133-217) and the FFN
 (component/feedforward_network.py:131-142) in eval mode.  The residual stream stays fp32;
-GEMM operands are bf16 with fp32 accumulation.  Weights are packed once per parameter
+GEMM operands are 16-bit (bf16, or fp16 under the caller's fp16 autocast) with fp32 accumulation.  Weights are packed once per parameter
 version (fused QKV weight, bf16 GEMM operands, fp32 norms/biases) and workspaces are reused
 across calls of the same shape.  No CPU fallback exists: every non-GEMM op is a HIP kernel.
 """
@@ -24,6 +24,7 @@ from __future__ import annotations
 import functools
 import math
 import os
+import threading
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -52,16 +53,44 @@ def use_tuned_gemms(dev=None):
     torch.cuda.tunable.read_file(_TUNED)
 
 
-def bf16_compute(fn):
-    """The MI355X path computes in bf16 (BASELINE's dtype) whatever autocast region its caller has
-    open: the reference pipeline runs the slide encoder under torch.cuda.amp.autocast(fp16)
-    (pipeline.py:186-187), and autocast must not retarget the GEMMs that write into the bf16
-    workspaces (out=).  fp16 / fp32 inputs are converted to bf16 on entry; outputs keep the
-    model's parameter dtype (fp32), as the reference's autocast LayerNorm readout does."""
+_ACT = threading.local()
+
+
+def call_act_dtype(module: Optional[torch.nn.Module] = None) -> torch.dtype:
+    """The 16-bit activation format of a call: fp16 inside torch.autocast("cuda", float16) -- the
+    reference pipeline runs the slide encoder that way (pipeline.py:186-187), so its Linear layers
+    and flash-attn compute in fp16 -- or for a module whose parameters are fp16 (model.half());
+    bf16 (BASELINE's dtype) otherwise, including under bf16 autocast."""
+    if torch.is_autocast_enabled("cuda"):
+        return torch.float16 if torch.get_autocast_dtype("cuda") == torch.float16 else torch.bfloat16
+    if module is not None:
+        p = next(module.parameters(), None)
+        if p is not None and p.dtype == torch.float16:
+            return torch.float16
+    return torch.bfloat16
+
+
+def act_dtype() -> torch.dtype:
+    """The activation format of the compute_format call in progress on this thread (bf16 outside)."""
+    return getattr(_ACT, "dtype", None) or torch.bfloat16
+
+
+def compute_format(fn):
+    """Decorator of the module forwards: fixes the call's activation format (call_act_dtype) for the
+    whole call, nested forwards included, then runs with autocast off (autocast must not retarget
+    the GEMMs that write into the 16-bit workspaces with out=).  Every 16-bit activation, GEMM operand
+    and kernel format of the call follows it; the residual stream, LN parameters, LSEs and readouts
+    stay fp32; outputs keep the model's parameter dtype, as the reference's autocast LayerNorm
+    readout does."""
     @functools.wraps(fn)
-    def wrapped(*args, **kw):
-        with torch.autocast("cuda", enabled=False):
-            return fn(*args, **kw)
+    def wrapped(self, *args, **kw):
+        outer = getattr(_ACT, "dtype", None)
+        _ACT.dtype = outer if outer is not None else call_act_dtype(self)
+        try:
+            with torch.autocast("cuda", enabled=False):
+                return fn(self, *args, **kw)
+        finally:
+            _ACT.dtype = outer
     return wrapped
 
 
@@ -136,8 +165,13 @@ def attention_valid_flops(L: int, segs: Sequence[int], ratios: Sequence[int], H:
 # ------------------------------------------------------------------------------------------
 # packed weights
 # ------------------------------------------------------------------------------------------
+def _act(t: torch.Tensor, dev, act: torch.dtype = torch.bfloat16) -> torch.Tensor:
+    """A 16-bit GEMM operand copy (bf16 or fp16)."""
+    return t.detach().to(device=dev, dtype=act).contiguous()
+
+
 def _bf16(t: torch.Tensor, dev) -> torch.Tensor:
-    return t.detach().to(device=dev, dtype=torch.bfloat16).contiguous()
+    return _act(t, dev, torch.bfloat16)
 
 
 def _f32(t: torch.Tensor, dev) -> torch.Tensor:
@@ -150,18 +184,19 @@ LOG2E = 1.4426950408889634
 @dataclass
 class PackedAttention:
     """Packed DilatedAttention weights.  The softmax scale D^-0.5 and log2(e) are folded into the
-    Q rows of the fused projection (in fp32, before the single bf16 rounding of the GEMM output),
-    so the attention kernel consumes log2-domain logits (gp_dilated_attn_fwd q_log2_prescaled)."""
+    Q rows of the fused projection (in fp32, before the single 16-bit rounding of the GEMM output),
+    so the attention kernel consumes log2-domain logits (gp_dilated_attn_fwd q_log2_prescaled).
+    16-bit operands are in `act` (bf16, or fp16 for the caller's fp16 autocast)."""
     E: int
     H: int
     D: int
     segs: List[int]
     ratios: List[int]
-    w_qkv: torch.Tensor      # [3E, E] bf16 (q * scale*log2e | k | v rows)
-    b_qkv: torch.Tensor      # [3E] bf16
-    w_o: torch.Tensor        # [E, E] bf16
+    w_qkv: torch.Tensor      # [3E, E] act (q * scale*log2e | k | v rows)
+    b_qkv: torch.Tensor      # [3E] act
+    w_o: torch.Tensor        # [E, E] act
     b_o: torch.Tensor        # [E] fp32 (added in the residual kernel)
-    b_o_bf16: torch.Tensor   # [E] bf16 (standalone module forward)
+    b_o_act: torch.Tensor    # [E] act (standalone module forward)
     ln_w: torch.Tensor
     ln_b: torch.Tensor
     ln_eps: float
@@ -169,7 +204,7 @@ class PackedAttention:
     prescaled: bool = True
 
     @staticmethod
-    def from_module(m, dev) -> "PackedAttention":
+    def from_module(m, dev, act: torch.dtype = torch.bfloat16) -> "PackedAttention":
         E, H = m.embed_dim, m.num_heads
         D = E // H
         qs = (D ** -0.5) * LOG2E if D in (48, 64) else 1.0   # D=96 uses the generic kernel
@@ -177,9 +212,10 @@ class PackedAttention:
         bq = m.q_proj.bias.detach().to(device=dev, dtype=torch.float32) * qs
         return PackedAttention(
             E=E, H=H, D=D, segs=list(m.args.segment_length), ratios=list(m.args.dilated_ratio),
-            w_qkv=_bf16(torch.cat([wq, _f32(m.k_proj.weight, dev), _f32(m.v_proj.weight, dev)], 0), dev),
-            b_qkv=_bf16(torch.cat([bq, _f32(m.k_proj.bias, dev), _f32(m.v_proj.bias, dev)], 0), dev),
-            w_o=_bf16(m.out_proj.weight, dev), b_o=_f32(m.out_proj.bias, dev), b_o_bf16=_bf16(m.out_proj.bias, dev),
+            w_qkv=_act(torch.cat([wq, _f32(m.k_proj.weight, dev), _f32(m.v_proj.weight, dev)], 0), dev, act),
+            b_qkv=_act(torch.cat([bq, _f32(m.k_proj.bias, dev), _f32(m.v_proj.bias, dev)], 0), dev, act),
+            w_o=_act(m.out_proj.weight, dev, act), b_o=_f32(m.out_proj.bias, dev),
+            b_o_act=_act(m.out_proj.bias, dev, act),
             ln_w=_f32(m.inner_attn_ln.weight, dev), ln_b=_f32(m.inner_attn_ln.bias, dev),
             ln_eps=float(m.inner_attn_ln.eps), prescaled=D in (48, 64))
 
@@ -193,27 +229,27 @@ class PackedLayer:
     ln2_w: torch.Tensor
     ln2_b: torch.Tensor
     ln2_eps: float
-    w1: torch.Tensor         # [F, E] bf16
-    b1: torch.Tensor         # [F] bf16
+    w1: torch.Tensor         # [F, E] act
+    b1: torch.Tensor         # [F] act
     fln_w: torch.Tensor      # [F] fp32
     fln_b: torch.Tensor
     fln_eps: float
-    w2: torch.Tensor         # [E, F] bf16
+    w2: torch.Tensor         # [E, F] act
     b2: torch.Tensor         # [E] fp32
 
     @staticmethod
-    def from_module(layer, dev) -> "PackedLayer":
+    def from_module(layer, dev, act: torch.dtype = torch.bfloat16) -> "PackedLayer":
         ffn = layer.ffn
         return PackedLayer(
-            attn=PackedAttention.from_module(layer.self_attn, dev),
+            attn=PackedAttention.from_module(layer.self_attn, dev, act),
             ln1_w=_f32(layer.self_attn_layer_norm.weight, dev), ln1_b=_f32(layer.self_attn_layer_norm.bias, dev),
             ln1_eps=float(layer.self_attn_layer_norm.eps),
             ln2_w=_f32(layer.final_layer_norm.weight, dev), ln2_b=_f32(layer.final_layer_norm.bias, dev),
             ln2_eps=float(layer.final_layer_norm.eps),
-            w1=_bf16(ffn.fc1.weight, dev), b1=_bf16(ffn.fc1.bias, dev),
+            w1=_act(ffn.fc1.weight, dev, act), b1=_act(ffn.fc1.bias, dev, act),
             fln_w=_f32(ffn.ffn_layernorm.weight, dev), fln_b=_f32(ffn.ffn_layernorm.bias, dev),
             fln_eps=float(ffn.ffn_layernorm.eps),
-            w2=_bf16(ffn.fc2.weight, dev), b2=_f32(ffn.fc2.bias, dev))
+            w2=_act(ffn.fc2.weight, dev, act), b2=_f32(ffn.fc2.bias, dev))
 
 
 def param_signature(module: torch.nn.Module) -> tuple:
@@ -225,12 +261,12 @@ def param_signature(module: torch.nn.Module) -> tuple:
 # and by the standalone DilatedAttention module
 # ------------------------------------------------------------------------------------------
 class AttentionScratch:
-    def __init__(self, dev, B: int, L: int, H: int, D: int, segs, ratios):
-        self.key = (B, L, H, D, tuple(segs), tuple(ratios))
+    def __init__(self, dev, B: int, L: int, H: int, D: int, segs, ratios, act: torch.dtype = torch.bfloat16):
+        self.key = (B, L, H, D, tuple(segs), tuple(ratios), act)
         self.outs, self.lses = [], []
         for sl, r in zip(segs, ratios):
             s, nseg, m = branch_geometry(L, sl, r)
-            self.outs.append(torch.empty(B * nseg * m * H * D, dtype=torch.bfloat16, device=dev))
+            self.outs.append(torch.empty(B * nseg * m * H * D, dtype=act, device=dev))
             self.lses.append(torch.empty(B * nseg * H * m, dtype=torch.float32, device=dev))
 
 
@@ -240,14 +276,14 @@ class VarlenScratch:
 
     def __init__(self, dev, Ls: Sequence[int], H: int, D: int, segs, ratios, qkv: torch.Tensor):
         self.plan = _hip.VarlenPlan(Ls, H, D, segs, ratios)
-        self.outs = [torch.empty(n, dtype=torch.bfloat16, device=dev) for n in self.plan.o_elems]
+        self.outs = [torch.empty(n, dtype=qkv.dtype, device=dev) for n in self.plan.o_elems]
         self.lses = [torch.empty(n, dtype=torch.float32, device=dev) for n in self.plan.lse_elems]
         self.plan.bind(qkv, self.outs, self.lses)
 
 
 def dilated_attention_core(pa: PackedAttention, qkv: torch.Tensor, B: int, L: int, scratch: AttentionScratch,
                            out: torch.Tensor, inner_ln: bool = True):
-    """qkv: [B*L, 3E] bf16 (q | k | v); out: [B*L, E] bf16 = inner_attn_ln(merge(branches)).
+    """qkv: [B*L, 3E] 16-bit (q | k | v); out: [B*L, E] same format = inner_attn_ln(merge(branches)).
     With a VarlenScratch (bound to this qkv), every packed slide in one launch each."""
     E, H, D = pa.E, pa.H, pa.D
     if isinstance(scratch, VarlenScratch):
@@ -271,31 +307,32 @@ def dilated_attention_core(pa: PackedAttention, qkv: torch.Tensor, B: int, L: in
 # encoder engine
 # ------------------------------------------------------------------------------------------
 class Workspace:
-    def __init__(self, dev, B: int, L: int, E: int, F: int, H: int, segs, ratios):
+    def __init__(self, dev, B: int, L: int, E: int, F: int, H: int, segs, ratios, act: torch.dtype = torch.bfloat16):
         M = B * L
-        self.key = (str(dev), B, L, E, F, H, tuple(segs), tuple(ratios))
+        self.key = (str(dev), B, L, E, F, H, tuple(segs), tuple(ratios), act)
         self.x = torch.empty(M, E, dtype=torch.float32, device=dev)
-        self.a = torch.empty(M, E, dtype=torch.bfloat16, device=dev)
-        self.qkv = torch.empty(M, 3 * E, dtype=torch.bfloat16, device=dev)
-        self.y = torch.empty(M, E, dtype=torch.bfloat16, device=dev)
-        self.f = torch.empty(M, F, dtype=torch.bfloat16, device=dev)
-        self.attn = AttentionScratch(dev, B, L, H, E // H, segs, ratios)
+        self.a = torch.empty(M, E, dtype=act, device=dev)
+        self.qkv = torch.empty(M, 3 * E, dtype=act, device=dev)
+        self.y = torch.empty(M, E, dtype=act, device=dev)
+        self.f = torch.empty(M, F, dtype=act, device=dev)
+        self.attn = AttentionScratch(dev, B, L, H, E // H, segs, ratios, act)
 
 
 class PackedWorkspace(Workspace):
     """Workspace of several slides packed token-major: T = sum(L_i) rows, slide i at rows
     [tok_off[i], tok_off[i] + L_i) with its CLS first; attention through a VarlenScratch."""
 
-    def __init__(self, dev, Ls: Sequence[int], E: int, F: int, H: int, segs, ratios):
+    def __init__(self, dev, Ls: Sequence[int], E: int, F: int, H: int, segs, ratios,
+                 act: torch.dtype = torch.bfloat16):
         self.Ls = [int(x) for x in Ls]
         T = sum(self.Ls)
         M = T
-        self.key = (str(dev), tuple(self.Ls), E, F, H, tuple(segs), tuple(ratios))
+        self.key = (str(dev), tuple(self.Ls), E, F, H, tuple(segs), tuple(ratios), act)
         self.x = torch.empty(M, E, dtype=torch.float32, device=dev)
-        self.a = torch.empty(M, E, dtype=torch.bfloat16, device=dev)
-        self.qkv = torch.empty(M, 3 * E, dtype=torch.bfloat16, device=dev)
-        self.y = torch.empty(M, E, dtype=torch.bfloat16, device=dev)
-        self.f = torch.empty(M, F, dtype=torch.bfloat16, device=dev)
+        self.a = torch.empty(M, E, dtype=act, device=dev)
+        self.qkv = torch.empty(M, 3 * E, dtype=act, device=dev)
+        self.y = torch.empty(M, E, dtype=act, device=dev)
+        self.f = torch.empty(M, F, dtype=act, device=dev)
         self.attn = VarlenScratch(dev, self.Ls, H, E // H, segs, ratios, self.qkv)
         self.tok_off = self.attn.plan.tok_off
         self.cls_idx = torch.tensor(self.tok_off[:-1], dtype=torch.int64, device=dev)
@@ -307,33 +344,41 @@ class EncoderEngine:
     def __init__(self):
         self._sig = None
         self.layers: List[PackedLayer] = []
+        self._packs: Dict[torch.dtype, tuple] = {}     # act -> (signature, packed layers)
         self.ws: Optional[Workspace] = None
         self.pws: Optional[PackedWorkspace] = None
 
-    def pack(self, encoder, dev):
+    def pack(self, encoder, dev, act: Optional[torch.dtype] = None):
+        """Packed layers for the activation format `act` (default: the current call's, act_dtype());
+        one packing per format is kept, so alternating bf16 / fp16 callers do not repack."""
         use_tuned_gemms(dev)
-        sig = (str(dev), param_signature(encoder))
-        if sig != self._sig:
-            self.layers = [PackedLayer.from_module(l, dev) for l in encoder.layers]
-            self._sig = sig
+        act = act or act_dtype()
+        sig = (str(dev), param_signature(encoder), act)
+        ent = self._packs.get(act)
+        if ent is None or ent[0] != sig:
+            ent = (sig, [PackedLayer.from_module(l, dev, act) for l in encoder.layers])
+            self._packs[act] = ent
+        self._sig, self.layers = ent
         return self.layers
 
-    def workspace(self, dev, B, L, E, F, H, segs, ratios) -> Workspace:
-        key = (str(dev), B, L, E, F, H, tuple(segs), tuple(ratios))
+    def workspace(self, dev, B, L, E, F, H, segs, ratios, act: Optional[torch.dtype] = None) -> Workspace:
+        act = act or act_dtype()
+        key = (str(dev), B, L, E, F, H, tuple(segs), tuple(ratios), act)
         if self.ws is None or self.ws.key != key:
             self.ws = None
-            self.ws = Workspace(dev, B, L, E, F, H, segs, ratios)
+            self.ws = Workspace(dev, B, L, E, F, H, segs, ratios, act)
         return self.ws
 
-    def workspace_packed(self, dev, Ls, E, F, H, segs, ratios) -> PackedWorkspace:
-        key = (str(dev), tuple(int(x) for x in Ls), E, F, H, tuple(segs), tuple(ratios))
+    def workspace_packed(self, dev, Ls, E, F, H, segs, ratios, act: Optional[torch.dtype] = None) -> PackedWorkspace:
+        act = act or act_dtype()
+        key = (str(dev), tuple(int(x) for x in Ls), E, F, H, tuple(segs), tuple(ratios), act)
         if self.pws is None or self.pws.key != key:
             self.pws = None
-            self.pws = PackedWorkspace(dev, Ls, E, F, H, segs, ratios)
+            self.pws = PackedWorkspace(dev, Ls, E, F, H, segs, ratios, act)
         return self.pws
 
     def run_layers(self, ws: Workspace, B: int, L: int, layer_hook=None):
-        """ws.x holds the fp32 embedding and ws.a = LN1_0(ws.x) (bf16).  Runs every layer in
+        """ws.x holds the fp32 embedding and ws.a = LN1_0(ws.x) (16-bit).  Runs every layer in
         place; layer_hook(i) is called after layer i-1 finishes (i = 1..depth)."""
         M = B * L
         E = ws.x.shape[1]
@@ -368,7 +413,7 @@ def gemm_flops(B: int, N: int, E: int, F: int, C: int, depth: int) -> float:
 
 
 def merge_bytes(L: int, segs: Sequence[int], ratios: Sequence[int], H: int, D: int, B: int = 1) -> float:
-    """Algorithmic HBM bytes of one gp_branch_merge_ln launch (bf16 o, fp32 lse, bf16 out): per token,
+    """Algorithmic HBM bytes of one gp_branch_merge_ln launch (16-bit o, fp32 lse, 16-bit out): per token,
     branch b contributes the E/r_b covered output columns and H/r_b LSE values."""
     E = H * D
     per_tok = sum(E / r * 2 + H / r * 4 for r in ratios) + E * 2

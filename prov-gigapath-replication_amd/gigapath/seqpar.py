@@ -275,29 +275,29 @@ class Exchange:
 # per-rank engine
 # ------------------------------------------------------------------------------------------
 class ShardWorkspace:
-    def __init__(self, plan: ShardPlan, rank: int, dev, F: int):
+    def __init__(self, plan: ShardPlan, rank: int, dev, F: int, act: torch.dtype = torch.bfloat16):
         E, H, D = plan.E, plan.H, plan.D
         a, e = plan.bounds[rank]
         self.rank = rank
         self.n = e - a
         self.hq = plan.q_halo[rank]
         self.x = torch.empty(self.n, E, dtype=torch.float32, device=dev)
-        self.a = torch.empty(self.n, E, dtype=torch.bfloat16, device=dev)
-        self.qkv_ext = torch.empty(self.hq + self.n, 3 * E, dtype=torch.bfloat16, device=dev)
+        self.a = torch.empty(self.n, E, dtype=act, device=dev)
+        self.qkv_ext = torch.empty(self.hq + self.n, 3 * E, dtype=act, device=dev)
         self.qkv = self.qkv_ext[self.hq:]
-        self.y = torch.empty(self.n, E, dtype=torch.bfloat16, device=dev)
-        self.f = torch.empty(self.n, F, dtype=torch.bfloat16, device=dev)
+        self.y = torch.empty(self.n, E, dtype=act, device=dev)
+        self.f = torch.empty(self.n, F, dtype=act, device=dev)
         # per branch: K/V receive buffer = the need range in token order; send buffer packed by peer
         self.kvs, self.kv_base, self.send, self.send_off = [], [], [], []
         for b in range(len(plan.geo)):
             lo, hi = plan.need[rank][b]
-            self.kvs.append(torch.empty(hi - lo, 2 * plan.C[b], dtype=torch.bfloat16, device=dev))
+            self.kvs.append(torch.empty(hi - lo, 2 * plan.C[b], dtype=act, device=dev))
             self.kv_base.append(lo)
             splits = plan.send_splits(rank, b)
-            self.send.append(torch.empty(sum(splits), 2 * plan.C[b], dtype=torch.bfloat16, device=dev))
+            self.send.append(torch.empty(sum(splits), 2 * plan.C[b], dtype=act, device=dev))
             self.send_off.append(list(np.cumsum([0] + splits[:-1])))
         # branch outputs keep the single-device layout; only the window's rows are written/read
-        self.attn = runtime.AttentionScratch(dev, 1, plan.L, H, D, plan.segs, plan.ratios)
+        self.attn = runtime.AttentionScratch(dev, 1, plan.L, H, D, plan.segs, plan.ratios, act)
 
 
 class SeqParallelEngine:
@@ -447,15 +447,15 @@ class SeqParallelContext:
         self.ws: Optional[ShardWorkspace] = None
         self.engine: Optional[SeqParallelEngine] = None
 
-    def prepare(self, dev, L: int, segs, ratios, H: int, D: int, F: int):
-        key = (str(dev), L, tuple(segs), tuple(ratios), H, D, F)
+    def prepare(self, dev, L: int, segs, ratios, H: int, D: int, F: int, act: torch.dtype = torch.bfloat16):
+        key = (str(dev), L, tuple(segs), tuple(ratios), H, D, F, act)
         if self._key is None:
             # a collective every rank joins before any point-to-point call: with RCCL the first
             # P2P on a communicator must not be the first call of the group (torch batch_isend_irecv)
             self.exchange.all_reduce_(torch.zeros(1, device=dev))
         if key != self._key:
             self.plan = ShardPlan(L, self.world, segs, ratios, H, D, F)
-            self.ws = ShardWorkspace(self.plan, self.rank, dev, F)
+            self.ws = ShardWorkspace(self.plan, self.rank, dev, F, act)
             self.engine = SeqParallelEngine(self.plan, self.rank, self.exchange)
             self._key = key
         return self.plan, self.ws, self.engine

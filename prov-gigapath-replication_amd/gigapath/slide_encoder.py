@@ -55,8 +55,9 @@ class PatchEmbed(nn.Module):
         if dev.type != "cuda":
             raise RuntimeError("PatchEmbed (MI355X path) needs ROCm device tensors")
         B, L, C = x.shape
-        y = torch.addmm(self.proj.bias.to(dev, torch.bfloat16), x.reshape(B * L, C).to(torch.bfloat16),
-                        self.proj.weight.to(dev, torch.bfloat16).t())
+        act = runtime.call_act_dtype(self)
+        with torch.autocast("cuda", enabled=False):
+            y = torch.addmm(self.proj.bias.to(dev, act), x.reshape(B * L, C).to(act), self.proj.weight.to(dev, act).t())
         return y.view(B, L, -1).to(x.dtype)
 
 
@@ -162,10 +163,10 @@ class LongNetViT(nn.Module):
         sig = (str(dev), self.cls_token.data_ptr(), self.cls_token._version,
                tuple(runtime.param_signature(m) for m in mods))
         if sig != self._top_sig:
-            f32, bf = runtime._f32, runtime._bf16
+            f32 = runtime._f32
             ln1 = self.encoder.layers[0].self_attn_layer_norm
             self._top = dict(
-                wp=bf(self.patch_embed.proj.weight, dev), bp=bf(self.patch_embed.proj.bias, dev),
+                patch={},              # act -> (patch weight, patch bias) in that 16-bit format
                 cls=f32(self.cls_token.reshape(-1), dev),
                 tab=torch.from_numpy(axis_table(self.embed_dim, self.slide_ngrids)).to(dev),
                 ln1_w=f32(ln1.weight, dev), ln1_b=f32(ln1.bias, dev), ln1_eps=float(ln1.eps),
@@ -175,8 +176,19 @@ class LongNetViT(nn.Module):
             self._top_sig = sig
         return self._top
 
+    def _patch_gemm(self, top, x2d, out):
+        """out = x2d . Wp^T + bp in the call's activation format (hipBLASLt, bias epilogue)."""
+        act = out.dtype
+        if act not in top["patch"]:
+            dev = out.device
+            top["patch"][act] = (runtime._act(self.patch_embed.proj.weight, dev, act),
+                                 runtime._act(self.patch_embed.proj.bias, dev, act))
+        wp, bp = top["patch"][act]
+        with runtime.TIMER.span("gemm_patch"):
+            torch.addmm(bp, x2d.to(act), wp.t(), out=out)
+
     # ---------------------------------------------------------------- forward
-    @runtime.bf16_compute
+    @runtime.compute_format
     def forward(self, x, coords, all_layer_embed=False):
         """x [B, N, in_chans], coords [B, N, 2] (pixels) -> list of [B, E] slide embeddings:
         1 (final, after encoder.layer_norm) or, with all_layer_embed, 1 + depth (embedding and
@@ -239,8 +251,8 @@ class LongNetViT(nn.Module):
         dev = self.cls_token.device
         self._packed_top(dev)
         self.encoder.engine.pack(self.encoder, dev)
-        key = (str(dev), tuple(x.shape), x.dtype, c.dtype, bool(all_layer_embed), bool(self.global_pool),
-               self._top_sig, self.encoder.engine._sig)
+        key = (str(dev), tuple(x.shape), x.dtype, c.dtype, runtime.act_dtype(), bool(all_layer_embed),
+               bool(self.global_pool), self._top_sig, self.encoder.engine._sig)
         ent = self._graph_lookup(key)
         if ent is None and self._graph_wanted(key):
             ent = self._capture(key, x, c, lambda sx, sc: self._forward_device(sx, sc, all_layer_embed, False),
@@ -289,10 +301,10 @@ class LongNetViT(nn.Module):
         for old in [k for k in self._graphs if k[-2:] != sig]:    # superseded weights never replay
             self._drop_graph(old)
         stream = self.graph_stream()
-        # the static input is kept in bf16 (the forward's first use converts to bf16 anyway): the
-        # per-replay sx.copy_(x) then converts while copying, instead of a full-precision copy plus
-        # a conversion pass inside the graph (one 0.86 GB HBM round trip fewer at 70k tiles)
-        sx, sc = x.detach().to(torch.bfloat16, copy=True).contiguous(), c.detach().clone().contiguous()
+        # the static input is kept in the activation format (the forward's first use converts to it
+        # anyway): the per-replay sx.copy_(x) then converts while copying, instead of a full-precision
+        # copy plus a conversion pass inside the graph (one 0.86 GB HBM round trip fewer at 70k tiles)
+        sx, sc = x.detach().to(runtime.act_dtype(), copy=True).contiguous(), c.detach().clone().contiguous()
         cur = torch.cuda.current_stream()
         stream.wait_stream(cur)
         with torch.cuda.stream(stream):
@@ -315,7 +327,7 @@ class LongNetViT(nn.Module):
         return ent
 
     # ---------------------------------------------------------------- varlen packing (C5)
-    @runtime.bf16_compute
+    @runtime.compute_format
     def forward_packed(self, slides, all_layer_embed=False):
         """Several slides in ONE forward (config C5 "varlen segment packing").
 
@@ -354,8 +366,8 @@ class LongNetViT(nn.Module):
         if self.use_hip_graphs and not runtime.TIMER.enabled:
             self._packed_top(dev)
             self.encoder.engine.pack(self.encoder, dev)
-            key = ("packed", str(dev), Ns, x_cat.dtype, c_cat.dtype, bool(all_layer_embed), bool(self.global_pool),
-                   self._top_sig, self.encoder.engine._sig)
+            key = ("packed", str(dev), Ns, x_cat.dtype, c_cat.dtype, runtime.act_dtype(), bool(all_layer_embed),
+                   bool(self.global_pool), self._top_sig, self.encoder.engine._sig)
             ent = self._graph_lookup(key)
             if ent is None and self._graph_wanted(key):
                 ent = self._capture(key, x_cat, c_cat,
@@ -389,8 +401,7 @@ class LongNetViT(nn.Module):
         if not hasattr(ws, "pos"):
             ws.pos = torch.empty(Nt, dtype=torch.int64, device=dev)
         xp = ws.y[:Nt]
-        with runtime.TIMER.span("gemm_patch"):
-            torch.addmm(top["bp"], x_cat.to(torch.bfloat16), top["wp"].t(), out=xp)
+        self._patch_gemm(top, x_cat, xp)
         _hip.coords_to_pos(c_cat.contiguous(), self.slide_ngrids, self.tile_size, ws.pos, None)
         with runtime.TIMER.span("posembed"):
             n0 = 0
@@ -440,10 +451,9 @@ class LongNetViT(nn.Module):
             ws.pos = torch.empty(B * N, dtype=torch.int64, device=dev)
             ws.err = torch.zeros(1, dtype=torch.int32, device=dev)
 
-        # patch embedding (hipBLASLt, bias epilogue) into the spare bf16 buffer
+        # patch embedding (hipBLASLt, bias epilogue) into the spare 16-bit buffer
         xp = ws.y[:B * N]
-        with runtime.TIMER.span("gemm_patch"):
-            torch.addmm(top["bp"], x.reshape(B * N, C).to(torch.bfloat16), top["wp"].t(), out=xp)
+        self._patch_gemm(top, x.reshape(B * N, C), xp)
         c = coords if coords.dtype in (torch.float32, torch.float64) else coords.float()
         ws.err.zero_()
         _hip.coords_to_pos(c.contiguous(), self.slide_ngrids, self.tile_size, ws.pos, ws.err)
@@ -495,7 +505,7 @@ class LongNetViT(nn.Module):
         layers = eng.pack(self.encoder, dev)
         pa = layers[0].attn
         F = self.encoder.args.encoder_ffn_embed_dim
-        plan, ws, spe = sp.prepare(dev, L, pa.segs, pa.ratios, pa.H, pa.D, F)
+        plan, ws, spe = sp.prepare(dev, L, pa.segs, pa.ratios, pa.H, pa.D, F, runtime.act_dtype())
         spe.use_graphs = self.use_hip_graphs
         a, e = plan.bounds[sp.rank]
         t0, t1 = max(a, 1) - 1, e - 1                      # tiles of this shard (token = tile + 1)
@@ -505,8 +515,7 @@ class LongNetViT(nn.Module):
             ws.err = torch.zeros(1, dtype=torch.int32, device=dev)
         xp = ws.y[:nt]
         if nt > 0:
-            with runtime.TIMER.span("gemm_patch"):
-                torch.addmm(top["bp"], x[0, t0:t1].to(torch.bfloat16), top["wp"].t(), out=xp)
+            self._patch_gemm(top, x[0, t0:t1], xp)
         c = coords if coords.dtype in (torch.float32, torch.float64) else coords.float()
         ws.err.zero_()
         if nt > 0:

@@ -17,13 +17,14 @@ from ..component.dilated_attention import DilatedAttention
 from ..component.feedforward_network import FeedForwardNetwork
 
 
-def _ln_to_bf16(x32: torch.Tensor, ln: nn.LayerNorm, out_bf16: torch.Tensor):
-    """out = LayerNorm(x) for an fp32 [M, E] residual stream (standalone-module entry only)."""
+def _ln_to_act(x32: torch.Tensor, ln: nn.LayerNorm, out_act: torch.Tensor):
+    """out = LayerNorm(x) for an fp32 [M, E] residual stream, rounded to the 16-bit activation format
+    (standalone-module entry only)."""
     dev = x32.device
     tmp = torch.empty_like(x32)
     _hip.layernorm_f32(x32, x32.shape[1], runtime._f32(ln.weight, dev), runtime._f32(ln.bias, dev), float(ln.eps),
                        tmp, x32.shape[0], x32.shape[1])
-    out_bf16.copy_(tmp)
+    out_act.copy_(tmp)
 
 
 class EncoderLayer(nn.Module):
@@ -47,7 +48,7 @@ class EncoderLayer(nn.Module):
         return DilatedAttention(args, embed_dim, args.encoder_attention_heads, dropout=args.attention_dropout,
                                 self_attention=True, subln=args.subln)
 
-    @runtime.bf16_compute
+    @runtime.compute_format
     def forward(self, x, encoder_padding_mask=None, attn_mask=None, rel_pos=None, multiway_split_position=None,
                 incremental_state=None):
         if self.training and (self.dropout > 0 or self.drop_path_prob > 0):
@@ -57,11 +58,12 @@ class EncoderLayer(nn.Module):
         if dev.type != "cuda":
             raise RuntimeError("EncoderLayer (MI355X path) needs ROCm device tensors")
         eng = runtime.EncoderEngine()
-        pl = runtime.PackedLayer.from_module(self, dev)
+        act = runtime.act_dtype()
+        pl = runtime.PackedLayer.from_module(self, dev, act)
         eng.layers = [pl]
-        ws = runtime.Workspace(dev, B, L, E, self.ffn_dim, pl.attn.H, pl.attn.segs, pl.attn.ratios)
+        ws = runtime.Workspace(dev, B, L, E, self.ffn_dim, pl.attn.H, pl.attn.segs, pl.attn.ratios, act)
         ws.x.copy_(x.reshape(B * L, E))
-        _ln_to_bf16(ws.x, self.self_attn_layer_norm, ws.a)
+        _ln_to_act(ws.x, self.self_attn_layer_norm, ws.a)
         eng.run_layers(ws, B, L)
         return ws.x.view(B, L, E).to(x.dtype), None
 
@@ -86,7 +88,7 @@ class Encoder(nn.Module):
         if self.training and (self.args.dropout > 0 or self.args.drop_path_rate > 0):
             raise RuntimeError("the MI355X slide encoder is inference-only: call model.eval()")
 
-    @runtime.bf16_compute
+    @runtime.compute_format
     def forward(self, src_tokens, encoder_padding_mask=None, attn_mask=None, return_all_hiddens=False,
                 token_embeddings=None, multiway_split_position=None, features_only=False,
                 incremental_state=None, positions=None, **kwargs):
@@ -114,7 +116,7 @@ class Encoder(nn.Module):
         pa = layers[0].attn
         ws = self.engine.workspace(dev, B, L, E, self.args.encoder_ffn_embed_dim, pa.H, pa.segs, pa.ratios)
         ws.x.copy_(x_in.reshape(B * L, E))
-        _ln_to_bf16(ws.x, self.layers[0].self_attn_layer_norm, ws.a)
+        _ln_to_act(ws.x, self.layers[0].self_attn_layer_norm, ws.a)
         states = [x_in] if return_all_hiddens else []
 
         def hook(i):

@@ -39,14 +39,14 @@ class DilatedAttention(nn.Module):
         self._packed_sig = None
         self._scratch = None
 
-    def packed(self, dev) -> runtime.PackedAttention:
-        sig = (str(dev), runtime.param_signature(self))
+    def packed(self, dev, act: torch.dtype = torch.bfloat16) -> runtime.PackedAttention:
+        sig = (str(dev), runtime.param_signature(self), act)
         if sig != self._packed_sig:
-            self._packed = runtime.PackedAttention.from_module(self, dev)
+            self._packed = runtime.PackedAttention.from_module(self, dev, act)
             self._packed_sig = sig
         return self._packed
 
-    @runtime.bf16_compute
+    @runtime.compute_format
     def forward(self, query, key, value, incremental_state=None, key_padding_mask=None, attn_mask=None,
                 rel_pos=None, is_first_step=False, is_causal=False):
         if incremental_state is not None or is_causal or rel_pos is not None or attn_mask is not None:
@@ -59,19 +59,20 @@ class DilatedAttention(nn.Module):
         dev = query.device
         if dev.type != "cuda":
             raise RuntimeError("DilatedAttention (MI355X path) needs ROCm device tensors")
-        pa = self.packed(dev)
+        act = runtime.act_dtype()
+        pa = self.packed(dev, act)
         M = B * L
-        qkv = torch.empty(M, 3 * E, dtype=torch.bfloat16, device=dev)
+        qkv = torch.empty(M, 3 * E, dtype=act, device=dev)
         if key is query and value is query:
-            torch.addmm(pa.b_qkv, query.reshape(M, E).to(torch.bfloat16), pa.w_qkv.t(), out=qkv)
+            torch.addmm(pa.b_qkv, query.reshape(M, E).to(act), pa.w_qkv.t(), out=qkv)
         else:
             for i, t in enumerate((query, key, value)):
-                torch.addmm(pa.b_qkv[i * E:(i + 1) * E], t.reshape(M, E).to(torch.bfloat16),
+                torch.addmm(pa.b_qkv[i * E:(i + 1) * E], t.reshape(M, E).to(act),
                             pa.w_qkv[i * E:(i + 1) * E].t(), out=qkv[:, i * E:(i + 1) * E])
-        key_ = (B, L, pa.H, pa.D, tuple(pa.segs), tuple(pa.ratios))
+        key_ = (B, L, pa.H, pa.D, tuple(pa.segs), tuple(pa.ratios), act)
         if self._scratch is None or self._scratch.key != key_:
-            self._scratch = runtime.AttentionScratch(dev, B, L, pa.H, pa.D, pa.segs, pa.ratios)
-        merged = torch.empty(M, E, dtype=torch.bfloat16, device=dev)
+            self._scratch = runtime.AttentionScratch(dev, B, L, pa.H, pa.D, pa.segs, pa.ratios, act)
+        merged = torch.empty(M, E, dtype=act, device=dev)
         runtime.dilated_attention_core(pa, qkv, B, L, self._scratch, merged)
-        out = torch.addmm(pa.b_o_bf16, merged, pa.w_o.t())
+        out = torch.addmm(pa.b_o_act, merged, pa.w_o.t())
         return out.view(B, L, E).to(query.dtype), None

@@ -63,18 +63,20 @@ def test_argument_errors_are_reported_without_gpu():
     _lib_path()
     from gigapath import _hip
     lib = _hip.load_library()
-    rc = lib.gp_dilated_attn_fwd(None, None, None, 0, 1, 10, 16, 40, None, None, 1, None, None, 0.0, 0, None)
+    rc = lib.gp_dilated_attn_fwd(None, None, None, 0, 1, 10, 16, 40, None, None, 1, None, None, 0.0, 0, 0, None)
     assert rc == -1
     assert b"head dim 40" in lib.gp_last_error_string()
-    rc = lib.gp_residual_layernorm(None, None, None, None, None, 1e-5, None, 4, 100, None)
+    rc = lib.gp_residual_layernorm(None, None, None, None, None, 1e-5, None, 4, 100, 0, None)
     assert rc == -1 and b"cols=100" in lib.gp_last_error_string()
+    rc = lib.gp_gelu_layernorm(None, None, None, 1e-5, None, 4, 3072, 7, None)     # fmt: GP_FMT_BF16 / GP_FMT_F16
+    assert rc == -1 and b"bad fmt 7" in lib.gp_last_error_string()
     br = (_hip.GpAttnBranch * 1)(_hip.GpAttnBranch(1024, 1, 16, 16, 2304, 0, 0, 16, 16))
-    rc = lib.gp_dilated_attn_fwd_ex(16, 2304, 0, 1, 100, 16, 48, 50, 101, br, 1, 0.0, 0, None)
+    rc = lib.gp_dilated_attn_fwd_ex(16, 2304, 0, 1, 100, 16, 48, 50, 101, br, 1, 0.0, 0, 0, None)
     assert rc == -1 and b"bad window" in lib.gp_last_error_string()
     rc = lib.gp_dilated_sparsify(16, 2304, 768, 1536, 0, 10, 100, 16, 48, (ctypes.c_int32 * 1)(1024),
                                  (ctypes.c_int32 * 1)(3), 1, (ctypes.c_void_p * 1)(16), None, None)
     assert rc == -1 and b"H % r == 0" in lib.gp_last_error_string()
-    rc = lib.gp_branch_merge_ln_window(None, None, None, None, 1, 1, 100, 90, 20, 16, 48, None, None, 1e-5, None, None)
+    rc = lib.gp_branch_merge_ln_window(None, None, None, None, 1, 1, 100, 90, 20, 16, 48, None, None, 1e-5, None, 0, None)
     assert rc == -1
 
 
@@ -95,7 +97,7 @@ def test_varlen_plan_host_side():
     lib = _hip.load_library()
     assert lib.gp_varlen_plan_bytes(0, 5) == -1
     fake = (ctypes.c_uint8 * 64)()
-    rc = lib.gp_dilated_attn_fwd_varlen(fake, 16, 1, None)
+    rc = lib.gp_dilated_attn_fwd_varlen(fake, 16, 1, 0, None)
     assert rc == -1 and b"not a gp_varlen_plan" in lib.gp_last_error_string()
     L_bad = (ctypes.c_int64 * 1)(0)
     el = (ctypes.c_int64 * 5)()

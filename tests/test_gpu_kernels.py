@@ -116,7 +116,7 @@ def _run_attn(h, qkv, B, L, H, D, segs, ratios, prescaled=False):
     outs, lses = [], []
     for sl, r in zip(segs, ratios):
         geo = orc.branch_geometry(L, sl, r, H)
-        outs.append(torch.full((B * geo["nseg"] * geo["m"] * H * D,), float("nan"), dtype=torch.bfloat16, device=DEV))
+        outs.append(torch.full((B * geo["nseg"] * geo["m"] * H * D,), float("nan"), dtype=qkv.dtype, device=DEV))
         lses.append(torch.full((B * geo["nseg"] * H * geo["m"],), float("nan"), dtype=torch.float32, device=DEV))
     q = qkv.to(DEV)
     h.dilated_attn_fwd(q, q[:, E:], q[:, 2 * E:], 3 * E, B, L, H, D, segs, ratios, outs, lses, 0.0, prescaled)
@@ -315,10 +315,41 @@ def test_attention_other_head_dims(D):
         assert (o - o_ref).abs()[mask.expand(B, -1, -1, -1)].max().item() <= 1.2e-2
 
 
+@pytest.mark.parametrize("prescaled", [True, False])
+@pytest.mark.parametrize("name,B,L,segs,ratios", ATTN_CASES)
+def test_dilated_attention_fp16_vs_oracle(name, B, L, segs, ratios, prescaled):
+    """fp16 q/k/v (the forward under the reference pipeline's fp16 autocast): pre-scaled q runs the
+    LDS-DMA exact kernel (kModeExact, the product layout), otherwise the register-staged one.  P is
+    rounded to fp16 (11 significant bits): o within 2e-3, lse within 1.5e-3 of the fp32 oracle."""
+    h = _hip()
+    H, D = 16, 48
+    E = H * D
+    qkv = _rand_qkv(B, L, E, seed=L + 7).float()
+    sc = 0.6931471805599453 if prescaled else None
+    if prescaled:
+        qkv[:, :E] *= D ** -0.5 * 1.4426950408889634
+    qkv = qkv.half()
+    outs, lses = _run_attn(h, qkv, B, L, H, D, segs, ratios, prescaled=prescaled)
+    q, k, v = (qkv[:, i * E:(i + 1) * E].float().view(B, L, H, D) for i in range(3))
+    for b, (sl, r) in enumerate(zip(segs, ratios)):
+        o_ref, l_ref = orc.branch_attention(q, k, v, sl, r, **({"scale": sc} if sc else {}))
+        geo = orc.branch_geometry(L, sl, r, H)
+        assert outs[b].dtype == torch.float16
+        o = outs[b].float().cpu().view(B, geo["nseg"], geo["m"], H, D).permute(0, 1, 3, 2, 4)
+        l = lses[b].cpu().view(B, geo["nseg"], H, geo["m"])
+        need = _rows_needed(L, sl, r, H)
+        mask = torch.from_numpy(np.arange(geo["m"])[None, None, :] < need[:, :, None]).unsqueeze(0)
+        mask = mask.expand(B, -1, -1, -1)
+        assert torch.isfinite(o[mask]).all() and torch.isfinite(l[mask]).all(), (name, b)
+        assert (o - o_ref).abs()[mask].max().item() <= 2e-3 * max(1.0, o_ref.abs().max().item()), (name, b)
+        assert (l - l_ref).abs()[mask].max().item() <= 1.5e-3, (name, b)
+
+
 # ------------------------------------------------------------------ branch merge
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("name,B,L,segs,ratios", ATTN_CASES[:4])
 @pytest.mark.parametrize("with_ln", [False, True])
-def test_branch_merge_vs_oracle(name, B, L, segs, ratios, with_ln):
+def test_branch_merge_vs_oracle(name, B, L, segs, ratios, with_ln, dt):
     h = _hip()
     H, D = 16, 48
     E = H * D
@@ -326,7 +357,7 @@ def test_branch_merge_vs_oracle(name, B, L, segs, ratios, with_ln):
     outs, lses, outs_ref, lses_ref = [], [], [], []
     for sl, r in zip(segs, ratios):
         geo = orc.branch_geometry(L, sl, r, H)
-        o = torch.from_numpy(rng.standard_normal((B, geo["nseg"], geo["m"], H, D)).astype(np.float32)).bfloat16()
+        o = torch.from_numpy(rng.standard_normal((B, geo["nseg"], geo["m"], H, D)).astype(np.float32)).to(dt)
         l = torch.from_numpy((3 * rng.standard_normal((B, geo["nseg"], H, geo["m"]))).astype(np.float32))
         l.view(-1)[::97] = 0.0                       # exercise lse == 0 -> -1e8 (dilated_attention.py:46)
         outs.append(o.to(DEV).contiguous())
@@ -335,14 +366,15 @@ def test_branch_merge_vs_oracle(name, B, L, segs, ratios, with_ln):
         lses_ref.append(l)
     lw = torch.from_numpy((1 + 0.1 * rng.standard_normal(E)).astype(np.float32))
     lb = torch.from_numpy((0.1 * rng.standard_normal(E)).astype(np.float32))
-    out = torch.empty(B * L, E, dtype=torch.bfloat16, device=DEV)
+    out = torch.empty(B * L, E, dtype=dt, device=DEV)
     h.branch_merge_ln(outs, lses, segs, ratios, B, L, H, D, lw.to(DEV) if with_ln else None,
                       lb.to(DEV) if with_ln else None, 1e-5, out)
     ref = orc.merge_branches(outs_ref, lses_ref, L, segs, ratios)
     if with_ln:
         ref = torch.nn.functional.layer_norm(ref, (E,), lw, lb, 1e-5)
     got = out.float().cpu().view(B, L, E)
-    assert (got - ref).abs().max().item() <= 2 ** -7 * max(1.0, ref.abs().max().item())
+    ulp = 2 ** -7 if dt == torch.bfloat16 else 2 ** -10        # one rounding of the output format
+    assert (got - ref).abs().max().item() <= ulp * max(1.0, ref.abs().max().item())
 
 
 # ------------------------------------------------------------------ row kernels
@@ -360,6 +392,50 @@ def test_gelu_layernorm_grid_stride_rows(F):
     ref = torch.nn.functional.layer_norm(torch.nn.functional.gelu(f.float()).bfloat16().float(), (F,), fw, fb, 1e-5)
     err = (fd.float().cpu() - ref).abs().max().item()
     assert err <= 2 ** -8 * ref.abs().max().item(), err
+
+
+@pytest.mark.parametrize("F", [3072, 6144])
+def test_fp16_row_kernels(F):
+    """fp16 activations: residual + LN, GELU + LN (fp16 lookup table for F = 3072, per-element GELU
+    for 6144; GELU rounded to fp16 before the LN as gelu(x.float()).type_as(x) does) and the
+    pos-embed + CLS + LN1 kernel, against torch fp32 with one fp16 output rounding."""
+    h = _hip()
+    rng = np.random.default_rng(F)
+    M, E = 1111, 768
+    x = torch.from_numpy(rng.standard_normal((M, E)).astype(np.float32))
+    y = torch.from_numpy(rng.standard_normal((M, E)).astype(np.float32)).half()
+    bias = torch.from_numpy(rng.standard_normal(E).astype(np.float32))
+    w = torch.from_numpy((1 + 0.1 * rng.standard_normal(E)).astype(np.float32))
+    b = torch.from_numpy((0.1 * rng.standard_normal(E)).astype(np.float32))
+    xd = x.to(DEV)
+    ln = torch.empty(M, E, dtype=torch.float16, device=DEV)
+    h.residual_layernorm(xd, y.to(DEV), bias.to(DEV), w.to(DEV), b.to(DEV), 1e-5, ln, M, E)
+    x_ref = x + (y.float() + bias)
+    assert torch.equal(xd.cpu(), x_ref)
+    ln_ref = torch.nn.functional.layer_norm(x_ref, (E,), w, b, 1e-5)
+    assert (ln.float().cpu() - ln_ref).abs().max().item() <= 2 ** -10 * ln_ref.abs().max().item()
+
+    f = torch.from_numpy((2 * rng.standard_normal((M, F))).astype(np.float32)).half()
+    fw = torch.from_numpy((1 + 0.1 * rng.standard_normal(F)).astype(np.float32))
+    fb = torch.from_numpy((0.1 * rng.standard_normal(F)).astype(np.float32))
+    fd = f.to(DEV)
+    h.gelu_layernorm(fd, fw.to(DEV), fb.to(DEV), 1e-5, fd, M, F)     # in place
+    f_ref16 = torch.nn.functional.layer_norm(torch.nn.functional.gelu(f.float()).half().float(), (F,), fw, fb, 1e-5)
+    assert (fd.float().cpu() - f_ref16).abs().max().item() <= 2 ** -9 * f_ref16.abs().max().item()
+
+    G, N = 1000, 257
+    xp = torch.from_numpy(rng.standard_normal((N, E)).astype(np.float32)).half()
+    pos = rng.integers(1, G * G + 1, N).astype(np.int64)
+    tab = orc.sincos_axis_table(E, G)
+    cls = torch.from_numpy(rng.standard_normal(E).astype(np.float32))
+    x_out = torch.empty(N + 1, E, device=DEV)
+    a_out = torch.empty(N + 1, E, dtype=torch.float16, device=DEV)
+    h.posembed_cls_ln(xp.to(DEV), torch.from_numpy(pos).to(DEV), torch.from_numpy(tab).to(DEV), cls.to(DEV), 1, N,
+                      E, G, w.to(DEV), b.to(DEV), 1e-5, x_out, a_out)
+    xr = torch.cat([cls[None], xp.float() + torch.from_numpy(orc.pos_embed_rows(pos, tab, G))], 0)
+    assert torch.equal(x_out.cpu(), xr)          # fp16 -> fp32 is exact, the add is the oracle's
+    ar = torch.nn.functional.layer_norm(xr, (E,), w, b, 1e-5)
+    assert (a_out.float().cpu() - ar).abs().max().item() <= 2 ** -10 * ar.abs().max().item()
 
 
 def test_residual_gelu_layernorm_kernels():
