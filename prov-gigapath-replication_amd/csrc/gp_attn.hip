@@ -463,6 +463,9 @@ static_assert(kNWFast == 4 || kNWFast == 8 || kNWFast == 16, "GP_ATTN_NW must be
 // GP_ATTN_ONES_SPARSE: the V image's spare d-block carries 1.0 only in the two rows the epilogue reads
 // (d = 48 and 52) and 0 elsewhere: same outputs, fewer toggling MFMA operand bits (same-box A/B
 // 1.276 -> 1.262 ms per 70k layer, profiles/r02_s6_ab_ones.json)
+#ifndef GP_ATTN_SKIP_IDLE
+#define GP_ATTN_SKIP_IDLE 1
+#endif
 #ifndef GP_ATTN_ONES_SPARSE
 #define GP_ATTN_ONES_SPARSE 1
 #endif
@@ -662,6 +665,10 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   }
   // one 64-key tile; SET = the tile's LDS buffer when the loop is unrolled by two (kDMA), so the
   // buffer offsets fold into the ds_read immediates
+  // GP_ATTN_SKIP_IDLE: a wave whose 32 queries all lie at or past the last needed row (the tail
+  // q-block of a segment) skips the MFMAs and the softmax -- its outputs are never stored -- and
+  // only issues its share of the K/V staging and the barriers (~2 % of the wave-tiles at 70k)
+  const bool wact = !GP_ATTN_SKIP_IDLE || __builtin_amdgcn_readfirstlane(q0 + w * 32) < rows_needed;
   auto tile_step = [&](int t, auto setc) {
     constexpr int SET = decltype(setc)::value;
     if (t + 1 < ntiles) load_tile((t + 1) * KT);
@@ -669,162 +676,164 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
     const int bsel = kDMA ? SET : (t & 1);
     const char* Kb = smem + bsel * BUF;
     const char* Vb = smem + bsel * BUF + KTILE;
-    // ---- S^T for two 32-key sub-tiles.  kPre (q pre-multiplied by scale*log2 e): the
-    // accumulator starts at -m_run, so it already holds log2-domain scores minus the max.
-    f32x16 sacc[2];
-    f32x16 ini;
-    if constexpr (kMI) {
-      f32x16 zero;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) zero[r] = 0.f;
-      ini = __builtin_amdgcn_mfma_f32_32x32x16_bf16(onesA, mqB, zero, 0, 0, 0);
-    }
-    const float init = (kPre && !kZM && !kMI && t > 0) ? -m_run : 0.f;
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      f32x16 acc;
+    if (wact) {   // (GP_ATTN_SKIP_IDLE) waves with no needed query only stage K/V and join the barriers
+      // ---- S^T for two 32-key sub-tiles.  kPre (q pre-multiplied by scale*log2 e): the
+      // accumulator starts at -m_run, so it already holds log2-domain scores minus the max.
+      f32x16 sacc[2];
+      f32x16 ini;
       if constexpr (kMI) {
-        acc = ini;
-      } else {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[r] = init;
+        f32x16 zero;
+  #pragma unroll
+        for (int r = 0; r < 16; ++r) zero[r] = 0.f;
+        ini = __builtin_amdgcn_mfma_f32_32x32x16_bf16(onesA, mqB, zero, 0, 0, 0);
       }
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const bf16x8 kk = *reinterpret_cast<const bf16x8*>(Kb + (32 * u + l32) * KROWB + 32 * ks + 16 * h);
-        acc = mfma_32x32x16<kH>(kk, qf[ks], acc);
+      const float init = (kPre && !kZM && !kMI && t > 0) ? -m_run : 0.f;
+  #pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        f32x16 acc;
+        if constexpr (kMI) {
+          acc = ini;
+        } else {
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) acc[r] = init;
+        }
+  #pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          const bf16x8 kk = *reinterpret_cast<const bf16x8*>(Kb + (32 * u + l32) * KROWB + 32 * ks + 16 * h);
+          acc = mfma_32x32x16<kH>(kk, qf[ks], acc);
+        }
+        sacc[u] = acc;
       }
-      sacc[u] = acc;
-    }
-    if (kv0 + 64 > c) {      // keys >= c are zero pads (added analytically at the end)
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (kv0 + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * h >= c) sacc[u][r] = -INFINITY;
-    }
+      if (kv0 + 64 > c) {      // keys >= c are zero pads (added analytically at the end)
+  #pragma unroll
+        for (int u = 0; u < 2; ++u)
+  #pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (kv0 + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * h >= c) sacc[u][r] = -INFINITY;
+      }
 
-    // ---- online softmax with deferred rescale (two independent max chains)
-    float mx = 0.f;
-    if constexpr (!kZM) {
-      float mxa = sacc[0][0], mxb = sacc[1][0];
-#pragma unroll
-      for (int r = 1; r < 16; ++r) {
-        mxa = fmaxf(mxa, sacc[0][r]);
-        mxb = fmaxf(mxb, sacc[1][r]);
-      }
-      mx = fmaxf(mxa, mxb);
-      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-      mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
-    }
-    bf16x8 pf[2][2];
-    if constexpr (kPre) {
+      // ---- online softmax with deferred rescale (two independent max chains)
+      float mx = 0.f;
       if constexpr (!kZM) {
-        // scores are s*c - m_run; rescale only when a query's max moved up by > kThr
-        // (tile 0: always, which sets m_run to that tile's exact max)
-        const bool need = (t == 0) || (mx > kThr);
+        float mxa = sacc[0][0], mxb = sacc[1][0];
+  #pragma unroll
+        for (int r = 1; r < 16; ++r) {
+          mxa = fmaxf(mxa, sacc[0][r]);
+          mxb = fmaxf(mxb, sacc[1][r]);
+        }
+        mx = fmaxf(mxa, mxb);
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+        mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+      }
+      bf16x8 pf[2][2];
+      if constexpr (kPre) {
+        if constexpr (!kZM) {
+          // scores are s*c - m_run; rescale only when a query's max moved up by > kThr
+          // (tile 0: always, which sets m_run to that tile's exact max)
+          const bool need = (t == 0) || (mx > kThr);
+          if (__builtin_amdgcn_ballot_w64(need)) {
+            if constexpr (kMI) {
+              // m kept as an exact hi + lo pair of bf16 values (two rows of the init MFMA), so it
+              // tracks the max to ~2^-16 relative and numerator and denominator stay consistent
+              const float m_old = (t == 0) ? 0.f : m_run;
+              float m_new = m_old;
+              if (need) {
+                const float tt = -(m_old + mx);
+                const __bf16 hi = (__bf16)tt;
+                const __bf16 lo = (__bf16)(tt - (float)hi);
+                m_new = -((float)hi + (float)lo);
+              }
+              const float d = m_new - m_old;
+              if (t > 0) {
+                const float alpha = fast_exp2(-d);
+  #pragma unroll
+                for (int mt = 0; mt < 2; ++mt)
+  #pragma unroll
+                  for (int r = 0; r < 16; ++r) oacc[mt][r] *= alpha;
+                lsum *= alpha;
+              }
+              m_run = m_new;
+  #pragma unroll
+              for (int u = 0; u < 2; ++u)
+  #pragma unroll
+                for (int r = 0; r < 16; ++r) sacc[u][r] -= d;
+              if (h == 0) {
+                const __bf16 hi = (__bf16)(-m_run);
+                mqB[0] = hi;
+                mqB[1] = (__bf16)(-m_run - (float)hi);
+              }
+            } else {
+              const float delta = need ? mx : 0.f;
+              const float alpha = fast_exp2(-delta);
+              if (t > 0) {
+  #pragma unroll
+                for (int mt = 0; mt < 2; ++mt)
+  #pragma unroll
+                  for (int r = 0; r < 16; ++r) oacc[mt][r] *= alpha;
+                lsum *= alpha;
+              }
+              m_run = (t == 0) ? delta : m_run + delta;
+  #pragma unroll
+              for (int u = 0; u < 2; ++u)
+  #pragma unroll
+                for (int r = 0; r < 16; ++r) sacc[u][r] -= delta;
+            }
+          }
+        }
+  #pragma unroll
+        for (int u = 0; u < 2; ++u)
+  #pragma unroll
+          for (int s = 0; s < 2; ++s)
+  #pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float p = fast_exp2(sacc[u][8 * s + e]);
+              if constexpr (!kOnes) lsum += p;
+              pf[u][s][e] = f2e_slot<kH>(p);
+            }
+      } else {
+        const float tm = mx * a.c_log2;
+        const bool need = tm > m_run + kThr;
         if (__builtin_amdgcn_ballot_w64(need)) {
-          if constexpr (kMI) {
-            // m kept as an exact hi + lo pair of bf16 values (two rows of the init MFMA), so it
-            // tracks the max to ~2^-16 relative and numerator and denominator stay consistent
-            const float m_old = (t == 0) ? 0.f : m_run;
-            float m_new = m_old;
-            if (need) {
-              const float tt = -(m_old + mx);
-              const __bf16 hi = (__bf16)tt;
-              const __bf16 lo = (__bf16)(tt - (float)hi);
-              m_new = -((float)hi + (float)lo);
+          const float m_new = need ? tm : m_run;
+          const float alpha = fast_exp2(m_run - m_new);
+  #pragma unroll
+          for (int mt = 0; mt < 2; ++mt)
+  #pragma unroll
+            for (int r = 0; r < 16; ++r) oacc[mt][r] *= alpha;
+          lsum *= alpha;
+          m_run = m_new;
+        }
+  #pragma unroll
+        for (int u = 0; u < 2; ++u)
+  #pragma unroll
+          for (int s = 0; s < 2; ++s)
+  #pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float p = fast_exp2(fmaf(sacc[u][8 * s + e], a.c_log2, -m_run));
+              if constexpr (!kOnes) lsum += p;
+              pf[u][s][e] = f2e_slot<kH>(p);
             }
-            const float d = m_new - m_old;
-            if (t > 0) {
-              const float alpha = fast_exp2(-d);
-#pragma unroll
-              for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) oacc[mt][r] *= alpha;
-              lsum *= alpha;
-            }
-            m_run = m_new;
-#pragma unroll
-            for (int u = 0; u < 2; ++u)
-#pragma unroll
-              for (int r = 0; r < 16; ++r) sacc[u][r] -= d;
-            if (h == 0) {
-              const __bf16 hi = (__bf16)(-m_run);
-              mqB[0] = hi;
-              mqB[1] = (__bf16)(-m_run - (float)hi);
-            }
-          } else {
-            const float delta = need ? mx : 0.f;
-            const float alpha = fast_exp2(-delta);
-            if (t > 0) {
-#pragma unroll
-              for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) oacc[mt][r] *= alpha;
-              lsum *= alpha;
-            }
-            m_run = (t == 0) ? delta : m_run + delta;
-#pragma unroll
-            for (int u = 0; u < 2; ++u)
-#pragma unroll
-              for (int r = 0; r < 16; ++r) sacc[u][r] -= delta;
+      }
+
+      // ---- O^T += V^T . P^T  (2 sub-tiles x 2 k-steps x 2 d-tiles)
+  #pragma unroll
+      for (int u = 0; u < 2; ++u)
+  #pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const int row = 32 * u + 16 * s + 4 * (lane >> 5) + ((lane >> 2) & 3);
+  #pragma unroll
+          for (int mt = 0; mt < 2; ++mt) {
+            const int blk = 2 * mt + ((lane >> 4) & 1);
+            const char* p0 = Vb + row * VROWB + 32 * (blk ^ (row & 3)) + 8 * (lane & 3);
+            const char* p1 = p0 + 8 * VROWB;   // rows + 8 keep (row & 3)
+            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
+            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p1);
+            const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+            oacc[mt] = mfma_32x32x16<kH>(vf, pf[u][s], oacc[mt]);
           }
         }
-      }
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float p = fast_exp2(sacc[u][8 * s + e]);
-            if constexpr (!kOnes) lsum += p;
-            pf[u][s][e] = f2e_slot<kH>(p);
-          }
-    } else {
-      const float tm = mx * a.c_log2;
-      const bool need = tm > m_run + kThr;
-      if (__builtin_amdgcn_ballot_w64(need)) {
-        const float m_new = need ? tm : m_run;
-        const float alpha = fast_exp2(m_run - m_new);
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) oacc[mt][r] *= alpha;
-        lsum *= alpha;
-        m_run = m_new;
-      }
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float p = fast_exp2(fmaf(sacc[u][8 * s + e], a.c_log2, -m_run));
-            if constexpr (!kOnes) lsum += p;
-            pf[u][s][e] = f2e_slot<kH>(p);
-          }
+
     }
-
-    // ---- O^T += V^T . P^T  (2 sub-tiles x 2 k-steps x 2 d-tiles)
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int row = 32 * u + 16 * s + 4 * (lane >> 5) + ((lane >> 2) & 3);
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
-          const int blk = 2 * mt + ((lane >> 4) & 1);
-          const char* p0 = Vb + row * VROWB + 32 * (blk ^ (row & 3)) + 8 * (lane & 3);
-          const char* p1 = p0 + 8 * VROWB;   // rows + 8 keep (row & 3)
-          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
-          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p1);
-          const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-          oacc[mt] = mfma_32x32x16<kH>(vf, pf[u][s], oacc[mt]);
-        }
-      }
-
     if (t + 1 < ntiles) store_tile((t + 1) & 1);
     if constexpr (kDMA) __builtin_amdgcn_s_waitcnt(0x0f70);   // this wave's DMA pieces landed
     __syncthreads();
