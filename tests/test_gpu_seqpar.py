@@ -33,7 +33,7 @@ def _model(max_wsi_size):
     return m.cuda().eval()
 
 
-def _worker(rank, world, port, N, max_wsi_size, global_pool, q, graphs=True):
+def _worker(rank, world, port, N, max_wsi_size, global_pool, q, graphs=True, half=False):
     try:
         import torch.distributed as dist
         import oracle as orc
@@ -45,7 +45,9 @@ def _worker(rank, world, port, N, max_wsi_size, global_pool, q, graphs=True):
         x, coords = orc.synthetic_slide(N)
         xt, ct = torch.from_numpy(x).cuda(), torch.from_numpy(coords).cuda()
         model.enable_sequence_parallel()
-        with torch.no_grad():
+        if half:      # the reference pipeline's autocast(float16) caller: fp16 compute on every shard
+            xt = xt.half()
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.float16, enabled=half):
             out = torch.stack(model(xt, ct, all_layer_embed=True)).cpu().numpy()
             last = model(xt, ct)[0].cpu().numpy()
             # per-layer compute segments as HIP-graph replays: bit-identical to the eager shard
@@ -62,11 +64,12 @@ def _worker(rank, world, port, N, max_wsi_size, global_pool, q, graphs=True):
         q.put((rank, traceback.format_exc()))
 
 
-def _run_ranks(world, N, max_wsi, gp, graphs=True):
+def _run_ranks(world, N, max_wsi, gp, graphs=True, half=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, N, max_wsi, gp, q, graphs)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, N, max_wsi, gp, q, graphs, half))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=300) for _ in range(world))
@@ -114,6 +117,30 @@ def test_sequence_parallel_matches_single_device(world, N, max_wsi, gp):
             for idx in np.ndindex(*want.shape[:-1]):
                 rel, cos, ok = close_enough(res[r][0][idx], want[idx])
                 assert ok, (r, idx, rel, cos)
+
+
+def test_sequence_parallel_fp16_autocast():
+    """Sequence parallel under the fp16 autocast caller: every shard computes in fp16 (fp16 sparsified
+    K/V exchange, kModeExact attention windows), equal to the single-device fp16 forward up to the
+    GEMMs' row-count rounding, and within the model tolerance of the fp32 oracle."""
+    import oracle as orc
+    N, world = 5000, 2
+    res = _run_ranks(world, N, 262144, False, half=True)
+    model = _model(262144)
+    x, coords = orc.synthetic_slide(N)
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.float16):
+        ref = torch.stack(model(torch.from_numpy(x).cuda().half(), torch.from_numpy(coords).cuda(),
+                                all_layer_embed=True)).cpu().numpy()
+    cfg = orc.arch_config("gigapath_slide_enc12l768d", max_wsi_size=262144)
+    Wt = {k: torch.from_numpy(v) for k, v in orc.make_weights(cfg, seed=0).items()}
+    want = torch.stack(orc.slide_encoder_forward(Wt, x, coords, cfg, all_layer_embed=True)).numpy()
+    from test_gpu_model import close_enough
+    for r in range(world):
+        d, cos, ok = _sp_close(res[r][0], ref)
+        assert ok, (r, d, cos)
+        for idx in np.ndindex(*want.shape[:-1]):
+            rel, cos, ok = close_enough(res[r][0][idx], want[idx])
+            assert ok, (r, idx, rel, cos)
 
 
 @pytest.mark.timeout(600)
