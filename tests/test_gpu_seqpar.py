@@ -119,6 +119,50 @@ def test_sequence_parallel_matches_single_device(world, N, max_wsi, gp):
                 assert ok, (r, idx, rel, cos)
 
 
+def _rccl_worker(port, N, q):
+    try:
+        import torch.distributed as dist
+        import oracle as orc
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+        model = _model(262144)
+        x, coords = orc.synthetic_slide(N)
+        xt, ct = torch.from_numpy(x).cuda(), torch.from_numpy(coords).cuda()
+        model.enable_sequence_parallel()
+        assert model._sp.exchange.device_comm          # the RCCL transport, not the host-staged one
+        with torch.no_grad():
+            single = torch.stack(model(xt, ct, all_layer_embed=True)).cpu().numpy()   # world 1: 1-GPU path
+            eager = torch.stack(model._forward_sp(xt, ct, True)).cpu().numpy()
+            model.use_hip_graphs = True
+            graphs = [torch.stack(model._forward_sp(xt, ct, True)).cpu().numpy() for _ in range(2)]
+        torch.cuda.synchronize()
+        dist.destroy_process_group()
+        q.put((eager, graphs, single))
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put(traceback.format_exc())
+
+
+def test_sequence_parallel_rccl_transport_single_rank():
+    """The sharded engine over the RCCL ("nccl") backend, forced on one rank (RCCL refuses two ranks
+    on one GPU, and this pool's boxes have one): every per-layer sparsified K/V all_to_all_single,
+    the async handles' stream waits, the all-reduce / broadcast of the readout and the HIP-graph
+    segments between the collectives run through RCCL; the result equals the single-device forward."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), 3000, q))
+    p.start()
+    res = q.get(timeout=300)
+    p.join(timeout=60)
+    assert not isinstance(res, str), res
+    eager, graphs, single = res
+    d, cos, ok = _sp_close(eager, single)
+    assert ok, (d, cos)
+    for g in graphs:
+        assert np.array_equal(g, eager)
+
+
 def test_sequence_parallel_fp16_autocast():
     """Sequence parallel under the fp16 autocast caller: every shard computes in fp16 (fp16 sparsified
     K/V exchange, kModeExact attention windows), equal to the single-device fp16 forward up to the
