@@ -42,7 +42,8 @@ def use_tuned_gemms(dev=None):
     shapes (PyTorch TunableOp, tuning itself off).  Shapes not in the file keep hipBLASLt's
     default heuristic.  GIGAPATH_NO_TUNED_GEMMS=1 disables it."""
     global _tuned_loaded
-    if _tuned_loaded or os.environ.get("GIGAPATH_NO_TUNED_GEMMS") == "1" or not os.path.exists(_TUNED):
+    path = os.environ.get("GIGAPATH_TUNED_GEMMS_FILE", _TUNED)     # an alternative tuning (A/B runs)
+    if _tuned_loaded or os.environ.get("GIGAPATH_NO_TUNED_GEMMS") == "1" or not os.path.exists(path):
         return
     if dev is None or torch.device(dev).type != "cuda":
         return
@@ -50,7 +51,7 @@ def use_tuned_gemms(dev=None):
     torch.cuda.tunable.enable(True)
     torch.cuda.tunable.tuning_enable(False)
     torch.cuda.tunable.record_untuned_enable(False)
-    torch.cuda.tunable.read_file(_TUNED)
+    torch.cuda.tunable.read_file(path)
 
 
 _ACT = threading.local()

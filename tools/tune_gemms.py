@@ -73,6 +73,10 @@ def main():
     ap.add_argument("--packed-slides", type=int, default=32)
     ap.add_argument("--out", default=OUT)
     ap.add_argument("--list", action="store_true", help="print the --sp-tiles shapes and exit (no GPU)")
+    ap.add_argument("--rotating-mb", type=int, default=0,
+                    help="TunableOp rotating buffer: time each candidate on operands cycled through this many MB "
+                         "(cold caches, as inside the forward) instead of the same warm operands")
+    ap.add_argument("--fresh", action="store_true", help="do not start from the entries already in --out")
     args = ap.parse_args()
     log = lambda s: print(s, flush=True)  # noqa: E731
     shapes = sp_shapes(args.sp_tiles, args.sp_worlds) if args.sp_tiles else []
@@ -87,7 +91,9 @@ def main():
     torch.cuda.tunable.tuning_enable(True)
     torch.cuda.tunable.set_max_tuning_duration(60)
     torch.cuda.tunable.set_max_tuning_iterations(30)
-    if os.path.exists(args.out):
+    if args.rotating_mb:
+        torch.cuda.tunable.set_rotating_buffer_size(args.rotating_mb)
+    if os.path.exists(args.out) and not args.fresh:
         torch.cuda.tunable.read_file(args.out)
     torch.cuda.tunable.set_filename(args.out + ".exit.csv", False)   # TunableOp's own copy at exit
     n0 = len(torch.cuda.tunable.get_results())
