@@ -321,8 +321,10 @@ def test_hip_graph_replay_matches_eager(model):
 
 
 @pytest.mark.parametrize("arch", ["gigapath_slide_enc24l1024d", "gigapath_slide_enc12l1536d"])
-def test_other_registered_archs_vs_oracle(arch):
-    """24L1024d (D = 64) and 12L1536d (D = 96) end to end against the fp32 oracle."""
+@pytest.mark.parametrize("half", [False, True])
+def test_other_registered_archs_vs_oracle(arch, half):
+    """24L1024d (D = 64) and 12L1536d (D = 96) end to end against the fp32 oracle, in bf16 and under
+    the fp16 autocast caller (their register-staged fp16 attention kernels, F = 4096 / 6144 fp16 GELU)."""
     from gigapath import slide_encoder
     cfg = orc.arch_config(arch)
     m = slide_encoder.create_model("", arch, 1536)
@@ -330,9 +332,10 @@ def test_other_registered_archs_vs_oracle(arch):
     m.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()}, strict=True)
     m = m.to(DEV).eval()
     x, coords = orc.synthetic_slide(700)
-    with torch.no_grad():
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.float16, enabled=half):
         got = torch.stack(m(torch.from_numpy(x).to(DEV), torch.from_numpy(coords).to(DEV),
                             all_layer_embed=True)).cpu().numpy()
+        assert m.encoder.engine.ws.qkv.dtype == (torch.float16 if half else torch.bfloat16)
     Wt = {k: torch.from_numpy(v) for k, v in W.items()}
     ref = torch.stack(orc.slide_encoder_forward(Wt, x, coords, cfg, all_layer_embed=True)).numpy()
     for idx in np.ndindex(*got.shape[:-1]):
