@@ -463,6 +463,9 @@ static_assert(kNWFast == 4 || kNWFast == 8 || kNWFast == 16, "GP_ATTN_NW must be
 // GP_ATTN_ONES_SPARSE: the V image's spare d-block carries 1.0 only in the two rows the epilogue reads
 // (d = 48 and 52) and 0 elsewhere: same outputs, fewer toggling MFMA operand bits (same-box A/B
 // 1.276 -> 1.262 ms per 70k layer, profiles/r02_s6_ab_ones.json)
+#ifndef GP_ATTN_PV16
+#define GP_ATTN_PV16 0
+#endif
 #ifndef GP_ATTN_SKIP_IDLE
 #define GP_ATTN_SKIP_IDLE 1
 #endif
@@ -480,7 +483,11 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   constexpr int QB = NW * 32;                // query rows per workgroup
   constexpr int KT = 64;                     // keys per staged tile
   constexpr int KS = D / 16;                 // k-steps of Q.K^T
-  constexpr bool kOnes = (D % 32) != 0;      // spare d rows carry the row-sum ones
+  // GP_ATTN_PV16 (lab A/B of the verdict's 16x16x32 question): P.V of the fast kernel on
+  // v_mfma_f32_16x16x32 over the 3 real d-blocks (no padding; P regrouped by v_permlane16_swap), the
+  // row sum by VALU adds of the fp32 p
+  constexpr bool kPV16 = GP_ATTN_PV16 != 0 && MODE == kModeFast && D == 48;
+  constexpr bool kOnes = (D % 32) != 0 && !kPV16;   // spare d rows carry the row-sum ones
   constexpr bool kDMA = MODE != kModeGen;
   constexpr bool kZM = MODE == kModeFast;    // no max, no offset
   constexpr bool kMI = MODE == kModeFix;     // -m start block from one MFMA
@@ -642,11 +649,16 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   }
   float m_run = -INFINITY;   // running max, log2 domain, of query l32
   float lsum = 0.f;          // row sum (VALU path, D % 32 == 0 only)
-  f32x16 oacc[2];
+  f32x16 oacc[kPV16 ? 1 : 2];
 #pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
+  for (int mt = 0; mt < (kPV16 ? 1 : 2); ++mt)
 #pragma unroll
     for (int r = 0; r < 16; ++r) oacc[mt][r] = 0.f;
+  f32x4 o16[2][3];              // kPV16: O^T blocks [query half][d-block]
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+    for (int dt = 0; dt < 3; ++dt) o16[nb][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int ntiles = (c + KT - 1) / KT;
   if (ntiles > 0) {
@@ -816,6 +828,33 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
       }
 
       // ---- O^T += V^T . P^T  (2 sub-tiles x 2 k-steps x 2 d-tiles)
+      if constexpr (kPV16) {
+        // pf[u][s] lane (h, j) holds keys 16s + 8(e/4) + 4h + e%4 of query j; one permlane16_swap per
+        // dword pair gives x = queries 0-15, y = queries 16-31, 16-lane group G = (s = G&1, h = G>>1):
+        // the 16x16x32 B operand (n = lane % 16, k-slots of group G)
+        typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+  #pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          u32x4v xa = __builtin_bit_cast(u32x4v, pf[u][0]), ya = __builtin_bit_cast(u32x4v, pf[u][1]);
+  #pragma unroll
+          for (int d = 0; d < 4; ++d) {
+            const auto r = __builtin_amdgcn_permlane16_swap(xa[d], ya[d], false, false);
+            xa[d] = r[0];
+            ya[d] = r[1];
+          }
+          const bf16x8 bq[2] = {__builtin_bit_cast(bf16x8, xa), __builtin_bit_cast(bf16x8, ya)};
+          const int row = 32 * u + 16 * ((lane >> 4) & 1) + 4 * (lane >> 5) + ((lane >> 2) & 3);
+  #pragma unroll
+          for (int dt = 0; dt < 3; ++dt) {
+            const char* p0 = Vb + row * VROWB + 32 * (dt ^ (row & 3)) + 8 * (lane & 3);
+            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
+            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0 + 8 * VROWB));
+            const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  #pragma unroll
+            for (int nb = 0; nb < 2; ++nb) o16[nb][dt] = mfma_16x16x32<kH>(vf, bq[nb], o16[nb][dt]);
+          }
+        }
+      } else
   #pragma unroll
       for (int u = 0; u < 2; ++u)
   #pragma unroll
@@ -874,7 +913,23 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   }
   const float inv = so / l;
   const int i = q0 + w * 32 + l32;
-  if constexpr (GP_ATTN_WIDE_STORE != 0) {
+  if constexpr (kPV16) {
+    // lane (G = lane / 16, c = lane % 16) holds O^T rows 16dt + 4G + 0..3 of queries c and c + 16
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      const int qq = (lane & 15) + 16 * nb;
+      const float iv = __shfl(inv, qq, 64);
+      const int iq = q0 + w * 32 + qq;
+      if (iq < rows_needed) {
+        uint16_t* orow = brr.o + (((int64_t)bn * g.m + iq) * a.H + hh) * (int64_t)D + 4 * (lane >> 4);
+#pragma unroll
+        for (int dt = 0; dt < 3; ++dt) {
+          float vv[4] = {o16[nb][dt][0] * iv, o16[nb][dt][1] * iv, o16[nb][dt][2] * iv, o16[nb][dt][3] * iv};
+          store_e<kH, 4>(orow + 16 * dt, vv);
+        }
+      }
+    }
+  } else if constexpr (GP_ATTN_WIDE_STORE != 0) {
     // lane (q, h) holds d = 8k + 4h .. +3 for the D/8 groups k.  For each pair of groups (k, k+1)
     // one permlane32_swap per dword gives lanes 0-31 d = 8k .. 8k+7 and lanes 32-63 d = 8k+8 .. 8k+15
     // (T21): one 16-byte store per pair.  The swap needs EXEC full: it runs before the row check.

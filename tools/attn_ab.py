@@ -98,6 +98,12 @@ def main():
                     else:
                         ident[(p, name)] = all(torch.equal(a.view(torch.uint8), b.view(torch.uint8))
                                                for a, b in zip(outs, ref[name]))
+                        if not ident[(p, name)]:       # a variant with other arithmetic: how far off
+                            no = len(sc.outs)
+                            dif = [(a.float() - b.float()).abs().nan_to_num(0.0, 0.0, 0.0).max().item()
+                                   for a, b in zip(outs, ref[name])]
+                            print("%s br=%s: max |d o| %.3e, max |d lse| %.3e vs the first build" %
+                                  (p, name, max(dif[:no]), max(dif[no:])))
                     continue
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
