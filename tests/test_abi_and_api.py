@@ -200,3 +200,37 @@ def test_classification_head_surface():
     head.train()
     assert head.training and not head.slide_encoder.training
     assert sum(p.requires_grad for p in head.parameters()) == 2      # classifier weight + bias
+
+
+def test_activation_format_selection():
+    """runtime.call_act_dtype / compute_format: bf16 by default, fp16 for an fp16 model (the
+    reference pipeline's autocast(float16) case is covered on the GPU, where autocast("cuda") is
+    live); nested decorated calls keep the outer call's format; _hip.fmt_of maps the dtypes the C ABI
+    accepts and rejects the rest."""
+    _lib_path()
+    import torch.nn as nn
+    from gigapath import _hip, runtime
+    lin = nn.Linear(4, 4)
+    assert runtime.call_act_dtype(lin) == torch.bfloat16
+    assert runtime.call_act_dtype(lin.half()) == torch.float16
+    assert runtime.act_dtype() == torch.bfloat16                 # outside any decorated call
+
+    class M(nn.Module):
+        def __init__(self, half):
+            super().__init__()
+            self.p = nn.Parameter(torch.zeros(1, dtype=torch.float16 if half else torch.float32))
+
+        @runtime.compute_format
+        def forward(self, inner=None):
+            seen = [runtime.act_dtype()]
+            if inner is not None:
+                seen += inner()
+            return seen
+
+    assert M(True)() == [torch.float16]
+    assert M(True)(inner=M(False)) == [torch.float16, torch.float16]      # the outer call decides
+    assert M(False)(inner=M(True)) == [torch.bfloat16, torch.bfloat16]
+    assert runtime.act_dtype() == torch.bfloat16
+    assert (_hip.fmt_of(torch.bfloat16), _hip.fmt_of(torch.float16)) == (_hip.FMT_BF16, _hip.FMT_F16)
+    with pytest.raises(TypeError):
+        _hip.fmt_of(torch.float32)
