@@ -249,6 +249,10 @@ __global__ __launch_bounds__(256) void gelu_ln_wave2_kernel(const uint16_t* h, c
 // kCopy: the table is copied into LDS from g_gelu_tab (filled once per device by gelu_tab_fill_kernel,
 // the same arithmetic, so the entries are bit-identical) -- 128 KiB from L2 instead of 65,536 gelu_erf
 // evaluations per block (~8 % of the launch at 70k rows).  Without kCopy each block evaluates the table.
+// GP_GELU_NW: waves per block of the lookup-table kernel (one block per CU: the table fills the LDS)
+#ifndef GP_GELU_NW
+#define GP_GELU_NW 8
+#endif
 // One table per format (index: the input's 16 bits; entry: gelu_erf rounded to the same format).
 __device__ __attribute__((aligned(16))) uint16_t g_gelu_tab[2][65536];
 
@@ -507,11 +511,11 @@ extern "C" int gp_gelu_layernorm(const uint16_t* h, const float* ln_w, const flo
   if (cols == 3072 || cols == 4096) {
     // GELU by lookup table (the table + LN weights fit in LDS): one block per CU, the table copied
     // from g_gelu_tab, or evaluated per block while a graph capture runs before any eager call
-    const int64_t want = (rows + 7) / 8;
+    const int64_t want = (rows + GP_GELU_NW - 1) / GP_GELU_NW;
     const int cus = gp_num_cus(s);
     const unsigned nb = (unsigned)(want < cus ? want : cus);
     const bool copy = gelu_tab_ready(s, fmt == GP_FMT_F16);
-#define GP_LUT(EPL, CP, KH) gelu_ln_lut_kernel<EPL, 8, CP, KH><<<nb, 512, 0, s>>>(h, ln_w, ln_b, eps, out, rows)
+#define GP_LUT(EPL, CP, KH) gelu_ln_lut_kernel<EPL, GP_GELU_NW, CP, KH><<<nb, 64 * GP_GELU_NW, 0, s>>>(h, ln_w, ln_b, eps, out, rows)
     if (cols == 3072) {
       if (copy) GP_FMT_DISPATCH(fmt, GP_LUT(48, true, true), GP_LUT(48, true, false));
       else GP_FMT_DISPATCH(fmt, GP_LUT(48, false, true), GP_LUT(48, false, false));
