@@ -1,0 +1,536 @@
+"""Tile-embedding slide files: the input side of the slide encoder.
+
+The reference reads a slide's tile embeddings in ``SlideDataset.get_images_from_path``
+(finetune/datasets/slide_datatset.py:170-193): a ``.pt`` file is one ``[N, 1536]`` tensor (coords 0),
+an ``.h5`` file holds the datasets ``features`` [N, 1536] and ``coords`` [N, 2], read whole by
+``read_assets_from_h5`` (:155-164) through h5py, then optionally shuffled (:148-153) and cut to
+``max_tiles`` (:182-185).  demo/fenlei.py:22-24 reads ``features`` the same way.
+
+h5py is not part of this stack, so the HDF5 side is a small reader of its own over a memory map,
+restating the HDF5 file format specification (version 3.0, sections cited per function) for the
+subset h5py writes: superblocks v0-v3, object headers v1/v2, symbol-table groups and compact link
+messages, contiguous / compact / chunked (v1 B-tree) layouts with the deflate, shuffle and
+fletcher32 filters, and attributes of numeric, fixed-string and variable-length-string type.
+Everything outside that subset (dense link/attribute storage in fractal heaps, v4 chunk indexes,
+third-party filters, compound types) raises ``NotImplementedError`` naming what was found -- nothing
+is silently skipped.  ``.pt`` files load with ``torch.load(weights_only=True)`` (the reference's
+plain ``torch.load`` would unpickle arbitrary objects).
+
+Parity: h5py is absent from this image and no HDF5 file exists in it or in the reference, so the
+reader is checked against files built byte by byte from the specification by an independent writer
+(tests/h5_spec_writer.py); when h5py is importable the tests also compare against it.
+"""
+from __future__ import annotations
+
+import mmap
+import os
+import zlib
+from concurrent.futures import ThreadPoolExecutor
+from typing import Dict, Tuple
+
+import numpy as np
+import torch
+
+_SIG = b"\x89HDF\r\n\x1a\n"
+_IO_THREADS = max(1, min(8, os.cpu_count() or 1))
+
+
+class _Reader:
+    """Read-only view of one HDF5 file (spec §II superblock, §III-IV objects)."""
+
+    def __init__(self, path: str):
+        self._f = open(path, "rb")
+        size = os.fstat(self._f.fileno()).st_size
+        if size < 48:
+            self._f.close()
+            raise ValueError("%s: not an HDF5 file (%d bytes)" % (path, size))
+        self.mm = mmap.mmap(self._f.fileno(), 0, access=mmap.ACCESS_READ)
+        self.path = path
+        try:
+            self._superblock(size)
+        except Exception:
+            self.close()
+            raise
+
+    def close(self):
+        if self.mm is not None:
+            self.mm.close()
+            self.mm = None
+        self._f.close()
+
+    # -- primitives ------------------------------------------------------------------------------
+    def u(self, off: int, n: int) -> int:
+        return int.from_bytes(self.mm[off:off + n], "little")
+
+    def addr(self, off: int) -> int:
+        return self.u(off, self.so)
+
+    def length(self, off: int) -> int:
+        return self.u(off, self.sl)
+
+    def undef(self, a: int) -> bool:
+        return a == (1 << (8 * self.so)) - 1
+
+    def sig(self, off: int, s: bytes):
+        if self.mm[off:off + len(s)] != s:
+            raise ValueError("%s: expected %r at offset %d, found %r" % (self.path, s, off, self.mm[off:off + len(s)]))
+
+    # -- superblock (spec §II.A: searched at 0, 512, 1024, 2048, ...) ------------------------------
+    def _superblock(self, size: int):
+        at = 0
+        while at + 8 <= size and self.mm[at:at + 8] != _SIG:
+            at = 512 if at == 0 else at * 2
+        if at + 8 > size:
+            raise ValueError("%s: no HDF5 superblock signature" % self.path)
+        ver = self.mm[at + 8]
+        if ver in (0, 1):
+            self.so, self.sl = self.mm[at + 13], self.mm[at + 14]
+            p = at + 24 + (4 if ver == 1 else 0)
+            self.base = self.addr(p)
+            p += 4 * self.so                                   # base, free-space, EOF, driver info
+            # root group symbol table entry: link name offset, object header address, cache type...
+            self.root = self.addr(p + self.so)
+        elif ver in (2, 3):
+            self.so, self.sl = self.mm[at + 9], self.mm[at + 10]
+            p = at + 12
+            self.base = self.addr(p)
+            self.root = self.addr(p + 3 * self.so)             # base, extension, EOF, root header
+        else:
+            raise NotImplementedError("%s: superblock version %d" % (self.path, ver))
+        if self.so not in (2, 4, 8) or self.sl not in (2, 4, 8):
+            raise ValueError("%s: bad offset/length sizes %d/%d" % (self.path, self.so, self.sl))
+
+    # -- object headers (spec §IV.A.1.a version 1, §IV.A.1.b version 2) ---------------------------
+    def messages(self, oh: int):
+        """[(type, data_offset, size)] of every header message, continuation blocks followed."""
+        oh += self.base
+        out = []
+        if self.mm[oh:oh + 4] == b"OHDR":
+            flags = self.mm[oh + 5]
+            p = oh + 6 + (16 if flags & 0x20 else 0) + (4 if flags & 0x10 else 0)
+            w = 1 << (flags & 3)
+            blocks = [(p + w, self.u(p, w))]
+            track = bool(flags & 0x04)
+            while blocks:
+                p, n = blocks.pop(0)
+                end = p + n
+                hdr = 4 + (2 if track else 0)
+                while p + hdr <= end:
+                    t, sz = self.mm[p], self.u(p + 1, 2)
+                    self._not_shared(t, self.mm[p + 3])
+                    d = p + hdr
+                    if t == 0x10:
+                        a, ln = self.addr(d) + self.base, self.length(d + self.so)
+                        self.sig(a, b"OCHK")
+                        blocks.append((a + 4, ln - 8))
+                    elif t != 0:
+                        out.append((t, d, sz))
+                    p = d + sz
+            return out
+        if self.mm[oh] != 1:
+            raise NotImplementedError("%s: object header version %d at %d" % (self.path, self.mm[oh], oh))
+        nmsg = self.u(oh + 2, 2)
+        blocks = [(oh + 16, self.u(oh + 8, 4))]
+        while blocks and len(out) < nmsg:
+            p, n = blocks.pop(0)
+            end = p + n
+            while p + 8 <= end:
+                t, sz = self.u(p, 2), self.u(p + 2, 2)
+                self._not_shared(t, self.mm[p + 4])
+                d = p + 8
+                if t == 0x10:
+                    blocks.append((self.addr(d) + self.base, self.length(d + self.so)))
+                out.append((t, d, sz))
+                p = d + sz
+        return [m for m in out if m[0] not in (0, 0x10)]
+
+    def _not_shared(self, t: int, flags: int):
+        if flags & 0x02 and t != 0:                            # message stored elsewhere (committed datatype)
+            raise NotImplementedError("%s: shared header message of type %#x" % (self.path, t))
+
+    # -- groups (spec §III.A.1 v1 B-tree, §III.B symbol table node, §III.D local heap; §IV.A.2.g links)
+    def links(self, oh: int) -> Dict[str, int]:
+        names: Dict[str, int] = {}
+        for t, d, _ in self.messages(oh):
+            if t == 0x11:                                      # symbol table: B-tree + local heap
+                bt, heap = self.addr(d) + self.base, self.addr(d + self.so) + self.base
+                self.sig(heap, b"HEAP")
+                hdata = self.addr(heap + 8 + 2 * self.sl) + self.base
+                self._group_btree(bt, hdata, names)
+            elif t == 0x06:                                    # link message (compact new-style group)
+                name, target = self._link(d)
+                if target is not None:
+                    names[name] = target
+            elif t == 0x02:                                    # link info: dense storage if heap defined
+                p = d + 2 + (8 if self.mm[d + 1] & 1 else 0)
+                if not self.undef(self.addr(p)):
+                    raise NotImplementedError("%s: dense link storage (fractal heap) in a group" % self.path)
+        return names
+
+    def _group_btree(self, node: int, hdata: int, names: Dict[str, int]):
+        self.sig(node, b"TREE")
+        if self.mm[node + 4] != 0:
+            raise ValueError("%s: group B-tree node of type %d" % (self.path, self.mm[node + 4]))
+        level, used = self.mm[node + 5], self.u(node + 6, 2)
+        p = node + 8 + 2 * self.so + self.sl                   # past siblings and key 0
+        for _ in range(used):
+            child = self.addr(p) + self.base
+            p += self.so + self.sl
+            if level > 0:
+                self._group_btree(child, hdata, names)
+                continue
+            self.sig(child, b"SNOD")
+            e = child + 8
+            for _ in range(self.u(child + 6, 2)):
+                name_off, ohdr = self.addr(e), self.addr(e + self.so)
+                s = hdata + name_off
+                names[bytes(self.mm[s:self.mm.find(b"\0", s)]).decode("utf-8")] = ohdr
+                e += 2 * self.so + 24
+
+    def _link(self, d: int):
+        flags = self.mm[d + 1]
+        p = d + 2
+        ltype = 0
+        if flags & 0x08:
+            ltype = self.mm[p]
+            p += 1
+        p += (8 if flags & 0x04 else 0) + (1 if flags & 0x10 else 0)
+        w = 1 << (flags & 3)
+        n = self.u(p, w)
+        name = bytes(self.mm[p + w:p + w + n]).decode("utf-8")
+        return name, (self.addr(p + w + n) if ltype == 0 else None)   # soft / external links: not followed
+
+    # -- datatypes (spec §IV.A.2.d) -----------------------------------------------------------------
+    def dtype(self, d: int):
+        """-> (kind, numpy dtype or None, element size, extra)."""
+        cls, ver = self.mm[d] & 0x0F, self.mm[d] >> 4
+        b0, size = self.mm[d + 1], self.u(d + 4, 4)
+        bo = ">" if b0 & 1 else "<"
+        if cls == 0:
+            return "num", np.dtype("%s%s%d" % (bo, "i" if b0 & 0x08 else "u", size)), size, None
+        if cls == 1:
+            if b0 & 0x40 or size not in (2, 4, 8):
+                raise NotImplementedError("%s: floating-point layout (flags %#x, %d bytes)" % (self.path, b0, size))
+            return "num", np.dtype("%sf%d" % (bo, size)), size, None
+        if cls == 3:
+            return "str", np.dtype("S%d" % size), size, None
+        if cls == 8:                                           # enumeration (h5py's bool: FALSE / TRUE)
+            kind, base, bsize, _ = self.dtype(d + 8)
+            if kind != "num":
+                raise NotImplementedError("%s: enumeration over a non-integer base" % self.path)
+            nmem = self.u(d + 1, 2)
+            p, mem = d + 8 + self._dt_len(d + 8), []
+            for _ in range(nmem):
+                e = self.mm.find(b"\0", p)
+                mem.append(bytes(self.mm[p:e]).decode("utf-8"))
+                p = e + 1 if ver >= 3 else p + ((e - p) // 8 + 1) * 8
+            return "enum", base, size, mem
+        if cls == 9:
+            if (b0 & 0x0F) != 1:
+                raise NotImplementedError("%s: variable-length sequence datatype" % self.path)
+            return "vlstr", None, size, None
+        raise NotImplementedError("%s: datatype class %d" % (self.path, cls))
+
+    def _dt_len(self, d: int) -> int:
+        cls = self.mm[d] & 0x0F
+        return 8 + {0: 4, 1: 12, 3: 0}.get(cls, 0)
+
+    # -- dataspace (spec §IV.A.2.b) ---------------------------------------------------------------------
+    def shape(self, d: int):
+        ver, nd = self.mm[d], self.mm[d + 1]
+        if ver == 1:
+            p = d + 8
+        elif ver == 2:
+            if self.mm[d + 3] == 2:
+                return None                                    # null dataspace
+            p = d + 4
+        else:
+            raise NotImplementedError("%s: dataspace version %d" % (self.path, ver))
+        return tuple(self.length(p + i * self.sl) for i in range(nd))
+
+    # -- raw data ---------------------------------------------------------------------------------------
+    def _elements(self, raw: bytes, kind, npdt, esize, extra, shape):
+        n = int(np.prod(shape)) if shape else 1
+        if kind == "vlstr":
+            vals = []
+            for i in range(n):
+                e = raw[i * esize:(i + 1) * esize]
+                ln = int.from_bytes(e[:4], "little")
+                col = int.from_bytes(e[4:4 + self.so], "little")
+                idx = int.from_bytes(e[4 + self.so:8 + self.so], "little")
+                vals.append(self._global_heap(col, idx)[:ln].decode("utf-8"))
+            arr = np.empty(n, dtype=object)
+            arr[:] = vals
+            return arr.reshape(shape)
+        arr = np.frombuffer(raw, dtype=npdt, count=n).reshape(shape)
+        if kind == "enum" and sorted(extra) == ["FALSE", "TRUE"]:
+            return arr.astype(bool)
+        return arr.astype(npdt.newbyteorder("="))
+
+    def _global_heap(self, col: int, idx: int) -> bytes:
+        col += self.base
+        self.sig(col, b"GCOL")
+        end = col + self.length(col + 8)
+        p = col + 8 + self.sl
+        while p + 8 + self.sl <= end:
+            i, sz = self.u(p, 2), self.length(p + 8)
+            if i == 0:
+                break
+            if i == idx:
+                return bytes(self.mm[p + 8 + self.sl:p + 8 + self.sl + sz])
+            p += 8 + self.sl + ((sz + 7) // 8) * 8
+        raise ValueError("%s: global heap object %d not in collection %d" % (self.path, idx, col))
+
+    def dataset(self, oh: int) -> np.ndarray:
+        msgs = {t: (d, s) for t, d, s in self.messages(oh)}
+        if 0x03 not in msgs or 0x01 not in msgs or 0x08 not in msgs:
+            raise ValueError("%s: object at %d is not a dataset" % (self.path, oh))
+        kind, npdt, esize, extra = self.dtype(msgs[0x03][0])
+        shape = self.shape(msgs[0x01][0])
+        if shape is None:
+            return np.empty(0, dtype=npdt if npdt is not None else object)
+        filters = self._filters(msgs[0x0B][0]) if 0x0B in msgs else []
+        d = msgs[0x08][0]
+        ver = self.mm[d]
+        n = int(np.prod(shape)) if shape else 1
+        if ver == 3 or ver == 4:
+            cls = self.mm[d + 1]
+            if cls == 0:
+                raw = bytes(self.mm[d + 4:d + 4 + self.u(d + 2, 2)])
+            elif cls == 1:
+                a = self.addr(d + 2)
+                if self.undef(a):                              # never written: the zero fill value
+                    raw = b"\0" * (n * esize)
+                elif kind in ("num", "enum"):                  # bulk data: read straight into the array
+                    return self._native(self._pread(a + self.base, npdt, shape), kind, extra)
+                else:
+                    raw = bytes(self.mm[a + self.base:a + self.base + n * esize])
+            elif cls == 2 and ver == 3:
+                nd = self.mm[d + 2]
+                bt = self.addr(d + 3)
+                cdims = tuple(self.u(d + 3 + self.so + 4 * i, 4) for i in range(nd - 1))
+                return self._chunked(bt, shape, cdims, kind, npdt, esize, extra, filters)
+            else:
+                raise NotImplementedError("%s: data layout version %d class %d (v4 chunk indexes)"
+                                          % (self.path, ver, cls))
+        elif ver in (1, 2):
+            nd, cls = self.mm[d + 1], self.mm[d + 2]
+            p = d + 8
+            if cls == 0:
+                raw = bytes(self.mm[p + 4 * nd + 4:p + 4 * nd + 4 + self.u(p + 4 * nd, 4)])
+            elif cls == 1:
+                a = self.addr(p) + self.base
+                raw = bytes(self.mm[a:a + n * esize])
+            else:
+                cdims = tuple(self.u(p + self.so + 4 * i, 4) for i in range(nd - 1))
+                return self._chunked(self.addr(p), shape, cdims, kind, npdt, esize, extra, filters)
+        else:
+            raise NotImplementedError("%s: data layout version %d" % (self.path, ver))
+        return self._elements(raw, kind, npdt, esize, extra, shape)
+
+    # -- filter pipeline (spec §IV.A.2.l) and chunk B-tree (§III.A.1, node type 1) ----------------------
+    def _filters(self, d: int):
+        ver, nf = self.mm[d], self.mm[d + 1]
+        p = d + (8 if ver == 1 else 2)
+        out = []
+        for _ in range(nf):
+            fid = self.u(p, 2)
+            if ver == 1 or fid >= 256:
+                nlen = self.u(p + 2, 2)
+                p += 4
+            else:
+                nlen = 0
+                p += 2
+            nvals = self.u(p + 2, 2)
+            p += 4
+            p += ((nlen + 7) // 8) * 8 if ver == 1 else nlen
+            vals = [self.u(p + 4 * i, 4) for i in range(nvals)]
+            p += 4 * nvals + (4 if ver == 1 and nvals % 2 else 0)
+            if fid not in (1, 2, 3):
+                raise NotImplementedError("%s: HDF5 filter %d (only deflate, shuffle, fletcher32)" % (self.path, fid))
+            out.append((fid, vals))
+        return out
+
+    def _unfilter(self, raw: bytes, filters, mask: int, esize: int) -> bytes:
+        for i in reversed(range(len(filters))):
+            if mask & (1 << i):
+                continue
+            fid, _ = filters[i]
+            if fid == 1:
+                raw = zlib.decompress(raw)
+            elif fid == 2 and esize > 1:
+                a = np.frombuffer(raw, dtype=np.uint8)
+                ne = len(a) // esize
+                body = a[:ne * esize].reshape(esize, ne).T.reshape(-1)
+                raw = body.tobytes() + a[ne * esize:].tobytes()
+            elif fid == 3:
+                raw = raw[:-4]
+        return raw
+
+    def _chunked(self, bt, shape, cdims, kind, npdt, esize, extra, filters) -> np.ndarray:
+        if kind == "vlstr":
+            raise NotImplementedError("%s: chunked variable-length strings" % self.path)
+        out = np.zeros(shape, dtype=npdt)
+        nd = len(shape)
+        ksz = 8 + 8 * (nd + 1)
+        rec = np.dtype([("size", "<u4"), ("mask", "<u4"), ("offs", "<u8", (nd + 1,)), ("child", "<u%d" % self.so)])
+        offs, child, csize, mask = [], [], [], []
+        stack = [] if self.undef(bt) else [bt + self.base]     # undefined: never written, zero fill
+        while stack:                                           # B-tree nodes: fixed-size key+child records
+            node = stack.pop()
+            self.sig(node, b"TREE")
+            if self.mm[node + 4] != 1:
+                raise ValueError("%s: chunk B-tree node of type %d" % (self.path, self.mm[node + 4]))
+            level, used = self.mm[node + 5], self.u(node + 6, 2)
+            r = np.frombuffer(self.mm, dtype=rec, count=used, offset=node + 8 + 2 * self.so).copy()
+            if level > 0:
+                stack.extend(int(c) + self.base for c in r["child"])
+                continue
+            offs.append(r["offs"][:, :nd].astype(np.int64))
+            child.append(r["child"].astype(np.int64) + self.base)
+            csize.append(r["size"].astype(np.int64))
+            mask.append(r["mask"])
+        if not offs:
+            return self._native(out, kind, extra)
+        offs, child, csize, mask = (np.concatenate(offs), np.concatenate(child), np.concatenate(csize),
+                                    np.concatenate(mask))
+        cbytes = int(np.prod(cdims)) * esize
+        order = np.lexsort(offs.T[::-1])
+        offs, child, csize, mask = offs[order], child[order], csize[order], mask[order]
+        raw_chunks = not filters or bool(np.all((mask & ((1 << len(filters)) - 1)) == (1 << len(filters)) - 1))
+        rowslab = tuple(cdims[1:]) == tuple(shape[1:]) and nd >= 1
+        if raw_chunks and rowslab and np.all(csize == cbytes):
+            # unfiltered row-slab chunks (e.g. one tile per chunk): runs that are consecutive both in the
+            # file and in rows are one pread straight into the output rows
+            rows = offs[:, 0]
+            brk = np.nonzero((np.diff(child) != cbytes) | (np.diff(rows) != cdims[0]))[0] + 1
+            flat = out.reshape(shape[0], -1) if nd > 1 else out.reshape(-1, 1)
+            for lo, hi in zip(np.r_[0, brk], np.r_[brk, len(rows)]):
+                r0 = int(rows[lo])
+                r1 = min(int(rows[hi - 1]) + cdims[0], shape[0])
+                self._pread_into(flat[r0:r1], int(child[lo]))
+            return self._native(out, kind, extra)
+        count = int(np.prod(cdims))
+
+        def place(i):
+            raw = bytes(self.mm[child[i]:child[i] + csize[i]])
+            raw = self._unfilter(raw, filters, int(mask[i]), esize) if filters else raw
+            chunk = np.frombuffer(raw, dtype=npdt, count=count).reshape(cdims)
+            sl = tuple(slice(int(o), min(int(o) + n, s)) for o, n, s in zip(offs[i], cdims, shape))
+            out[sl] = chunk[tuple(slice(0, q.stop - q.start) for q in sl)]
+
+        # chunks are disjoint; zlib and numpy copies release the GIL, so decode them in parallel
+        if len(child) > 1:
+            with ThreadPoolExecutor(min(_IO_THREADS, len(child))) as ex:
+                list(ex.map(place, range(len(child))))
+        else:
+            place(0)
+        return self._native(out, kind, extra)
+
+    @staticmethod
+    def _native(arr: np.ndarray, kind, extra) -> np.ndarray:
+        if kind == "enum" and sorted(extra) == ["FALSE", "TRUE"]:
+            return arr.astype(bool)
+        return arr if arr.dtype.isnative else arr.astype(arr.dtype.newbyteorder("="))
+
+    def _pread(self, off: int, npdt, shape) -> np.ndarray:
+        """Contiguous bulk data straight into a fresh array (pread in parallel slabs; no page-fault
+        walk over a memory map)."""
+        arr = np.empty(shape, dtype=npdt)
+        self._pread_into(arr, off)
+        return arr
+
+    def _pread_into(self, arr: np.ndarray, off: int):
+        buf = memoryview(arr.reshape(-1).view(np.uint8))
+        n = len(buf)
+        slab = max(1 << 26, -(-n // _IO_THREADS))
+        fd = self._f.fileno()
+
+        def rd(lo):
+            hi = min(lo + slab, n)
+            while lo < hi:
+                got = os.preadv(fd, [buf[lo:hi]], off + lo)
+                if got <= 0:
+                    raise ValueError("%s: truncated data at offset %d" % (self.path, off + lo))
+                lo += got
+
+        starts = list(range(0, n, slab))
+        if len(starts) > 1:
+            with ThreadPoolExecutor(len(starts)) as ex:
+                list(ex.map(rd, starts))
+        elif starts:
+            rd(0)
+
+    # -- attributes (spec §IV.A.2.m) -------------------------------------------------------------------
+    def attrs(self, oh: int) -> dict:
+        out = {}
+        for t, d, _ in self.messages(oh):
+            if t == 0x15:                                      # attribute info: dense if heap defined
+                p = d + 2 + (2 if self.mm[d + 1] & 1 else 0)
+                if not self.undef(self.addr(p)):
+                    raise NotImplementedError("%s: dense attribute storage (fractal heap)" % self.path)
+            if t != 0x0C:
+                continue
+            ver = self.mm[d]
+            nlen, tlen, slen = self.u(d + 2, 2), self.u(d + 4, 2), self.u(d + 6, 2)
+            pad = (lambda x: ((x + 7) // 8) * 8) if ver == 1 else (lambda x: x)
+            p = d + 8 + (1 if ver == 3 else 0)
+            name = bytes(self.mm[p:p + nlen]).split(b"\0")[0].decode("utf-8")
+            p += pad(nlen)
+            kind, npdt, esize, extra = self.dtype(p)
+            p += pad(tlen)
+            shape = self.shape(p)
+            p += pad(slen)
+            if shape is None:
+                out[name] = None
+                continue
+            n = int(np.prod(shape)) if shape else 1
+            val = self._elements(bytes(self.mm[p:p + n * esize]), kind, npdt, esize, extra, shape)
+            out[name] = val[()] if shape == () else val
+        return out
+
+
+def read_assets_from_h5(h5_path: str) -> Tuple[dict, dict]:
+    """Every top-level dataset of the file and its attributes (reference slide_datatset.py:155-164:
+    ``assets[key] = f[key][:]``, ``attrs[key] = dict(f[key].attrs)``)."""
+    r = _Reader(h5_path)
+    try:
+        assets, attrs = {}, {}
+        for key, oh in r.links(r.root).items():
+            assets[key] = r.dataset(oh)
+            attrs[key] = r.attrs(oh)
+        return assets, attrs
+    finally:
+        r.close()
+
+
+def shuffle_data(images: torch.Tensor, coords: torch.Tensor, generator: torch.Generator = None):
+    """Permute tiles and coordinates together (reference slide_datatset.py:148-153)."""
+    idx = torch.randperm(len(images), generator=generator)
+    return images[idx], coords[idx]
+
+
+def get_images_from_path(img_path: str, max_tiles: int = 10000, shuffle_tiles: bool = False,
+                         generator: torch.Generator = None) -> dict:
+    """One slide's inputs (reference slide_datatset.py:170-193): ``{'imgs', 'img_lens', 'pad_mask',
+    'coords'}``.  ``.pt``: the saved tensor, coords 0 (as the reference; the caller supplies coordinates);
+    ``.h5``: ``features`` and ``coords``, optionally shuffled together, each cut to ``max_tiles`` rows."""
+    if ".pt" in img_path:
+        images = torch.load(img_path, map_location="cpu", weights_only=True)
+        coords = 0
+    elif ".h5" in img_path:
+        assets, _ = read_assets_from_h5(img_path)
+        for k in ("features", "coords"):
+            if k not in assets:
+                raise KeyError("%s has no '%s' dataset (found %s)" % (img_path, k, sorted(assets)))
+        images = torch.from_numpy(assets["features"])
+        coords = torch.from_numpy(assets["coords"])
+        if shuffle_tiles:
+            images, coords = shuffle_data(images, coords, generator)
+        if images.size(0) > max_tiles:
+            images = images[:max_tiles, :]
+        if coords.size(0) > max_tiles:
+            coords = coords[:max_tiles, :]
+    else:
+        raise ValueError("unsupported slide file %r (expected .pt or .h5)" % img_path)
+    return {"imgs": images, "img_lens": images.size(0), "pad_mask": 0, "coords": coords}
