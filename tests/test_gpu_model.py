@@ -32,6 +32,30 @@ def model():
     return m.to(DEV).eval()
 
 
+def test_h5_slide_file_to_golden(model, golden_meta, tmp_path):
+    """Slide-file input path (gigapath.slide_io, reference slide_datatset.py:170-193): the golden
+    N = 1024 slide written as a CLAM-style h5 file (one tile per chunk, fp32 features, int64 coords),
+    read back with get_images_from_path and fed to the encoder, matches the reference golden."""
+    from gigapath import slide_io
+    from h5_spec_writer import Writer
+    g = load_golden("e2e_N1024_B1.npz")
+    ent = [e for e in golden_meta["e2e"] if e["N"] == 1024 and e["B"] == 1][0]
+    x, coords = orc.synthetic_slide(1024)
+    w = Writer()
+    w.dataset("features", x[0], layout="chunked", chunks=(1, x.shape[-1]))
+    w.dataset("coords", coords[0].astype(np.int64), layout="chunked", chunks=(1, 2))
+    p = str(tmp_path / "slide.h5")
+    w.save(p)
+    d = slide_io.get_images_from_path(p, max_tiles=100000)
+    assert d["img_lens"] == 1024
+    with torch.no_grad():
+        got = torch.stack(model(d["imgs"][None].to(DEV), d["coords"][None].float().to(DEV),
+                                all_layer_embed=True)).cpu().numpy()
+    for idx in np.ndindex(*got.shape[:-1]):
+        rel, cos, ok = close_enough(got[idx], g["all_layer"][idx], ent.get("ref_bf16_rel_inf", 0.0))
+        assert ok, (idx, rel, cos)
+
+
 @pytest.mark.parametrize("N,B", [(1024, 1), (4097, 1), (600, 2)])
 def test_end_to_end_vs_reference_golden(model, golden_meta, N, B):
     g = load_golden("e2e_N%d_B%d.npz" % (N, B))

@@ -64,7 +64,7 @@ def _worker(rank, world, port, N, max_wsi_size, global_pool, q, graphs=True, hal
         q.put((rank, traceback.format_exc()))
 
 
-def _run_ranks(world, N, max_wsi, gp, graphs=True, half=False):
+def _run_ranks(world, N, max_wsi, gp, graphs=True, half=False, timeout=300):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -72,7 +72,7 @@ def _run_ranks(world, N, max_wsi, gp, graphs=True, half=False):
              for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=300) for _ in range(world))
+    res = dict(q.get(timeout=timeout) for _ in range(world))
     for p in procs:
         p.join(timeout=60)
     for r, v in res.items():
@@ -208,3 +208,26 @@ def test_sequence_parallel_c4_256k_two_ranks():
         for got, want in ((out, ref), (last, ref_last)):
             d, cos, ok = _sp_close(got, want)
             assert ok, (r, d, cos)
+
+
+@pytest.mark.timeout(900)
+def test_sequence_parallel_c4_256k_eight_ranks():
+    """The driver's N = 8 scaling run, rehearsed: C4's 256,000-tile slide sharded over EIGHT ranks
+    (the exact shard plan, K/V exchange plan and windowed kernels of the 8-GPU run; gloo host-staged
+    transport, eight processes on the one GPU) equals the single-device 256k forward."""
+    import oracle as orc
+    N = 256000
+    res = _run_ranks(8, N, 262144, False, graphs=False, timeout=800)
+    model = _model(262144)
+    x, coords = orc.synthetic_slide(N)
+    with torch.no_grad():
+        xt, ct = torch.from_numpy(x).cuda(), torch.from_numpy(coords).cuda()
+        ref = torch.stack(model(xt, ct, all_layer_embed=True)).cpu().numpy()
+        ref_last = model(xt, ct)[0].cpu().numpy()
+    for r in range(8):
+        out, last = res[r]
+        assert np.isfinite(out).all()
+        for got, want in ((out, ref), (last, ref_last)):
+            d, cos, ok = _sp_close(got, want)
+            assert ok, (r, d, cos)
+
