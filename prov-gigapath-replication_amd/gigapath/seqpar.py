@@ -123,15 +123,16 @@ class ShardPlan:
         # K/V gather range each rank's queries need, per branch (= its receive buffer)
         self.need = [[self._kv_need(w, b) for b in range(nb)] for w in range(world)]
         self.q_halo = [max(0, max(self._q_halo(w, b) for b in range(nb))) for w in range(world)]
-        # exchange phases, each one's attention overlapping the next one's transfer: short segments
-        # (halo-only traffic) first, then segments spanning several shards, then the branches
-        # whose one segment is the whole sequence (every rank needs every token's rows)
+        # exchange phases: the short segments (halo-only traffic) first, their attention overlapping
+        # the long branches' transfers; then ONE attention launch for every long branch.  A third
+        # phase (the whole-sequence branch's transfer hidden behind the multi-segment branches'
+        # attention) split that work into launches of 128-1,500 work items for 256 CUs: 23.6 vs
+        # 21.2 ms of compute per rank of the 256k slide on 8 ranks (tools/sp_rank_probe.py)
+        # for at most the whole-sequence branch's transfer time (~0.1 ms per layer) hidden.
         shard = L / world
         self.phase_a = [b for b in range(nb) if self.geo[b].s < shard]
-        self.phase_b1 = [b for b in range(nb) if b not in self.phase_a and self.geo[b].nseg > 1]
-        self.phase_b2 = [b for b in range(nb) if b not in self.phase_a and self.geo[b].nseg == 1]
-        if not self.phase_b1:                      # nothing in the middle: keep two phases
-            self.phase_b1, self.phase_b2 = self.phase_b2, []
+        self.phase_b1 = [b for b in range(nb) if b not in self.phase_a]
+        self.phase_b2: List[int] = []
         self.phase_b = self.phase_b1 + self.phase_b2
 
     # ---- geometry of one rank

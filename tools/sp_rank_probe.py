@@ -1,0 +1,112 @@
+"""Per-rank compute of the sequence-parallel forward at W ranks, measured on ONE GPU (the pool's boxes
+have one): for each rank r of the W-rank shard plan of the C4 slide, that rank's 12 encoder layers
+(QKV GEMM + sparsify, windowed attention over all branches, merge, out-proj, residual/LN, FFN) run with
+the K/V exchange replaced by nothing (the receive buffers hold random rows), as HIP-graph replays, timed
+with HIP events.  max over ranks = the compute floor of the W-GPU forward's encoder; the plan's
+received bytes per rank say what the RCCL exchange has to hide.  W = 1 is the same engine on the whole
+slide (the reference point for the scaling ratio).
+
+    python tools/sp_rank_probe.py [--tiles 256000] [--worlds 1,2,4,8] [--reps 3]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "prov-gigapath-replication_amd"))
+
+from gigapath import runtime, seqpar, slide_encoder   # noqa: E402
+
+
+class NullExchange:
+    device_comm = True
+
+    def all_to_all(self, *a, **k):
+        return None
+
+    def p2p(self, *a, **k):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tiles", type=int, default=256000)
+    ap.add_argument("--worlds", default="1,2,4,8")
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--ranks", default="", help="only these ranks of each W (default: all)")
+    ap.add_argument("--phases", default="2", help="comma list of attention launch splits to time: "
+                    "2 = the plan's (short branches, long branches), 3 = the long branches split by "
+                    "whole-sequence vs multi-segment, 1 = one launch")
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    model = slide_encoder.create_model("", "gigapath_slide_enc12l768d", 1536).to(dev).eval()
+    enc = model.encoder
+    layers = enc.engine.pack(enc, dev)
+    pa = layers[0].attn
+    F = enc.args.encoder_ffn_embed_dim
+    L = args.tiles + 1
+    g = torch.Generator(device=dev).manual_seed(0)
+    out = {"tiles": args.tiles, "worlds": {}}
+    for W, nph in [(int(w), int(p)) for w in args.worlds.split(",") for p in args.phases.split(",")]:
+        plan = seqpar.ShardPlan(L, W, pa.segs, pa.ratios, pa.H, pa.D, F)
+        if nph == 3:            # the round-2 plan: whole-sequence branches in a launch of their own
+            long_ = plan.phase_b1
+            plan.phase_b1 = [b for b in long_ if plan.geo[b].nseg > 1]
+            plan.phase_b2 = [b for b in long_ if plan.geo[b].nseg == 1]
+            if not plan.phase_b1:
+                plan.phase_b1, plan.phase_b2 = plan.phase_b2, []
+        elif nph == 1:
+            plan.phase_a, plan.phase_b1, plan.phase_b2 = [], plan.phase_a + plan.phase_b1 + plan.phase_b2, []
+        ranks = []
+        sel = [int(r) for r in args.ranks.split(",") if r != "" and int(r) < W] or range(W)
+        for r in sel:
+            ws = seqpar.ShardWorkspace(plan, r, dev, F, torch.bfloat16)
+            ws.x.normal_(generator=g)
+            ws.a.copy_(ws.x)
+            for kv in ws.kvs:
+                kv.normal_(generator=g)
+            if ws.hq:
+                ws.qkv_ext[:ws.hq].normal_(generator=g)
+            eng = seqpar.SeqParallelEngine(plan, r, NullExchange())
+            eng.use_graphs = True
+            x0 = ws.x.clone()
+            with torch.no_grad():
+                eng.run_layers(layers, ws)               # eager + capture
+                best = 1e9
+                for _ in range(args.reps):
+                    ws.x.copy_(x0)
+                    ws.a.copy_(x0)
+                    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    s.record()
+                    eng.run_layers(layers, ws)
+                    e.record()
+                    e.synchronize()
+                    best = min(best, s.elapsed_time(e))
+                # per-kernel-kind breakdown of one eager run (HIP events around each launch)
+                ws.x.copy_(x0)
+                ws.a.copy_(x0)
+                runtime.TIMER.reset()
+                runtime.TIMER.enabled = True
+                eng.run_layers(layers, ws)
+                spans = {k: round(v[1], 3) for k, v in sorted(runtime.TIMER.totals_ms().items())}
+                runtime.TIMER.enabled = False
+            a, b = plan.bounds[r]
+            ranks.append({"rank": r, "tokens": b - a, "ms": round(best, 3),
+                          "recv_MB_per_layer": round(plan.exchange_bytes(r) / 1e6, 1), "spans_ms": spans})
+            del eng, ws
+            torch.cuda.empty_cache()
+        key = W if nph == 2 else "%d/phases%d" % (W, nph)
+        out["worlds"][key] = {"max_ms": max(x["ms"] for x in ranks), "ranks": ranks}
+        print(json.dumps({"W": key, "max_ms": out["worlds"][key]["max_ms"], "ms": [x["ms"] for x in ranks],
+                          "attn_ms": [x["spans_ms"].get("attn") for x in ranks]}), flush=True)
+    if 1 in out["worlds"]:
+        t1 = out["worlds"][1]["max_ms"]
+        out["compute_scaling"] = {W: round(t1 / v["max_ms"], 2) for W, v in out["worlds"].items()}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
