@@ -44,6 +44,10 @@ from . import _hip, runtime
 ATTN_FLOPS_PER_S = 0.7e15
 GEMM_FLOPS_PER_S = 0.9e15
 ROW_BYTES_PER_S = 4.0e12
+# one xGMI link, one direction (MI355X: 7 links of ~153 GB/s bidirectional per GPU; ~64 GB/s per
+# direction assumed achievable).  Each rank pair exchanges over its own link, so the busiest pair
+# bounds a layer's all-to-alls.
+LINK_BYTES_PER_S = 64e9
 
 
 @dataclass(frozen=True)
@@ -96,6 +100,18 @@ def balanced_bounds(cost: np.ndarray, world: int) -> List[Tuple[int, int]]:
     return [(cuts[w], cuts[w + 1]) for w in range(world)]
 
 
+def snapped_bounds(bounds: List[Tuple[int, int]], unit: int, L: int) -> Optional[List[Tuple[int, int]]]:
+    """The cuts of `bounds` rounded to multiples of `unit` (None if two cuts collide)."""
+    cuts = [0]
+    for a, _ in bounds[1:]:
+        c = int(round(a / unit)) * unit
+        if c <= cuts[-1] or c >= L:
+            return None
+        cuts.append(c)
+    cuts.append(L)
+    return [(cuts[w], cuts[w + 1]) for w in range(len(bounds))]
+
+
 def _isect(a: Tuple[int, int], b: Tuple[int, int]) -> Tuple[int, int]:
     lo, hi = max(a[0], b[0]), min(a[1], b[1])
     return (lo, hi) if lo < hi else (0, 0)
@@ -117,7 +133,10 @@ class ShardPlan:
                 raise ValueError("sequence parallel needs H %% r == 0 (H=%d, r=%d)" % (H, r))
         self.geo = [branch_geo(L, sl, r, H) for sl, r in zip(segs, ratios)]
         self.C = [(H // r) * D for r in self.ratios]               # sparsified columns of K (and of V)
-        self.bounds = bounds or balanced_bounds(token_cost(L, segs, ratios, H, D, F), world)
+        self.model_s = None
+        if bounds is None:
+            bounds = self._choose_bounds(F)
+        self.bounds = bounds
         assert self.bounds[0][0] == 0 and self.bounds[-1][1] == L
         nb = len(self.geo)
         # K/V gather range each rank's queries need, per branch (= its receive buffer)
@@ -134,6 +153,41 @@ class ShardPlan:
         self.phase_b1 = [b for b in range(nb) if b not in self.phase_a]
         self.phase_b2: List[int] = []
         self.phase_b = self.phase_b1 + self.phase_b2
+
+    # ---- shard choice
+    def _choose_bounds(self, F: int) -> List[Tuple[int, int]]:
+        """Cost-balanced cuts, or those cuts snapped to a multiple of one branch's segment length when
+        the model says the exchange it removes is worth more than the imbalance it adds: per layer,
+        max over ranks of the modelled compute + the busiest rank pair's bytes over one xGMI link.
+        (At 256k / 8 ranks: cuts at multiples of 32,768 leave the 32,768-token branch and the
+        1,024-token branch with nothing to exchange; the busiest link carries 27.5 instead of 49 MB.)"""
+        L, world = self.L, self.world
+        cost = token_cost(L, self.segs, self.ratios, self.H, self.D, F)
+        bal = balanced_bounds(cost, world)
+        if world == 1:
+            return bal
+        cum = np.concatenate([[0.0], np.cumsum(cost)])
+        best, best_t = bal, None
+        for unit in [bal] + sorted({g.s for g in self.geo if g.nseg > 1}, reverse=True):
+            cand = bal if isinstance(unit, list) else snapped_bounds(bal, unit, L)
+            if cand is None:
+                continue
+            plan = ShardPlan(L, world, self.segs, self.ratios, self.H, self.D, F, bounds=cand)
+            t = max(cum[e] - cum[a] for a, e in cand) + plan.max_pair_bytes() / LINK_BYTES_PER_S
+            if best_t is None or t < best_t - 1e-12:
+                best, best_t = cand, t
+        self.model_s = best_t
+        return best
+
+    def max_pair_bytes(self) -> int:
+        """Bytes per layer over the busiest (source, destination) rank pair: sparse K/V + q halo."""
+        pair: Dict[Tuple[int, int], int] = {}
+        for v in range(self.world):
+            for b, w, lo, hi in self.recvs(v):
+                pair[(w, v)] = pair.get((w, v), 0) + (hi - lo) * 2 * self.C[b] * 2
+            for w, lo, hi in self.halo_recvs(v):
+                pair[(w, v)] = pair.get((w, v), 0) + (hi - lo) * 3 * self.E * 2
+        return max(pair.values(), default=0)
 
     # ---- geometry of one rank
     def _kv_need(self, w: int, b: int) -> Tuple[int, int]:

@@ -98,6 +98,28 @@ def test_balanced_bounds_equalise_modelled_cost():
     assert bounds[-1][1] - bounds[-1][0] > bounds[0][1] - bounds[0][0]
 
 
+def test_shard_cuts_snap_to_segments_when_the_exchange_pays():
+    """C4 on 8 ranks: the cuts land on multiples of 32,768, so the 32,768- and 1,024-token branches
+    exchange nothing and the busiest rank pair carries ~27.5 MB per layer instead of ~49 MB; the
+    chosen plan's modelled compute + busiest-link time is never worse than the cost-balanced cuts'."""
+    L = 256001
+    plan = seqpar.ShardPlan(L, 8, *DEFAULT, H, D, F)
+    assert all(a % 32768 == 0 for a, _ in plan.bounds)
+    for b in (0, 2):                                       # s = 1024 and s = 32768
+        assert not [x for x in plan.recvs(3) if x[0] == b]
+    bal = seqpar.ShardPlan(L, 8, *DEFAULT, H, D, F,
+                           bounds=seqpar.balanced_bounds(seqpar.token_cost(L, *DEFAULT, H, D, F), 8))
+    assert plan.max_pair_bytes() < 0.6 * bal.max_pair_bytes()
+    for n, w in [(70001, 2), (70001, 8), (100001, 3), (16385, 4), (256001, 2)]:
+        p = seqpar.ShardPlan(n, w, *DEFAULT, H, D, F)
+        cost = seqpar.token_cost(n, *DEFAULT, H, D, F)
+        q = seqpar.ShardPlan(n, w, *DEFAULT, H, D, F, bounds=seqpar.balanced_bounds(cost, w))
+
+        def model(pl):
+            return (max(cost[a:e].sum() for a, e in pl.bounds) + pl.max_pair_bytes() / seqpar.LINK_BYTES_PER_S)
+        assert model(p) <= model(q) * (1 + 1e-9), (n, w)
+
+
 def test_exchange_volume_is_sparse():
     """At 256k / 8 ranks each rank receives far less than the dense K/V (786 MB per layer)."""
     plan = seqpar.ShardPlan(256001, 8, *DEFAULT, H, D, F)

@@ -6,7 +6,7 @@ runtime.py loads (tuning disabled) on every later run.
     python tools/tune_gemms.py --sp-tiles 262144 --sp-worlds 1 2 4 8 [--packed-tiles 675587]
 
 --sp-tiles tunes, for every rank of every listed world size, the five GEMM shapes that rank's
-sequence-parallel forward issues (rows = its token window from seqpar.balanced_bounds, patch rows =
+sequence-parallel forward issues (rows = its token window from seqpar.ShardPlan, patch rows =
 its tiles), by calling the same torch.addmm / torch.mm forms the runtime uses (runtime.py:345-356,
 seqpar.py:397-414, slide_encoder.py:509) on random data -- no 256k forward per shape.  --packed-tiles
 adds the packed (C5) shapes of that many tiles over --packed-slides slides.  Existing entries of
@@ -29,12 +29,12 @@ SEGS, RATIOS = [1024, 5792, 32768, 185363, 1048576], [1, 2, 4, 8, 16]
 
 
 def sp_shapes(tiles, worlds):
-    """{(rows, patch_rows)} over every rank of every world size (seqpar.SPPlan's default bounds)."""
+    """{(rows, patch_rows)} over every rank of every world size (seqpar.ShardPlan's default bounds)."""
     from gigapath import seqpar
     L = tiles + 1
     out = set()
     for w in worlds:
-        bounds = seqpar.balanced_bounds(seqpar.token_cost(L, SEGS, RATIOS, H, D, F), w) if w > 1 else [(0, L)]
+        bounds = seqpar.ShardPlan(L, w, SEGS, RATIOS, H, D, F).bounds if w > 1 else [(0, L)]
         for a, e in bounds:
             out.add((e - a, (e - 1) - (max(a, 1) - 1)))
     return sorted(out)
