@@ -142,6 +142,13 @@ class ShardPlan:
         # K/V gather range each rank's queries need, per branch (= its receive buffer)
         self.need = [[self._kv_need(w, b) for b in range(nb)] for w in range(world)]
         self.q_halo = [max(0, max(self._q_halo(w, b) for b in range(nb))) for w in range(world)]
+        # branches with no cross-rank rows at all (every segment inside one shard, e.g. the 1,024- and
+        # 32,768-token branches under 32,768-aligned cuts): no all-to-all; each rank's sparsify writes
+        # its rows straight into its own K/V buffer.  (One rank keeps its self-only all-to-alls: SP on one
+        # rank exists only to exercise the RCCL transport, test_gpu_seqpar.py.)
+        self.no_xfer = [world > 1 and all(self.chunk(w, v, b)[1] <= self.chunk(w, v, b)[0]
+                                          for w in range(world) for v in range(world) if w != v)
+                        for b in range(nb)]
         # exchange phases: the short segments (halo-only traffic) first, their attention overlapping
         # the long branches' transfers; then ONE attention launch for every long branch.  A third
         # phase (the whole-sequence branch's transfer hidden behind the multi-segment branches'
@@ -348,11 +355,21 @@ class ShardWorkspace:
             lo, hi = plan.need[rank][b]
             self.kvs.append(torch.empty(hi - lo, 2 * plan.C[b], dtype=act, device=dev))
             self.kv_base.append(lo)
-            splits = plan.send_splits(rank, b)
+            splits = [0] * plan.world if plan.no_xfer[b] else plan.send_splits(rank, b)
             self.send.append(torch.empty(sum(splits), 2 * plan.C[b], dtype=act, device=dev))
             self.send_off.append(list(np.cumsum([0] + splits[:-1])))
+        self.plan = plan
         # branch outputs keep the single-device layout; only the window's rows are written/read
         self.attn = runtime.AttentionScratch(dev, 1, plan.L, H, D, plan.segs, plan.ratios, act)
+
+    def dest(self, b: int, v: int) -> Tuple[torch.Tensor, int]:
+        """(buffer, first row) where this rank's branch-b rows for rank v go: the send buffer's chunk
+        for v, or -- branch without transfers -- this rank's own K/V buffer."""
+        if self.plan.no_xfer[b]:
+            assert v == self.rank, "branch %d has no cross-rank rows" % b
+            lo, _ = self.plan.chunk(self.rank, v, b)
+            return self.kvs[b], lo - self.kv_base[b]
+        return self.send[b], int(self.send_off[b][v])
 
 
 class SeqParallelEngine:
@@ -379,7 +396,8 @@ class SeqParallelEngine:
             for v in range(plan.world):
                 lo, hi = plan.chunk(self.rank, v, b)
                 if hi > lo:
-                    lst.append((lo, hi, ws.send[b], int(ws.send_off[b][v])))
+                    buf, off = ws.dest(b, v)
+                    lst.append((lo, hi, buf, off))
             dests.append(lst)
         with runtime.TIMER.span("sparsify"):
             _hip.dilated_sparsify_dests(ws.qkv, 3 * E, E, 2 * E, a, e - a, plan.L, plan.H, plan.D, plan.segs,
@@ -394,7 +412,8 @@ class SeqParallelEngine:
             recvs = [(src, ws.qkv_ext[lo - (a - ws.hq):hi - (a - ws.hq)]) for src, lo, hi in self._hrecvs]
             handles += self.xch.p2p(sends, recvs) or []
         for b in branches:
-            handles += self.xch.all_to_all(ws.kvs[b], ws.send[b], self._rsplit[b], self._ssplit[b]) or []
+            if not plan.no_xfer[b]:
+                handles += self.xch.all_to_all(ws.kvs[b], ws.send[b], self._rsplit[b], self._ssplit[b]) or []
         return handles
 
     def attention(self, pa: runtime.PackedAttention, ws: ShardWorkspace, branches: List[int]):

@@ -120,6 +120,20 @@ def test_shard_cuts_snap_to_segments_when_the_exchange_pays():
         assert model(p) <= model(q) * (1 + 1e-9), (n, w)
 
 
+def test_branches_without_transfers():
+    """Under 32,768-aligned cuts (C4, 8 ranks) the 1,024- and 32,768-token branches have no
+    cross-rank rows: no all-to-all, sparsify writes them into the rank's own K/V buffer."""
+    plan = seqpar.ShardPlan(256001, 8, *DEFAULT, H, D, F)
+    assert plan.no_xfer == [True, False, True, False, False]
+    ws = seqpar.ShardWorkspace(plan, 3, "cpu", F)
+    buf, off = ws.dest(0, 3)
+    assert buf is ws.kvs[0] and off == plan.bounds[3][0] - plan.need[3][0][0]
+    assert ws.send[0].shape[0] == 0 and ws.send[2].shape[0] == 0
+    bal = seqpar.ShardPlan(256001, 8, *DEFAULT, H, D, F,
+                           bounds=seqpar.balanced_bounds(seqpar.token_cost(256001, *DEFAULT, H, D, F), 8))
+    assert not any(bal.no_xfer)
+
+
 def test_exchange_volume_is_sparse():
     """At 256k / 8 ranks each rank receives far less than the dense K/V (786 MB per layer)."""
     plan = seqpar.ShardPlan(256001, 8, *DEFAULT, H, D, F)
@@ -158,8 +172,10 @@ def _exchange_worker(rank, world, port, L, segs, ratios, q):
         for b in range(len(segs)):                       # this rank's sparsified rows, packed per peer
             for v in range(world):
                 lo, hi = plan.chunk(rank, v, b)
-                off = ws.send_off[b][v]
-                ws.send[b][off:off + hi - lo] = torch.from_numpy(ref[b][lo:hi]).to(ws.send[b].dtype)
+                if hi <= lo:
+                    continue
+                buf, off = ws.dest(b, v)
+                buf[off:off + hi - lo] = torch.from_numpy(ref[b][lo:hi]).to(buf.dtype)
         eng = seqpar.SeqParallelEngine(plan, rank, seqpar.Exchange())
         seqpar.Exchange.wait(eng.exchange(ws, list(range(len(segs))), halo=True))
         for b in range(len(segs)):
