@@ -143,9 +143,10 @@ class ShardPlan:
         self.need = [[self._kv_need(w, b) for b in range(nb)] for w in range(world)]
         self.q_halo = [max(0, max(self._q_halo(w, b) for b in range(nb))) for w in range(world)]
         # branches with no cross-rank rows at all (every segment inside one shard, e.g. the 1,024- and
-        # 32,768-token branches under 32,768-aligned cuts): no all-to-all; each rank's sparsify writes
-        # its rows straight into its own K/V buffer.  (One rank keeps its self-only all-to-alls: SP on one
-        # rank exists only to exercise the RCCL transport, test_gpu_seqpar.py.)
+        # 32,768-token branches under 32,768-aligned cuts): no sparsify, no all-to-all -- the attention
+        # reads their keys straight from the rank's own qkv rows, as the single-device launch does.
+        # (One rank keeps its self-only all-to-alls: SP on one rank exists only to exercise the RCCL
+        # transport, test_gpu_seqpar.py.)
         self.no_xfer = [world > 1 and all(self.chunk(w, v, b)[1] <= self.chunk(w, v, b)[0]
                                           for w in range(world) for v in range(world) if w != v)
                         for b in range(nb)]
@@ -353,6 +354,9 @@ class ShardWorkspace:
         self.kvs, self.kv_base, self.send, self.send_off = [], [], [], []
         for b in range(len(plan.geo)):
             lo, hi = plan.need[rank][b]
+            if plan.no_xfer[b]:              # keys come from qkv_ext (dense rows)
+                assert a <= lo and hi <= e, (b, lo, hi, a, e)
+                lo = hi
             self.kvs.append(torch.empty(hi - lo, 2 * plan.C[b], dtype=act, device=dev))
             self.kv_base.append(lo)
             splits = [0] * plan.world if plan.no_xfer[b] else plan.send_splits(rank, b)
@@ -363,12 +367,8 @@ class ShardWorkspace:
         self.attn = runtime.AttentionScratch(dev, 1, plan.L, H, D, plan.segs, plan.ratios, act)
 
     def dest(self, b: int, v: int) -> Tuple[torch.Tensor, int]:
-        """(buffer, first row) where this rank's branch-b rows for rank v go: the send buffer's chunk
-        for v, or -- branch without transfers -- this rank's own K/V buffer."""
-        if self.plan.no_xfer[b]:
-            assert v == self.rank, "branch %d has no cross-rank rows" % b
-            lo, _ = self.plan.chunk(self.rank, v, b)
-            return self.kvs[b], lo - self.kv_base[b]
+        """(buffer, first row) where this rank's branch-b rows for rank v go: the send buffer's chunk."""
+        assert not self.plan.no_xfer[b], "branch %d is read from qkv directly" % b
         return self.send[b], int(self.send_off[b][v])
 
 
@@ -390,8 +390,12 @@ class SeqParallelEngine:
         plan = self.plan
         a, e = plan.bounds[self.rank]
         E = plan.E
-        dests = []
+        dests, segs, ratios = [], [], []
         for b in range(len(plan.geo)):
+            if plan.no_xfer[b]:
+                continue
+            segs.append(plan.segs[b])
+            ratios.append(plan.ratios[b])
             lst = []
             for v in range(plan.world):
                 lo, hi = plan.chunk(self.rank, v, b)
@@ -399,9 +403,11 @@ class SeqParallelEngine:
                     buf, off = ws.dest(b, v)
                     lst.append((lo, hi, buf, off))
             dests.append(lst)
+        if not dests:
+            return
         with runtime.TIMER.span("sparsify"):
-            _hip.dilated_sparsify_dests(ws.qkv, 3 * E, E, 2 * E, a, e - a, plan.L, plan.H, plan.D, plan.segs,
-                                        plan.ratios, dests)
+            _hip.dilated_sparsify_dests(ws.qkv, 3 * E, E, 2 * E, a, e - a, plan.L, plan.H, plan.D, segs, ratios,
+                                        dests)
 
     def exchange(self, ws: ShardWorkspace, branches: List[int], halo: bool):
         plan = self.plan
@@ -422,7 +428,13 @@ class SeqParallelEngine:
         plan = self.plan
         a, e = plan.bounds[self.rank]
         descs = []
+        E = plan.E
         for b in branches:
+            if plan.no_xfer[b]:              # dense K / V columns of the rank's own qkv rows
+                k = ws.qkv_ext[:, E:]
+                descs.append(_hip.attn_branch(plan.segs[b], plan.ratios[b], k, k.data_ptr() + 2 * E, 3 * E,
+                                              a - ws.hq, False, ws.attn.outs[b], ws.attn.lses[b]))
+                continue
             C = plan.C[b]
             kv = ws.kvs[b]
             descs.append(_hip.attn_branch(plan.segs[b], plan.ratios[b], kv, kv.data_ptr() + 2 * C, 2 * C,

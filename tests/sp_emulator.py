@@ -107,11 +107,11 @@ def attn_branch(sl, r, k, v, kv_row_stride, kv_tok_base, kv_sparse_cols, o, lse)
 
 def _kv_tensor(k, v, stride, sparse, H, D, r):
     """Resolve (k tensor, v pointer) into two [rows, cols] views of the same buffer."""
-    assert isinstance(k, torch.Tensor) and k.shape[1] == stride
+    assert isinstance(k, torch.Tensor) and k.stride(0) == stride and k.stride(1) == 1
     C = (H // r) * D if sparse else H * D
     vp = v if isinstance(v, int) else v.data_ptr()
     off = (vp - k.data_ptr()) // k.element_size()
-    assert 0 <= off and off + C <= stride
+    assert 0 <= off and off + C <= k.shape[1]
     return k[:, :C], k[:, off:off + C]
 
 

@@ -122,13 +122,14 @@ def test_shard_cuts_snap_to_segments_when_the_exchange_pays():
 
 def test_branches_without_transfers():
     """Under 32,768-aligned cuts (C4, 8 ranks) the 1,024- and 32,768-token branches have no
-    cross-rank rows: no all-to-all, sparsify writes them into the rank's own K/V buffer."""
+    cross-rank rows: no sparsify rows, no all-to-all, no K/V buffer (the attention reads qkv)."""
     plan = seqpar.ShardPlan(256001, 8, *DEFAULT, H, D, F)
     assert plan.no_xfer == [True, False, True, False, False]
     ws = seqpar.ShardWorkspace(plan, 3, "cpu", F)
-    buf, off = ws.dest(0, 3)
-    assert buf is ws.kvs[0] and off == plan.bounds[3][0] - plan.need[3][0][0]
-    assert ws.send[0].shape[0] == 0 and ws.send[2].shape[0] == 0
+    for b in (0, 2):
+        assert ws.send[b].shape[0] == 0 and ws.kvs[b].shape[0] == 0
+        lo, hi = plan.need[3][b]
+        assert plan.bounds[3][0] <= lo and hi <= plan.bounds[3][1]
     bal = seqpar.ShardPlan(256001, 8, *DEFAULT, H, D, F,
                            bounds=seqpar.balanced_bounds(seqpar.token_cost(256001, *DEFAULT, H, D, F), 8))
     assert not any(bal.no_xfer)
@@ -172,13 +173,16 @@ def _exchange_worker(rank, world, port, L, segs, ratios, q):
         for b in range(len(segs)):                       # this rank's sparsified rows, packed per peer
             for v in range(world):
                 lo, hi = plan.chunk(rank, v, b)
-                if hi <= lo:
+                if hi <= lo or plan.no_xfer[b]:
                     continue
                 buf, off = ws.dest(b, v)
                 buf[off:off + hi - lo] = torch.from_numpy(ref[b][lo:hi]).to(buf.dtype)
         eng = seqpar.SeqParallelEngine(plan, rank, seqpar.Exchange())
         seqpar.Exchange.wait(eng.exchange(ws, list(range(len(segs))), halo=True))
         for b in range(len(segs)):
+            if plan.no_xfer[b]:                 # read from qkv by the attention, never exchanged
+                assert ws.kvs[b].shape[0] == 0
+                continue
             lo, hi = plan.need[rank][b]
             base = ws.kv_base[b]
             got = ws.kvs[b][lo - base:hi - base].float().numpy()
