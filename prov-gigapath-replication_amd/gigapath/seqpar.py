@@ -382,6 +382,11 @@ class SeqParallelEngine:
         self._ssplit = [plan.send_splits(rank, b) for b in range(len(plan.geo))]
         self._rsplit = [plan.recv_splits(rank, b) for b in range(len(plan.geo))]
         self.use_graphs = False
+        # True: the transfer-free branches' attention in a launch of its own before any wait (it would
+        # overlap every transfer); off: measured +1.05 ms of compute per 256k/8 rank forward (the long
+        # branches' launch loses its 32,768-token work items, r02_s10_sp_rank_probe_localfirst.json)
+        # against a modelled ~2 ms of exposed transfers at 64 GB/s per link -- not worth it unmeasured
+        self.local_first = False
         self.graphs = {}                    # (segment, layer, weights signature) -> CUDAGraph
         self._graph_sig = None
 
@@ -470,6 +475,10 @@ class SeqParallelEngine:
         M = ws.n
         F = ws.f.shape[1]
         nl = len(layers)
+        local = [b for b in range(len(plan.geo)) if plan.no_xfer[b]] if self.local_first else []
+        ph_a = [b for b in plan.phase_a if b not in local]
+        ph_b1 = [b for b in plan.phase_b1 if b not in local]
+        ph_b2 = [b for b in plan.phase_b2 if b not in local]
         wsig = weights_sig if weights_sig is not None else id(layers)
         if wsig != self._graph_sig:          # new weights: captures of the old ones never replay
             self.graphs.clear()
@@ -484,7 +493,7 @@ class SeqParallelEngine:
                 self.sparsify(ws)
 
             def tail(pa=pa, pl=pl, nxt=nxt):
-                self.attention(pa, ws, plan.phase_b2 if plan.phase_b2 else plan.phase_b1)
+                self.attention(pa, ws, ph_b2 if plan.phase_b2 else ph_b1)
                 with runtime.TIMER.span("merge"):
                     _hip.branch_merge_ln_window(ws.attn.outs, ws.attn.lses, plan.segs, plan.ratios, 1, plan.L, a, M,
                                                 H, D, pa.ln_w, pa.ln_b, pa.ln_eps, ws.a)
@@ -506,11 +515,12 @@ class SeqParallelEngine:
             h_a = self.exchange(ws, plan.phase_a, halo=True)
             h_b1 = self.exchange(ws, plan.phase_b1, halo=False)
             h_b2 = self.exchange(ws, plan.phase_b2, halo=False)
+            self.attention(pa, ws, local)          # needs no transfer: runs while they all fly
             Exchange.wait(h_a)
-            self.attention(pa, ws, plan.phase_a)
+            self.attention(pa, ws, ph_a)
             Exchange.wait(h_b1)
             if plan.phase_b2:                      # the middle phase runs while the last transfers
-                self.attention(pa, ws, plan.phase_b1)
+                self.attention(pa, ws, ph_b1)
             Exchange.wait(h_b2)
             self._segment(("tail", li, wsig), tail)
             if layer_hook is not None:

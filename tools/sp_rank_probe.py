@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--worlds", default="1,2,4,8")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--ranks", default="", help="only these ranks of each W (default: all)")
+    ap.add_argument("--local-first", default="0", help="comma list: 1 = transfer-free branches in a launch "
+                    "of their own before the waits, 0 = in their size phase (the engine's default)")
     ap.add_argument("--phases", default="2", help="comma list of attention launch splits to time: "
                     "2 = the plan's (short branches, long branches), 3 = the long branches split by "
                     "whole-sequence vs multi-segment, 1 = one launch")
@@ -50,7 +52,8 @@ def main():
     L = args.tiles + 1
     g = torch.Generator(device=dev).manual_seed(0)
     out = {"tiles": args.tiles, "worlds": {}}
-    for W, nph in [(int(w), int(p)) for w in args.worlds.split(",") for p in args.phases.split(",")]:
+    for W, nph, lf in [(int(w), int(p), int(f)) for w in args.worlds.split(",") for p in args.phases.split(",")
+                       for f in args.local_first.split(",")]:
         plan = seqpar.ShardPlan(L, W, pa.segs, pa.ratios, pa.H, pa.D, F)
         if nph == 3:            # the round-2 plan: whole-sequence branches in a launch of their own
             long_ = plan.phase_b1
@@ -72,6 +75,7 @@ def main():
                 ws.qkv_ext[:ws.hq].normal_(generator=g)
             eng = seqpar.SeqParallelEngine(plan, r, NullExchange())
             eng.use_graphs = True
+            eng.local_first = bool(lf)
             x0 = ws.x.clone()
             with torch.no_grad():
                 eng.run_layers(layers, ws)               # eager + capture
@@ -98,12 +102,12 @@ def main():
                           "recv_MB_per_layer": round(plan.exchange_bytes(r) / 1e6, 1), "spans_ms": spans})
             del eng, ws
             torch.cuda.empty_cache()
-        key = W if nph == 2 else "%d/phases%d" % (W, nph)
+        key = str(W) + ("" if nph == 2 else "/phases%d" % nph) + ("/local-first" if lf else "")
         out["worlds"][key] = {"max_ms": max(x["ms"] for x in ranks), "ranks": ranks}
         print(json.dumps({"W": key, "max_ms": out["worlds"][key]["max_ms"], "ms": [x["ms"] for x in ranks],
                           "attn_ms": [x["spans_ms"].get("attn") for x in ranks]}), flush=True)
-    if 1 in out["worlds"]:
-        t1 = out["worlds"][1]["max_ms"]
+    if "1" in out["worlds"]:
+        t1 = out["worlds"]["1"]["max_ms"]
         out["compute_scaling"] = {W: round(t1 / v["max_ms"], 2) for W, v in out["worlds"].items()}
     print(json.dumps(out))
 
