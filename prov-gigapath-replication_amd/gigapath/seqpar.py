@@ -375,6 +375,12 @@ class ShardWorkspace:
 class SeqParallelEngine:
     """Runs the encoder layers of one rank's shard.  `layers` are runtime.PackedLayer."""
 
+    # True: the transfer-free branches' attention in a launch of its own before any wait (it would
+    # overlap every transfer).  Off: measured +1.05 ms of compute per 256k/8 rank forward (the long
+    # branches' launch loses its 32,768-token work items, r02_s10_sp_rank_probe_localfirst.json) against
+    # a modelled ~2 ms of exposed transfers at 64 GB/s per link -- not worth it unmeasured.
+    local_first = False
+
     def __init__(self, plan: ShardPlan, rank: int, exchange: Exchange):
         self.plan, self.rank, self.xch = plan, rank, exchange
         self._hsends = plan.halo_sends(rank)
@@ -382,11 +388,7 @@ class SeqParallelEngine:
         self._ssplit = [plan.send_splits(rank, b) for b in range(len(plan.geo))]
         self._rsplit = [plan.recv_splits(rank, b) for b in range(len(plan.geo))]
         self.use_graphs = False
-        # True: the transfer-free branches' attention in a launch of its own before any wait (it would
-        # overlap every transfer); off: measured +1.05 ms of compute per 256k/8 rank forward (the long
-        # branches' launch loses its 32,768-token work items, r02_s10_sp_rank_probe_localfirst.json)
-        # against a modelled ~2 ms of exposed transfers at 64 GB/s per link -- not worth it unmeasured
-        self.local_first = False
+        self.local_first = type(self).local_first
         self.graphs = {}                    # (segment, layer, weights signature) -> CUDAGraph
         self._graph_sig = None
 

@@ -230,13 +230,14 @@ def _sp_model(segs, ratios):
     return m.eval(), cfg
 
 
-def _sp_forward_worker(rank, world, port, N, gp, q):
+def _sp_forward_worker(rank, world, port, N, gp, q, local_first=False):
     try:
         import sp_emulator
         sp_emulator.install()
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)
         torch.set_num_threads(2)
+        seqpar.SeqParallelEngine.local_first = local_first      # class default for the engine built below
         model, _ = _sp_model(*SP_SCHED)
         model.global_pool = gp
         model.enable_sequence_parallel()
@@ -251,15 +252,17 @@ def _sp_forward_worker(rank, world, port, N, gp, q):
         q.put((rank, traceback.format_exc()))
 
 
-@pytest.mark.parametrize("world,N,gp", [(2, 600, False), (3, 700, True)])
-def test_sharded_forward_matches_oracle_with_cpu_kernels(world, N, gp):
+@pytest.mark.parametrize("world,N,gp,local_first", [(2, 600, False, False), (3, 700, True, False),
+                                                    (2, 600, False, True)])
+def test_sharded_forward_matches_oracle_with_cpu_kernels(world, N, gp, local_first):
     """LongNetViT._forward_sp end to end over gloo with every HIP call replaced by an
     address-checking CPU stand-in (tests/sp_emulator.py): shard bounds, K/V and q-halo
     exchange, query windows, window merge, readouts, all-reduce/broadcast."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_sp_forward_worker, args=(r, world, port, N, gp, q)) for r in range(world)]
+    procs = [ctx.Process(target=_sp_forward_worker, args=(r, world, port, N, gp, q, local_first))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=600) for _ in range(world))
