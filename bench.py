@@ -313,12 +313,13 @@ def main():
     }
     if sp:
         result["sp_exchange_mb_per_layer_rank0"] = round(model._sp.plan.exchange_bytes(0) / 1e6, 1)
-        # the SP gather (gp_dilated_sparsify_dests): per branch, read the K and V head-group columns
-        # of this rank's tokens (2*C_b bf16 each) and write one row per destination chunk
+        # the SP gather (gp_dilated_sparsify_dests): per branch that crosses a cut, read the K and V
+        # head-group columns of this rank's tokens (2*C_b bf16 each) and write one row per destination
+        # chunk (transfer-free branches are read in place by the attention: no sparsify bytes)
         plan = model._sp.plan
         a_w, b_w = plan.bounds[rank]
         sp_bytes = sum((b_w - a_w) * 2 * plan.C[b] * 2 + sum(plan.send_splits(rank, b)) * 2 * plan.C[b] * 2
-                       for b in range(len(plan.C)))
+                       for b in range(len(plan.C)) if not plan.no_xfer[b])
         n_sp, ms_sp = kt.get("sparsify", (0, 0.0))
         sp_gbs = sp_bytes / (ms_sp / max(n_sp, 1) / 1e3) / 1e9 if ms_sp > 0 else 0.0
         result["sparsify_roofline"] = {"bound": "hbm", "kernel": "gp_dilated_sparsify_dests",
