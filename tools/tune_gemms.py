@@ -4,6 +4,7 @@ runtime.py loads (tuning disabled) on every later run.
 
     python tools/tune_gemms.py --tiles 70000 16384          # whole forwards of those slide sizes
     python tools/tune_gemms.py --sp-tiles 262144 --sp-worlds 1 2 4 8 [--packed-tiles 675587]
+    python tools/tune_gemms.py --half --tiles 70000 16384   # the fp16 autocast caller's shapes
 
 --sp-tiles tunes, for every rank of every listed world size, the five GEMM shapes that rank's
 sequence-parallel forward issues (rows = its token window from seqpar.ShardPlan, patch rows =
@@ -40,9 +41,8 @@ def sp_shapes(tiles, worlds):
     return sorted(out)
 
 
-def tune_rows(rows, patch_rows, log):
+def tune_rows(rows, patch_rows, log, bf=torch.bfloat16):
     dev = torch.device("cuda")
-    bf = torch.bfloat16
     g = torch.Generator(device=dev).manual_seed(0)
     r = lambda *s: torch.randn(*s, device=dev, generator=g).to(bf)  # noqa: E731
     a, f = r(rows, E), r(rows, F)
@@ -77,6 +77,8 @@ def main():
                     help="TunableOp rotating buffer: time each candidate on operands cycled through this many MB "
                          "(cold caches, as inside the forward) instead of the same warm operands")
     ap.add_argument("--fresh", action="store_true", help="do not start from the entries already in --out")
+    ap.add_argument("--half", action="store_true",
+                    help="fp16 shapes: the reference pipeline's autocast(float16) caller (DESIGN.md §3.3)")
     args = ap.parse_args()
     log = lambda s: print(s, flush=True)  # noqa: E731
     shapes = sp_shapes(args.sp_tiles, args.sp_worlds) if args.sp_tiles else []
@@ -99,14 +101,16 @@ def main():
     n0 = len(torch.cuda.tunable.get_results())
     with torch.no_grad():
         for rows, patch_rows in shapes:
-            tune_rows(rows, patch_rows, log)
+            tune_rows(rows, patch_rows, log, torch.float16 if args.half else torch.bfloat16)
         if args.tiles:
             import bench
             from gigapath import slide_encoder
             model = slide_encoder.create_model("", "gigapath_slide_enc12l768d", 1536).cuda().eval()
             for n in args.tiles:
                 x, c = bench.make_slide(n)
-                model(torch.from_numpy(x).cuda(), torch.from_numpy(c).cuda(), all_layer_embed=True)
+                xt = torch.from_numpy(x).cuda()
+                with torch.autocast("cuda", dtype=torch.float16, enabled=args.half):
+                    model(xt.half() if args.half else xt, torch.from_numpy(c).cuda(), all_layer_embed=True)
                 torch.cuda.synchronize()
                 log("tuned shapes for %d tiles" % n)
     with open(args.out, "w") as fh:                # the loaded + new entries, TunableOp's CSV format
