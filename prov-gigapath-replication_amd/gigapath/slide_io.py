@@ -32,7 +32,7 @@ import numpy as np
 import torch
 
 _SIG = b"\x89HDF\r\n\x1a\n"
-_IO_THREADS = max(1, min(8, os.cpu_count() or 1))
+_IO_THREADS = max(1, min(16, os.cpu_count() or 1))     # the GPU box grants 16 host threads per GPU
 
 
 class _Reader:
