@@ -52,7 +52,6 @@ GP_DEV f32x4 mfma_16x16x32(bf16x8 a, bf16x8 b, f32x4 c) {
 }
 template <bool kH>
 GP_DEV __bf16 f2e_slot(float f) { return __builtin_bit_cast(__bf16, f2e<kH>(f)); }
-
 // Exact unsigned division by a launch constant d < 2^31 via a multiply-high: the merge kernel's
 // per-token divisions are wave-uniform, so they run on the scalar unit instead of ~25 VALU
 // instructions each.  With m = floor(2^32 (2^l - d) / d) + 1, l = ceil(log2 d), the quotient is
@@ -441,9 +440,10 @@ constexpr uint32_t kLseRedo = 0x7fc0dead;
 //   kModeGen (D = 48 / 64, q pre-scaled or not): the same exact arithmetic with register-staged
 //     K/V tiles (global loads, addresses computed once), for k / v layouts the descriptor cannot
 //     cover (the operator seam's separate q / k / v tensors) and for D = 64.
-//   kModeExact (fp16 operands, D = 48, q pre-scaled): the LDS-DMA staging and work decomposition of
-//     kModeFast with the exact running-max arithmetic (no-max p = 2^s would overflow fp16), the
-//     -m start as the accumulator's initial value
+//   kModeExact (D = 48, q pre-scaled): the LDS-DMA staging and work decomposition of kModeFast with the
+//     exact running-max arithmetic, the -m start as the accumulator's initial value (round 2's fp16
+//     product kernel; kept for lab A/B).  fp16 now runs kModeFast with a tile-0 offset (kM0 below) +
+//     kModeFix without the bf16 hi + lo MFMA start.
 enum AttnMode { kModeFast = 0, kModeFix = 1, kModeGen = 2, kModeExact = 3 };
 constexpr int kFixItems = 32;
 
@@ -475,7 +475,7 @@ static_assert(kNWFast == 4 || kNWFast == 8 || kNWFast == 16, "GP_ATTN_NW must be
 
 template <int D, bool kPre, int MODE, bool kTab, int NW, bool kH>
 __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_idx) {
-  static_assert(!kH || MODE == kModeGen || MODE == kModeExact, "fp16 operands: exact kernels only");
+  static_assert(!kH || D == 48 || MODE == kModeGen, "fp16 LDS-DMA modes: D = 48");
   static_assert(D == 48 || D == 64, "v2 kernel covers D = 48 and 64");
   static_assert(MODE == kModeGen || (D == 48 && kPre), "LDS-DMA modes need D = 48 and a pre-scaled q");
   static_assert(NW == 4 || ((NW == 8 || NW == 16) && MODE != kModeGen), "8 / 16 waves: LDS-DMA modes only");
@@ -489,8 +489,13 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   constexpr bool kPV16 = GP_ATTN_PV16 != 0 && MODE == kModeFast && D == 48;
   constexpr bool kOnes = (D % 32) != 0 && !kPV16;   // spare d rows carry the row-sum ones
   constexpr bool kDMA = MODE != kModeGen;
-  constexpr bool kZM = MODE == kModeFast;    // no max, no offset
-  constexpr bool kMI = MODE == kModeFix;     // -m start block from one MFMA
+  constexpr bool kZM = MODE == kModeFast && !kH;   // no max, no offset
+  // fp16 fast mode: p = 2^(s - m0) with m0 the row max of tile 0 only (fp16's range ends at 2^16, so
+  // bf16's offset-free p = 2^s cannot be used); a later key more than 16 log2 units above m0
+  // overflows P to inf, the row is flagged and the fixup pass recomputes it exactly
+  constexpr bool kM0 = MODE == kModeFast && kH;
+  constexpr bool kFlag = MODE == kModeFast;        // flag rows for the fixup pass
+  constexpr bool kMI = MODE == kModeFix && !kH;    // -m start block from one MFMA (bf16 hi + lo pair)
   constexpr int KROWB = D * 2 + 16;          // K image row bytes (padded)
   constexpr int VROWB = 128;                 // V image row bytes (64 bf16, swizzled 32-B blocks)
   constexpr int KTILE = KT * KROWB;
@@ -726,7 +731,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
 
       // ---- online softmax with deferred rescale (two independent max chains)
       float mx = 0.f;
-      if constexpr (!kZM) {
+      if (!kZM && (!kM0 || t == 0)) {
         float mxa = sacc[0][0], mxb = sacc[1][0];
   #pragma unroll
         for (int r = 1; r < 16; ++r) {
@@ -742,7 +747,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
         if constexpr (!kZM) {
           // scores are s*c - m_run; rescale only when a query's max moved up by > kThr
           // (tile 0: always, which sets m_run to that tile's exact max)
-          const bool need = (t == 0) || (mx > kThr);
+          const bool need = (t == 0) || (!kM0 && mx > kThr);
           if (__builtin_amdgcn_ballot_w64(need)) {
             if constexpr (kMI) {
               // m kept as an exact hi + lo pair of bf16 values (two rows of the init MFMA), so it
@@ -896,8 +901,8 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   }
   const int npad = g.m - c;
   bool zm_bad = false;
-  if constexpr (kZM) {
-    m_run = 0.f;
+  if constexpr (kFlag) {
+    if constexpr (kZM) m_run = 0.f;
     const uint32_t eb = __float_as_uint(l) & 0x7f800000u;
     // with zero-pad keys (p = 1 each) a tiny real-key sum is not flagged: the pads then dominate
     // exactly as in the reference
@@ -969,7 +974,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   }
   if (i < rows_needed) {
     float lse = (mr + __builtin_amdgcn_logf(l)) * 0.69314718055994530942f;
-    if constexpr (kZM) {     // overflowed / out of range: flag the row for the fixup pass
+    if constexpr (kFlag) {   // overflowed / out of range: flag the row for the fixup pass
       if ((__float_as_uint(l) & 0x7f800000u) == 0x7f800000u || !(l > 0.f) || zm_bad) lse = __uint_as_float(kLseRedo);
     }
     if (h == 0) brr.lse[((int64_t)bn * a.H + hh) * g.m + i] = lse;
@@ -1234,7 +1239,8 @@ static int attn_fwd_impl(const uint16_t* q, int64_t q_row_stride, int64_t q_tok_
                          int D, int64_t win_lo, int64_t win_hi, const GpAttnBranch* branches, int nbranch,
                          float softmax_scale, int q_log2_prescaled, bool kh, void* stream) {
   // bf16: the no-max LDS-DMA kernel + fixup pass (kModeFast / kModeFix) when the layout allows LDS-DMA
-  // staging, else the register-staged exact kernel; fp16: kModeExact / kModeGen likewise
+  // staging, else the register-staged exact kernel; fp16 likewise (its fast mode offsets p by the
+  // row max of tile 0)
   GP_REQUIRE(D == 48 || D == 64 || D == 96, "gp_dilated_attn_fwd: head dim %d unsupported (48, 64, 96)", D);
   GP_REQUIRE(nbranch >= 1 && nbranch <= GP_MAX_BRANCHES, "gp_dilated_attn_fwd: nbranch must be 1..%d", GP_MAX_BRANCHES);
   GP_REQUIRE(B > 0 && L > 0 && H > 0 && q_row_stride >= (int64_t)H * D && q_row_stride % 8 == 0,
@@ -1331,8 +1337,11 @@ static int attn_fwd_impl(const uint16_t* q, int64_t q_row_stride, int64_t q_tok_
   GP_REQUIRE(items < (int64_t)0x7fffffff, "gp_dilated_attn_fwd: too many work items");
   hipStream_t s = gp_stream(stream);
   if (kh) {
-    if (fast) dilated_attn32_kernel<48, true, kModeExact, false, kNWFast, true><<<(unsigned)items, 64 * kNWFast, 0, s>>>(a);
-    else if (D == 96) dilated_attn_kernel<96, true><<<(unsigned)items, 256, 0, s>>>(a);
+    if (fast) {        // fp16 fast mode (tile-0 offset), then the exact fixup pass
+      dilated_attn32_kernel<48, true, kModeFast, false, kNWFast, true><<<(unsigned)items, 64 * kNWFast, 0, s>>>(a);
+      dilated_attn32_kernel<48, true, kModeFix, false, kNWFast, true>
+          <<<(unsigned)((items + kFixItems - 1) / kFixItems), 64 * kNWFast, 0, s>>>(a);
+    } else if (D == 96) dilated_attn_kernel<96, true><<<(unsigned)items, 256, 0, s>>>(a);
     else if (D == 48 && q_log2_prescaled) dilated_attn32_kernel<48, true, kModeGen, false, 4, true><<<(unsigned)items, 256, 0, s>>>(a);
     else if (D == 48) dilated_attn32_kernel<48, false, kModeGen, false, 4, true><<<(unsigned)items, 256, 0, s>>>(a);
     else if (q_log2_prescaled) dilated_attn32_kernel<64, true, kModeGen, false, 4, true><<<(unsigned)items, 256, 0, s>>>(a);
@@ -1626,8 +1635,10 @@ extern "C" int gp_dilated_attn_fwd_varlen(const void* plan_host, const void* pla
   a.d_H = make_div_magic((uint32_t)h.H);
   // the single-slide default's variant, so each packed slide's outputs equal its own launch's
   if (fmt == GP_FMT_F16) {
-    dilated_attn32_kernel<48, true, kModeExact, true, kNWFast, true>
+    dilated_attn32_kernel<48, true, kModeFast, true, kNWFast, true>
         <<<(unsigned)h.total_items, 64 * kNWFast, 0, gp_stream(stream)>>>(a);
+    dilated_attn32_kernel<48, true, kModeFix, true, kNWFast, true>
+        <<<(unsigned)((h.total_items + kFixItems - 1) / kFixItems), 64 * kNWFast, 0, gp_stream(stream)>>>(a);
     return gp_check_launch("gp_dilated_attn_fwd_varlen");
   }
   dilated_attn32_kernel<48, true, kModeFast, true, kNWFast><<<(unsigned)h.total_items, 64 * kNWFast, 0, gp_stream(stream)>>>(a);

@@ -232,6 +232,33 @@ def test_attention_no_max_overflow_fixup():
     assert (o[0, 0, 0] - v[0, 150, 0]).abs().max().item() <= 1e-2 * max(1.0, v[0, 150, 0].abs().max().item())
 
 
+def test_attention_fp16_fast_mode_overflow_fixup():
+    """fp16 product path (p = 2^(s - m0), m0 = the row max of the first 64-key tile only): head 0's
+    key 150 scores 200 log2 units above everything in tile 0, so its p overflows fp16 and the row is
+    recomputed by the exact fixup pass; head 1's scores climb 30 log2 units per tile (overflow at the
+    second tile); head 2 stays in range (the fast path itself).  All must match the oracle."""
+    h = _hip()
+    B, L, H, D = 1, 300, 16, 48
+    E = H * D
+    qkv = _rand_qkv(B, L, E, seed=23).float() * 0.3
+    qkv[:, 0 * D:2 * D] = 0.0
+    qkv[:, 0 * D] = 8.0
+    qkv[:, 1 * D] = 8.0
+    qkv[:, E:E + 2 * D] = 0.0
+    qkv[150, E] = 25.0
+    qkv[:, E + D] = torch.from_numpy((np.arange(L) // 64) * 3.75).float()
+    qkv = qkv.half()
+    segs, ratios = [300], [1]
+    outs, lses = _run_attn(h, qkv, B, L, H, D, segs, ratios, prescaled=True)
+    q, k, v = (qkv[:, i * E:(i + 1) * E].float().view(B, L, H, D) for i in range(3))
+    o_ref, l_ref = orc.branch_attention(q, k, v, 300, 1, scale=0.6931471805599453)
+    o = outs[0].float().cpu().view(B, 1, L, H, D).permute(0, 1, 3, 2, 4)
+    l = lses[0].cpu().view(B, 1, H, L)
+    assert torch.isfinite(o).all() and torch.isfinite(l).all()
+    assert (o - o_ref).abs().max().item() <= 2e-3 * max(1.0, o_ref.abs().max().item())
+    assert (l - l_ref).abs().max().item() <= 1.5e-3 + 1e-5 * l_ref.abs().max().item()
+
+
 def test_attention_large_scores_and_empty_heads():
     """Large-magnitude scores (online-softmax rescale path) and a segment with no valid keys."""
     h = _hip()
@@ -319,7 +346,7 @@ def test_attention_other_head_dims(D):
 @pytest.mark.parametrize("name,B,L,segs,ratios", ATTN_CASES)
 def test_dilated_attention_fp16_vs_oracle(name, B, L, segs, ratios, prescaled):
     """fp16 q/k/v (the forward under the reference pipeline's fp16 autocast): pre-scaled q runs the
-    LDS-DMA exact kernel (kModeExact, the product layout), otherwise the register-staged one.  P is
+    LDS-DMA fp16 fast kernel + fixup pass (the product layout), otherwise the register-staged one.  P is
     rounded to fp16 (11 significant bits): o within 2e-3, lse within 1.5e-3 of the fp32 oracle."""
     h = _hip()
     H, D = 16, 48
