@@ -54,15 +54,28 @@ def make_slide(n_tiles, seed=1, in_chans=1536, tile=256):
     return x, coords
 
 
-def cpu_baseline(n_tiles, threads):
-    """fp32 CPU oracle on a bounded sample: patch embed + pos add + ONE of the 12 encoder layers
-    of the same slide, extrapolated to the full 12-layer forward."""
+def host_cores():
+    """(threads used for the CPU baseline, usable cores = this process's affinity mask, os.cpu_count()).
+    The GPU box shows the whole machine in os.cpu_count(); the affinity mask is what this job may use."""
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = os.cpu_count() or 1
+    return min(16, usable), usable, os.cpu_count() or usable
+
+
+def cpu_baseline(n_tiles, threads, sample_tiles=70000, total_tflops=None):
+    """fp32 CPU oracle on a bounded sample: patch embed + pos add + ONE of the 12 encoder layers of
+    a slide of min(n_tiles, sample_tiles) tiles, extrapolated to the full 12-layer forward; for a
+    larger workload (C4's 256k slide, the C5 batch) further scaled by the valid-FLOP ratio of the
+    workload to the sampled forward (`total_tflops` = the workload's model TFLOP)."""
     import oracle
     torch.set_num_threads(threads)
     cfg = oracle.arch_config(ARCH)
     W = {k: torch.from_numpy(v) for k, v in oracle.make_weights(cfg, seed=0).items()
          if k.startswith(("patch_embed", "cls_token", "encoder.layers.0."))}
-    x, coords = make_slide(n_tiles)
+    ns = min(n_tiles, sample_tiles)
+    x, coords = make_slide(ns)
     with torch.no_grad():
         t0 = time.perf_counter()
         h = torch.nn.functional.linear(torch.from_numpy(x), W["patch_embed.proj.weight"], W["patch_embed.proj.bias"])
@@ -73,9 +86,21 @@ def cpu_baseline(n_tiles, threads):
         oracle.encoder_layer(h, W, "encoder.layers.0", cfg["segment_length"], cfg["dilated_ratio"], 16)
         t2 = time.perf_counter()
     full = (t1 - t0) + cfg["depth"] * (t2 - t1)
-    return {"value": round(n_tiles / full, 2), "unit": "tiles/s", "cores": threads, "kind": "port",
-            "sample": "EXTRAPOLATED: oracle fp32 torch-CPU, embed + 1 of 12 layers of the %d-tile slide (%.1f s), "
-                      "x12 layers (%.1f s per forward)" % (n_tiles, t2 - t0, full)}
+    _, usable, ncpu = host_cores()
+    res = {"value": round(ns / full, 2), "unit": "tiles/s", "cores": threads, "usable_cores": usable,
+           "cpu_count": ncpu, "kind": "port",
+           "sample": "EXTRAPOLATED: oracle fp32 torch-CPU, embed + 1 of 12 layers of the %d-tile slide (%.1f s), "
+                     "x12 layers (%.1f s per forward)" % (ns, t2 - t0, full)}
+    if total_tflops is not None and ns != n_tiles:
+        from gigapath import runtime
+        segs, ratios = cfg["segment_length"], cfg["dilated_ratio"]
+        sample_tf = (runtime.gemm_flops(1, ns, 768, 3072, 1536, 12)
+                     + 12 * runtime.attention_valid_flops(ns + 1, segs, ratios, 16, 48)) / 1e12
+        secs = full * total_tflops / sample_tf
+        res["value"] = round(n_tiles / secs, 2)
+        res["sample"] += ("; scaled to the %d-tile workload by its valid FLOPs (%.2f / %.2f TFLOP): %.0f s"
+                          % (n_tiles, total_tflops, sample_tf, secs))
+    return res
 
 
 def cpu_full_forwards(sizes, threads):
@@ -96,6 +121,34 @@ def cpu_full_forwards(sizes, threads):
         res[name] = {"tiles": n, "value": round(n / dt, 2), "unit": "tiles/s", "seconds": round(dt, 2),
                      "cores": threads, "kind": "port", "sample": "full 12-layer fp32 forward, timed"}
     return res
+
+
+def sp_rank_report(model, kt, rank, timing_steps, L, segs, ratios, monitor):
+    """This rank's line of the N > 1 report: its shard, bytes over xGMI per layer, exposed exchange
+    wait per layer (monitor), and its attention / sparsify kernels against their rooflines."""
+    from gigapath import runtime
+    plan = model._sp.plan
+    a_w, b_w = plan.bounds[rank]
+    nl = len(model.encoder.layers)
+    recv = plan.exchange_bytes(rank)
+    send = sum((hi - lo) * 2 * plan.C[b] * 2 for b, _, lo, hi in plan.sends(rank))
+    send += sum((hi - lo) * 3 * plan.E * 2 for _, lo, hi in plan.halo_sends(rank))
+    fl = runtime.attention_valid_flops_window(L, segs, ratios, 16, 48, a_w, b_w)
+    n_att, ms_att = kt.get("attn", (0, 0.0))
+    att_s = ms_att / max(timing_steps * nl, 1) / 1e3
+    sp_bytes = sum((b_w - a_w) * 2 * plan.C[b] * 2 + sum(plan.send_splits(rank, b)) * 2 * plan.C[b] * 2
+                   for b in range(len(plan.C)) if not plan.no_xfer[b])
+    n_sp, ms_sp = kt.get("sparsify", (0, 0.0))
+    rep = {"rank": rank, "tokens": [a_w, b_w], "recv_mb_per_layer": round(recv / 1e6, 2),
+           "send_mb_per_layer": round(send / 1e6, 2),
+           "attn_ms_per_layer": round(att_s * 1e3, 4),
+           "attn_tflops": round(fl / att_s / 1e12, 1) if att_s > 0 else None,
+           "attn_frac": round(fl / att_s / 1e12 / PEAK_BF16_TFLOPS, 4) if att_s > 0 else None,
+           "sparsify_gbs": round(sp_bytes / (ms_sp / n_sp / 1e3) / 1e9, 1) if ms_sp > 0 else None,
+           "kernel_ms_per_step": {k: round(v[1] / timing_steps, 3) for k, v in sorted(kt.items())}}
+    if monitor is not None:
+        rep["exchange_exposed"] = monitor.summary(nl)
+    return rep
 
 
 def config_label(n_tiles, world, sp):
@@ -214,9 +267,19 @@ def main():
         def step():
             return model(xt, ct, all_layer_embed=True)
 
+    monitor = None
+    if sp:
+        # exchange instrumentation + collective watchdog (seqpar.ExchangeMonitor) on the first warm-up
+        # step and the per-kernel timing pass only: it syncs the host at every wait
+        from gigapath import seqpar
+        monitor = seqpar.ExchangeMonitor(bound_s=float(os.environ.get("GP_SP_WATCHDOG_S", "180")), rank=rank)
+        model._sp.set_monitor(monitor)
     with torch.no_grad():
-        for _ in range(args.warmup):
+        for i in range(args.warmup):
             step()
+            if monitor is not None and i == 0:
+                torch.cuda.synchronize(dev)
+                model._sp.set_monitor(None)
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
@@ -232,10 +295,16 @@ def main():
         # work to the timed steps; a kernel's duration does not depend on how it was launched
         runtime.TIMER.reset()
         runtime.TIMER.enabled = True
+        if monitor is not None:              # drop the warm-up's records (it included graph capture)
+            monitor._pending.clear()
+            monitor.records.clear()
+            model._sp.set_monitor(monitor)
         for _ in range(args.timing_steps):
             step()
         torch.cuda.synchronize(dev)
         runtime.TIMER.enabled = False
+        if monitor is not None:
+            model._sp.set_monitor(None)
     elapsed = t1 - t0
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
@@ -326,10 +395,19 @@ def main():
                                        "achieved": round(sp_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                                        "frac": round(sp_gbs / PEAK_HBM_GBS, 4), "traffic": None,
                                        "bytes_per_launch": sp_bytes}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not mixed:
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        result["cpu_baseline"] = cpu_baseline(args.tiles, threads)
-        if not args.no_cpu_full:
+        # every rank's view (shard, xGMI bytes, exposed exchange wait, kernel rooflines), gathered
+        mine_rep = sp_rank_report(model, kt, rank, args.timing_steps, L, segs, ratios, monitor)
+        reps = [None] * world
+        dist.all_gather_object(reps, mine_rep)
+        result["sp_ranks"] = reps
+        result["sp_exchange_exposed_ms_per_layer_max"] = max(
+            r["exchange_exposed"]["ms_per_layer"] for r in reps)
+        result["sp_transport"] = "rccl" if backend == "nccl" else backend + " (host-staged rehearsal)"
+    if rank == 0 and not args.no_cpu_baseline:
+        threads, usable, ncpu = host_cores()
+        threads = args.cpu_threads or threads
+        result["cpu_baseline"] = cpu_baseline(args.tiles, threads, total_tflops=total_tf)
+        if world == 1 and not mixed and not args.no_cpu_full:
             result["cpu_full_forwards"] = cpu_full_forwards([("C1", 1024), ("C2", 16384)], threads)
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -424,7 +424,8 @@ GP_DEV float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 // lse bit pattern (a quiet NaN no real row produces) that flags a row for the fixup pass
 constexpr uint32_t kLseRedo = 0x7fc0dead;
 
-// Three builds of the v2 kernel (all 4 waves x 32 queries, 64-key K/V tiles, one barrier per tile):
+// Builds of the v2 kernel (NW waves x 32 queries per workgroup -- 8 for the LDS-DMA modes, 4 for kModeGen --
+// sharing each 64-key K/V tile, one barrier per tile):
 //   kModeFast (D = 48, q pre-scaled by D^-0.5*log2 e; the product launch): K/V tiles staged by
 //     LDS-DMA (buffer_load ... lds, 1 KiB per wave-instruction, lane-linear) straight into the
 //     padded K image and the swizzled V image through a per-tile buffer descriptor whose record
@@ -528,6 +529,15 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
     if (threadIdx.x < QB && i < rows_needed)
       flagged = __float_as_uint(brr.lse[((int64_t)wi.bn * a.H + wi.hh) * g.m + i]) == kLseRedo;
     if (!__syncthreads_or(flagged)) return;
+  }
+  // kModeFix rewrites ONLY the rows the fast kernel flagged (each query's own lse still holds the
+  // marker here: only this block writes it), so an unflagged row keeps the fast kernel's bits whatever
+  // items share its fixup block -- a packed (varlen) slide's rows never depend on a neighbour's overflow
+  bool fixrow = true;
+  if constexpr (MODE == kModeFix) {
+    const int iq = q0 + (int)(threadIdx.x >> 6) * 32 + (int)(threadIdx.x & 31);
+    fixrow = iq < rows_needed &&
+             __float_as_uint(brr.lse[((int64_t)wi.bn * a.H + wi.hh) * g.m + iq]) == kLseRedo;
   }
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -925,7 +935,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
       const int qq = (lane & 15) + 16 * nb;
       const float iv = __shfl(inv, qq, 64);
       const int iq = q0 + w * 32 + qq;
-      if (iq < rows_needed) {
+      if (iq < rows_needed && __shfl(fixrow ? 1 : 0, qq, 64)) {
         uint16_t* orow = brr.o + (((int64_t)bn * g.m + iq) * a.H + hh) * (int64_t)D + 4 * (lane >> 4);
 #pragma unroll
         for (int dt = 0; dt < 3; ++dt) {
@@ -952,13 +962,13 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
       pk[k].x = rx[0]; pk[k + 1].x = rx[1];
       pk[k].y = ry[0]; pk[k + 1].y = ry[1];
     }
-    if (i < rows_needed) {
+    if (i < rows_needed && fixrow) {
       uint16_t* orow = brr.o + (((int64_t)bn * g.m + i) * a.H + hh) * (int64_t)D + 8 * h;
 #pragma unroll
       for (int k = 0; k < D / 8; k += 2)
         *reinterpret_cast<uint4*>(orow + 8 * k) = make_uint4(pk[k].x, pk[k].y, pk[k + 1].x, pk[k + 1].y);
     }
-  } else if (i < rows_needed) {
+  } else if (i < rows_needed && fixrow) {
     uint16_t* orow = brr.o + (((int64_t)bn * g.m + i) * a.H + hh) * (int64_t)D;
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
@@ -972,7 +982,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
         }
       }
   }
-  if (i < rows_needed) {
+  if (i < rows_needed && fixrow) {
     float lse = (mr + __builtin_amdgcn_logf(l)) * 0.69314718055994530942f;
     if constexpr (kFlag) {   // overflowed / out of range: flag the row for the fixup pass
       if ((__float_as_uint(l) & 0x7f800000u) == 0x7f800000u || !(l > 0.f) || zm_bad) lse = __uint_as_float(kLseRedo);

@@ -346,6 +346,11 @@ class EncoderEngine:
         self._sig = None
         self.layers: List[PackedLayer] = []
         self._packs: Dict[torch.dtype, tuple] = {}     # act -> (signature, packed layers)
+        # activation workspaces per CALLER STREAM: two streams never share activation buffers, so
+        # forwards (and HIP graphs, which bake the workspace of the stream they were captured on)
+        # issued on different streams can run concurrently; ws / pws = the last one used
+        self._ws: Dict[int, Workspace] = {}
+        self._pws: Dict[int, PackedWorkspace] = {}
         self.ws: Optional[Workspace] = None
         self.pws: Optional[PackedWorkspace] = None
 
@@ -362,21 +367,31 @@ class EncoderEngine:
         self._sig, self.layers = ent
         return self.layers
 
+    @staticmethod
+    def _stream_key(dev) -> int:
+        return int(torch.cuda.current_stream(dev).cuda_stream) if torch.device(dev).type == "cuda" else 0
+
     def workspace(self, dev, B, L, E, F, H, segs, ratios, act: Optional[torch.dtype] = None) -> Workspace:
         act = act or act_dtype()
         key = (str(dev), B, L, E, F, H, tuple(segs), tuple(ratios), act)
-        if self.ws is None or self.ws.key != key:
-            self.ws = None
-            self.ws = Workspace(dev, B, L, E, F, H, segs, ratios, act)
-        return self.ws
+        sk = self._stream_key(dev)
+        ws = self._ws.get(sk)
+        if ws is None or ws.key != key:
+            self._ws.pop(sk, None)             # (a HIP graph that baked the old one keeps it alive)
+            ws = self._ws[sk] = Workspace(dev, B, L, E, F, H, segs, ratios, act)
+        self.ws = ws
+        return ws
 
     def workspace_packed(self, dev, Ls, E, F, H, segs, ratios, act: Optional[torch.dtype] = None) -> PackedWorkspace:
         act = act or act_dtype()
         key = (str(dev), tuple(int(x) for x in Ls), E, F, H, tuple(segs), tuple(ratios), act)
-        if self.pws is None or self.pws.key != key:
-            self.pws = None
-            self.pws = PackedWorkspace(dev, Ls, E, F, H, segs, ratios, act)
-        return self.pws
+        sk = self._stream_key(dev)
+        ws = self._pws.get(sk)
+        if ws is None or ws.key != key:
+            self._pws.pop(sk, None)
+            ws = self._pws[sk] = PackedWorkspace(dev, Ls, E, F, H, segs, ratios, act)
+        self.pws = ws
+        return ws
 
     def run_layers(self, ws: Workspace, B: int, L: int, layer_hook=None):
         """ws.x holds the fp32 embedding and ws.a = LN1_0(ws.x) (16-bit).  Runs every layer in

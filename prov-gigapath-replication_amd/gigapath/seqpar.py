@@ -31,6 +31,10 @@ output up to the GEMMs' row-count-dependent kernel choice.  Inference only, B = 
 """
 from __future__ import annotations
 
+import os
+import sys
+import threading
+import time
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -334,6 +338,69 @@ class Exchange:
             wk.wait()
 
 
+class ExchangeMonitor:
+    """Per-phase instrumentation and collective watchdog of the sharded forward's exchanges.
+
+    Attached to a ``SeqParallelEngine`` for diagnostic steps only (bench.py: the first warm-up step
+    and the per-kernel timing pass; never the timed steps, since it syncs the host at every wait).
+    RCCL: a HIP event on the compute stream right before each ``Exchange.wait`` and one right after
+    it; their distance is the time the compute stream sat waiting for that phase's transfers -- the
+    EXPOSED exchange time the attention launched meanwhile did not hide.  gloo (host-staged,
+    synchronous): the host time of the exchange calls themselves.  Watchdog: while a wait (RCCL: the
+    post-wait event, polled) or a synchronous exchange (gloo) is outstanding, a daemon thread checks
+    it against ``bound_s``; past it, it prints layer / phase / branches / peers to stderr and ends the
+    process with exit status 3 (``os._exit``: no exec, no retry), so a stuck collective names itself
+    instead of hanging the job until the launcher's timeout."""
+
+    def __init__(self, bound_s: float = 120.0, rank: int = 0):
+        self.bound_s = float(bound_s)
+        self.rank = rank
+        self.records: List[dict] = []
+        self._pending = []                   # RCCL (layer, phase, e0, e1) until resolve()
+        self._armed: Optional[Tuple[float, str]] = None
+        self._lock = threading.Lock()
+        self._thread = threading.Thread(target=self._watch, name="sp-exchange-watchdog", daemon=True)
+        self._thread.start()
+
+    def _watch(self):
+        while True:
+            time.sleep(0.25)
+            with self._lock:
+                armed = self._armed
+            if armed is not None and time.monotonic() - armed[0] > self.bound_s:
+                sys.stderr.write("SP exchange watchdog (rank %d): %s outstanding for > %.0f s -- exiting\n"
+                                 % (self.rank, armed[1], self.bound_s))
+                sys.stderr.flush()
+                os._exit(3)
+
+    def arm(self, label: str):
+        with self._lock:
+            self._armed = (time.monotonic(), label)
+
+    def disarm(self):
+        with self._lock:
+            self._armed = None
+
+    def resolve(self):
+        """Turn the pending RCCL event pairs into records (call after a device synchronize)."""
+        for li, ph, e0, e1 in self._pending:
+            self.records.append({"layer": li, "phase": ph, "kind": "stream_wait", "ms": e0.elapsed_time(e1)})
+        self._pending = []
+
+    def summary(self, n_layers: int) -> dict:
+        """Exposed exchange ms per layer (mean over the recorded forwards), per phase and in total."""
+        self.resolve()
+        n_fw = max(1, sum(1 for r in self.records if r["layer"] == 0 and r["phase"] == "A"))
+        by_phase: Dict[str, float] = {}
+        for r in self.records:
+            by_phase[r["phase"]] = by_phase.get(r["phase"], 0.0) + r["ms"]
+        per_layer = {ph: round(v / n_fw / max(n_layers, 1), 4) for ph, v in sorted(by_phase.items())}
+        return {"kind": sorted({r["kind"] for r in self.records}), "forwards": n_fw,
+                "ms_per_layer_by_phase": per_layer,
+                "ms_per_layer": round(sum(per_layer.values()), 4),
+                "ms_per_forward": round(sum(per_layer.values()) * n_layers, 3)}
+
+
 # ------------------------------------------------------------------------------------------
 # per-rank engine
 # ------------------------------------------------------------------------------------------
@@ -389,6 +456,7 @@ class SeqParallelEngine:
         self._rsplit = [plan.recv_splits(rank, b) for b in range(len(plan.geo))]
         self.use_graphs = False
         self.local_first = type(self).local_first
+        self.monitor: Optional[ExchangeMonitor] = None   # diagnostic steps only (bench.py)
         self.graphs = {}                    # (segment, layer, weights signature) -> CUDAGraph
         self._graph_sig = None
 
@@ -428,6 +496,49 @@ class SeqParallelEngine:
             if not plan.no_xfer[b]:
                 handles += self.xch.all_to_all(ws.kvs[b], ws.send[b], self._rsplit[b], self._ssplit[b]) or []
         return handles
+
+    def _peers(self, branches: List[int]) -> List[int]:
+        plan = self.plan
+        ps = set()
+        for b in branches:
+            for v, (ns, nr) in enumerate(zip(self._ssplit[b], self._rsplit[b])):
+                if v != self.rank and (ns or nr) and not plan.no_xfer[b]:
+                    ps.add(v)
+        return sorted(ps)
+
+    def _label(self, li: int, ph: str, branches: List[int]) -> str:
+        return "layer %d phase %s branches %s peers %s" % (li, ph, branches, self._peers(branches))
+
+    def _post(self, ws: ShardWorkspace, branches: List[int], halo: bool, li: int, ph: str):
+        """exchange() under the monitor: a synchronous (gloo) exchange is timed and watched."""
+        mon = self.monitor
+        if mon is None or self.xch.device_comm:
+            return self.exchange(ws, branches, halo)
+        mon.arm(self._label(li, ph, branches))
+        t0 = time.perf_counter()
+        h = self.exchange(ws, branches, halo)
+        mon.records.append({"layer": li, "phase": ph, "kind": "host_exchange",
+                            "ms": (time.perf_counter() - t0) * 1e3})
+        mon.disarm()
+        return h
+
+    def _wait(self, handles, li: int, ph: str, branches: List[int]):
+        """Exchange.wait under the monitor: events around the stream wait, the post-wait event polled
+        against the watchdog bound."""
+        mon = self.monitor
+        if mon is None or not self.xch.device_comm:
+            Exchange.wait(handles)
+            return
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        Exchange.wait(handles)
+        e1.record()
+        mon.arm(self._label(li, ph, branches))
+        while not e1.query():
+            time.sleep(2e-5)
+        mon.disarm()
+        mon._pending.append((li, ph, e0, e1))
 
     def attention(self, pa: runtime.PackedAttention, ws: ShardWorkspace, branches: List[int]):
         if not branches:
@@ -514,16 +625,16 @@ class SeqParallelEngine:
                                             nxt.ln1_b if nxt else None, nxt.ln1_eps if nxt else 1e-5, ws.a, M, E)
 
             self._segment(("head", li, wsig), head)
-            h_a = self.exchange(ws, plan.phase_a, halo=True)
-            h_b1 = self.exchange(ws, plan.phase_b1, halo=False)
-            h_b2 = self.exchange(ws, plan.phase_b2, halo=False)
+            h_a = self._post(ws, plan.phase_a, True, li, "A")
+            h_b1 = self._post(ws, plan.phase_b1, False, li, "B1")
+            h_b2 = self._post(ws, plan.phase_b2, False, li, "B2")
             self.attention(pa, ws, local)          # needs no transfer: runs while they all fly
-            Exchange.wait(h_a)
+            self._wait(h_a, li, "A", plan.phase_a)
             self.attention(pa, ws, ph_a)
-            Exchange.wait(h_b1)
+            self._wait(h_b1, li, "B1", plan.phase_b1)
             if plan.phase_b2:                      # the middle phase runs while the last transfers
                 self.attention(pa, ws, ph_b1)
-            Exchange.wait(h_b2)
+            self._wait(h_b2, li, "B2", plan.phase_b2)
             self._segment(("tail", li, wsig), tail)
             if layer_hook is not None:
                 layer_hook(li + 1)
@@ -544,6 +655,13 @@ class SeqParallelContext:
         self.plan: Optional[ShardPlan] = None
         self.ws: Optional[ShardWorkspace] = None
         self.engine: Optional[SeqParallelEngine] = None
+        self.monitor: Optional[ExchangeMonitor] = None
+
+    def set_monitor(self, monitor: Optional[ExchangeMonitor]):
+        """Attach (or, with None, detach) an ExchangeMonitor to this and every later engine."""
+        self.monitor = monitor
+        if self.engine is not None:
+            self.engine.monitor = monitor
 
     def prepare(self, dev, L: int, segs, ratios, H: int, D: int, F: int, act: torch.dtype = torch.bfloat16):
         key = (str(dev), L, tuple(segs), tuple(ratios), H, D, F, act)
@@ -555,5 +673,6 @@ class SeqParallelContext:
             self.plan = ShardPlan(L, self.world, segs, ratios, H, D, F)
             self.ws = ShardWorkspace(self.plan, self.rank, dev, F, act)
             self.engine = SeqParallelEngine(self.plan, self.rank, self.exchange)
+            self.engine.monitor = self.monitor
             self._key = key
         return self.plan, self.ws, self.engine

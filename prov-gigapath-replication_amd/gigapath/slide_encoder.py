@@ -238,11 +238,16 @@ class LongNetViT(nn.Module):
                              (self.slide_ngrids ** 2 + 1, int(err.item())))
 
     def graph_stream(self):
-        """The side stream graphs are captured on (one per device)."""
+        """The side stream graphs are captured on: one per (device, CALLER stream).  A captured GEMM
+        bakes the hipBLASLt workspace of the stream it was captured on (PyTorch keeps one per
+        (handle, stream): ATen/cuda/CUDAContextLight.h cublaslt_handle_stream_to_workspace) and the
+        engine's activation workspace of that stream, so graphs of different caller streams never
+        share either and may replay concurrently; graphs of one caller stream replay in its order."""
         dev = self.cls_token.device
-        if str(dev) not in self._capture_streams:
-            self._capture_streams[str(dev)] = torch.cuda.Stream(device=dev)
-        return self._capture_streams[str(dev)]
+        key = (str(dev), int(torch.cuda.current_stream(dev).cuda_stream))
+        if key not in self._capture_streams:
+            self._capture_streams[key] = torch.cuda.Stream(device=dev)
+        return self._capture_streams[key]
 
     def graph_entry(self, x, c, all_layer_embed):
         """(graph, static x, static coords, static outputs) for this input shape, captured if not
@@ -251,8 +256,9 @@ class LongNetViT(nn.Module):
         dev = self.cls_token.device
         self._packed_top(dev)
         self.encoder.engine.pack(self.encoder, dev)
-        key = (str(dev), tuple(x.shape), x.dtype, c.dtype, runtime.act_dtype(), bool(all_layer_embed),
-               bool(self.global_pool), self._top_sig, self.encoder.engine._sig)
+        key = (str(dev), int(torch.cuda.current_stream(dev).cuda_stream), tuple(x.shape), x.dtype, c.dtype,
+               runtime.act_dtype(), bool(all_layer_embed), bool(self.global_pool), self._top_sig,
+               self.encoder.engine._sig)
         ent = self._graph_lookup(key)
         if ent is None and self._graph_wanted(key):
             ent = self._capture(key, x, c, lambda sx, sc: self._forward_device(sx, sc, all_layer_embed, False),
@@ -293,12 +299,23 @@ class LongNetViT(nn.Module):
                 tot += LongNetViT._tensor_bytes(v, seen)
         return tot
 
+    @staticmethod
+    def _weights_sig(key):
+        """(top weights signature, encoder (device, param_signature)) of a graph key, whose last two
+        entries are self._top_sig and EncoderEngine._sig = (device, param_signature, act)."""
+        eng = key[-1]
+        return key[-2], (tuple(eng[:2]) if isinstance(eng, tuple) else eng)
+
     def _capture(self, key, x, c, run, workspace):
         """Capture run(static_x, static_coords) -> outputs on the side stream (after one eager
         warm-up run there: allocations, TunableOp lookups) and cache it under `key`, keeping the
         workspace the graph bakes in (workspace() after the warm-up) alive with it."""
-        sig = key[-2:]                                             # (top, encoder) weight signatures
-        for old in [k for k in self._graphs if k[-2:] != sig]:    # superseded weights never replay
+        # superseded weights never replay: drop graphs whose (top, encoder) WEIGHT signatures differ.
+        # The encoder signature's activation format is left out of that comparison (it stays in the
+        # lookup key): a bf16 and an fp16 caller each keep their graphs, as pack() keeps one packing
+        # per format
+        sig = self._weights_sig(key)
+        for old in [k for k in self._graphs if self._weights_sig(k) != sig]:
             self._drop_graph(old)
         stream = self.graph_stream()
         # the static input is kept in the activation format (the forward's first use converts to it
@@ -366,8 +383,9 @@ class LongNetViT(nn.Module):
         if self.use_hip_graphs and not runtime.TIMER.enabled:
             self._packed_top(dev)
             self.encoder.engine.pack(self.encoder, dev)
-            key = ("packed", str(dev), Ns, x_cat.dtype, c_cat.dtype, runtime.act_dtype(), bool(all_layer_embed),
-                   bool(self.global_pool), self._top_sig, self.encoder.engine._sig)
+            key = ("packed", str(dev), int(torch.cuda.current_stream(dev).cuda_stream), Ns, x_cat.dtype,
+                   c_cat.dtype, runtime.act_dtype(), bool(all_layer_embed), bool(self.global_pool),
+                   self._top_sig, self.encoder.engine._sig)
             ent = self._graph_lookup(key)
             if ent is None and self._graph_wanted(key):
                 ent = self._capture(key, x_cat, c_cat,

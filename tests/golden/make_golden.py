@@ -191,9 +191,15 @@ def main():
 
 
 def add_e2e(N, B=1):
-    """Append ONE end-to-end case (all_layer_embed and last output, fp32 reference) to the existing
-    golden set without regenerating the others:  python tests/golden/make_golden.py --e2e 16384
-    (config C2; ~1 min on 8 CPU threads)."""
+    """Append ONE end-to-end case to the existing golden set without regenerating the others:
+    python tests/golden/make_golden.py --e2e 16384   (C2, ~1 min on 8 CPU threads;
+    C3 = 70000 ~5 min, C4 = 256000 ~25 min).
+
+    ONE fp32 reference forward with all_layer_embed=True; a forward hook on the reference's
+    Encoder keeps its returned dict, so the default output (encoder_out, which the reference
+    passes through encoder.layer_norm whatever return_all_hiddens is, encoder.py:387-388) and the
+    global-pool readouts (slide_encoder.py:213-221) come from the same run through the
+    reference's own `norm` module instead of three more forwards."""
     t0 = time.time()
     se, _, _ = ref_harness.load_reference()
     arch = "gigapath_slide_enc12l768d"
@@ -206,17 +212,30 @@ def add_e2e(N, B=1):
     model.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()}, strict=True)
     x, coords = orc.synthetic_slide(N, B=B)
     res = {"x_sha256": sha(x), "coords_sha256": sha(coords)}
+    kept = {}
+    hook = model.encoder.register_forward_hook(lambda mod, inp, out: kept.update(out))
     with torch.no_grad():
         xt, ct = torch.from_numpy(x), torch.from_numpy(coords)
         t1 = time.time()
         allv = torch.stack(model(xt, ct, all_layer_embed=True), 0).numpy()
         res["sec_all_layer"] = time.time() - t1
-        last = model(xt, ct)[0].numpy()
-    save("e2e_N%d_B%d.npz" % (N, B), all_layer=allv, last=last)
+        hook.remove()
+        last = model.norm(kept["encoder_out"])[:, 0].numpy()
+        gp = torch.stack([model.norm(h[:, 1:, :].mean(dim=1)) for h in kept["encoder_states"]],
+                         0).numpy()
+        gp_last = model.norm(kept["encoder_out"][:, 1:, :].mean(dim=1)).numpy()
+        # the hooked states reproduce the returned list exactly (same tensors, same norm)
+        chk = torch.stack([model.norm(h)[:, 0] for h in kept["encoder_states"]], 0).numpy()
+        assert np.array_equal(chk, allv)
+    del kept
+    save("e2e_N%d_B%d.npz" % (N, B), all_layer=allv, last=last, gp_all_layer=gp, gp_last=gp_last)
     res.update(N=N, B=B)
     meta["e2e"] = [e for e in meta["e2e"] if not (e["N"] == N and e["B"] == B)] + [res]
+    with open(os.path.join(HERE, "golden_meta.json")) as f2:
+        meta2 = json.load(f2)          # another --e2e run may have appended meanwhile
+    meta2["e2e"] = [e for e in meta2["e2e"] if not (e["N"] == N and e["B"] == B)] + [res]
     with open(os.path.join(HERE, "golden_meta.json"), "w") as f:
-        json.dump(meta, f, indent=1)
+        json.dump(meta2, f, indent=1)
     print("e2e", N, B, "done %.1fs" % (time.time() - t0))
 
 

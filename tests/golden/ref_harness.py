@@ -62,11 +62,15 @@ def flash_attn_fp32(q, k, v, dropout=0.0, bias=None, softmax_scale=None, is_caus
     vf = v.float().permute(0, 2, 1, 3)
     out = torch.empty(B, H, L, D, dtype=torch.float32)
     lse = torch.empty(B, H, L, dtype=torch.float32)
-    for i0 in range(0, L, chunk):
-        s = torch.matmul(qf[:, :, i0:i0 + chunk], kf) * scale
-        l_ = torch.logsumexp(s, dim=-1)
-        out[:, :, i0:i0 + chunk] = torch.matmul(torch.exp(s - l_[..., None]), vf)
-        lse[:, :, i0:i0 + chunk] = l_
+    # chunked over query rows AND over the batch (segments) so one score block stays <= ~256 MB (the
+    # 256k slide's 251 x 1,024-token segments would otherwise need 17 GB per block)
+    bc = max(1, (64 << 20) // (H * min(chunk, L) * L))
+    for b0 in range(0, B, bc):
+        for i0 in range(0, L, chunk):
+            s = torch.matmul(qf[b0:b0 + bc, :, i0:i0 + chunk], kf[b0:b0 + bc]) * scale
+            l_ = torch.logsumexp(s, dim=-1)
+            out[b0:b0 + bc, :, i0:i0 + chunk] = torch.matmul(torch.exp(s - l_[..., None]), vf[b0:b0 + bc])
+            lse[b0:b0 + bc, :, i0:i0 + chunk] = l_
     return out.permute(0, 2, 1, 3).to(q.dtype).contiguous(), lse
 
 

@@ -28,6 +28,32 @@ def _pad8(b: bytes) -> bytes:
     return b + b"\0" * (-len(b) % 8)
 
 
+def fletcher32_spec(data: bytes) -> int:
+    """Fletcher-32 as the HDF5 spec's reference loop computes it (written independently of the
+    reader's vectorised form): big-endian 16-bit words in blocks of 360, both sums folded after each
+    block, an odd last byte as a high byte, two final folds."""
+    s1 = s2 = 0
+    nw = len(data) // 2
+    i = 0
+    while nw:
+        t = min(nw, 360)
+        nw -= t
+        for _ in range(t):
+            s1 += (data[i] << 8) | data[i + 1]
+            i += 2
+            s2 += s1
+        s1 = (s1 & 0xffff) + (s1 >> 16)
+        s2 = (s2 & 0xffff) + (s2 >> 16)
+    if len(data) % 2:
+        s1 += data[i] << 8
+        s2 += s1
+        s1 = (s1 & 0xffff) + (s1 >> 16)
+        s2 = (s2 & 0xffff) + (s2 >> 16)
+    s1 = (s1 & 0xffff) + (s1 >> 16)
+    s2 = (s2 & 0xffff) + (s2 >> 16)
+    return (s2 << 16) | s1
+
+
 class _File:
     def __init__(self, base: int):
         self.base = base
@@ -197,7 +223,7 @@ class Writer:
             elif fl == "deflate":
                 raw = zlib.compress(raw, 4)
             elif fl == "fletcher32":
-                raw = raw + struct.pack("<I", zlib.adler32(raw))   # checksum value is not verified by readers here
+                raw = raw + struct.pack("<I", fletcher32_spec(raw))
         return raw
 
     def _chunked(self, f: _File, data: np.ndarray, chunks, filters, leaf_max, alloc_seed=None):

@@ -79,35 +79,45 @@ def test_mixed_batch_graph_replays_bit_exact():
     assert len(model._graphs) == 5
 
 
-def test_varlen_attention_and_merge_bit_exact_per_slide():
+@pytest.mark.parametrize("fmt", ["bf16", "fp16_overflow"])
+def test_varlen_attention_and_merge_bit_exact_per_slide(fmt):
     """One varlen launch over packed slides == the single-slide kernels on each slide's rows,
-    bit for bit (same per-item math; each slide keeps its own segment schedule)."""
+    bit for bit (same per-item math; each slide keeps its own segment schedule).  fp16_overflow: the
+    first slide's head-0 scores spike 200 log2 units above tile 0 (fp16 fast mode overflows, rows
+    flagged, the exact fixup pass recomputes them); the fixup rewrites only flagged rows, so the
+    other slides' rows -- which may share a fixup block with the flagged items -- keep the fast
+    kernel's bits and still equal their own launches."""
     H, D, E = 16, 48, 768
     Ls = [1025, 2897, 700, 6001, 12000]         # 6001 / 12000: several segments of branches 0-1
     T = sum(Ls)
     g = torch.Generator(device="cuda").manual_seed(5)
     qkv = torch.randn(T, 3 * E, device="cuda", generator=g)
     qkv[:, :E] *= 0.35
-    qkv = qkv.to(torch.bfloat16)
+    if fmt == "fp16_overflow":
+        qkv[:1025, :D] = 0.0
+        qkv[:1025, 0] = 8.0
+        qkv[:1025, E:E + D] = 0.0
+        qkv[150, E] = 25.0
+    qkv = qkv.to(torch.bfloat16 if fmt == "bf16" else torch.float16)
     vs = runtime.VarlenScratch(torch.device("cuda"), Ls, H, D, SEGS, RATIOS, qkv)
     for t in vs.outs + vs.lses:
         t.zero_()
     _hip.dilated_attn_fwd_varlen(vs.plan, True)
     ln_w = torch.rand(E, device="cuda") + 0.5
     ln_b = torch.randn(E, device="cuda") * 0.1
-    merged = torch.empty(T, E, dtype=torch.bfloat16, device="cuda")
+    merged = torch.empty(T, E, dtype=qkv.dtype, device="cuda")
     _hip.branch_merge_ln_varlen(vs.plan, ln_w, ln_b, 1e-5, merged)
     o_off = [0] * len(SEGS)
     l_off = [0] * len(SEGS)
     t0 = 0
     for L in Ls:
         rows = qkv[t0:t0 + L]
-        sc = runtime.AttentionScratch(torch.device("cuda"), 1, L, H, D, SEGS, RATIOS)
+        sc = runtime.AttentionScratch(torch.device("cuda"), 1, L, H, D, SEGS, RATIOS, qkv.dtype)
         for t in sc.outs + sc.lses:
             t.zero_()
         _hip.dilated_attn_fwd(rows, rows[:, E:], rows[:, 2 * E:], 3 * E, 1, L, H, D, SEGS, RATIOS, sc.outs, sc.lses,
                               0.0, True)
-        ref = torch.empty(L, E, dtype=torch.bfloat16, device="cuda")
+        ref = torch.empty(L, E, dtype=qkv.dtype, device="cuda")
         _hip.branch_merge_ln(sc.outs, sc.lses, SEGS, RATIOS, 1, L, H, D, ln_w, ln_b, 1e-5, ref)
         torch.cuda.synchronize()
         for b in range(len(SEGS)):

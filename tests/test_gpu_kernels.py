@@ -236,7 +236,9 @@ def test_attention_fp16_fast_mode_overflow_fixup():
     """fp16 product path (p = 2^(s - m0), m0 = the row max of the first 64-key tile only): head 0's
     key 150 scores 200 log2 units above everything in tile 0, so its p overflows fp16 and the row is
     recomputed by the exact fixup pass; head 1's scores climb 30 log2 units per tile (overflow at the
-    second tile); head 2 stays in range (the fast path itself).  All must match the oracle."""
+    second tile); head 2 stays in range (the fast path itself); head 3's scores climb 5 log2 units per
+    tile for three tiles (+15 over tile 0's max: p reaches ~2^15 in fp16, the fast path's own large-P
+    range, no overflow, no fixup).  All must match the oracle."""
     h = _hip()
     B, L, H, D = 1, 300, 16, 48
     E = H * D
@@ -247,6 +249,10 @@ def test_attention_fp16_fast_mode_overflow_fixup():
     qkv[:, E:E + 2 * D] = 0.0
     qkv[150, E] = 25.0
     qkv[:, E + D] = torch.from_numpy((np.arange(L) // 64) * 3.75).float()
+    qkv[:, 3 * D:4 * D] = 0.0
+    qkv[:, 3 * D] = 8.0
+    qkv[:, E + 3 * D:E + 4 * D] = 0.0
+    qkv[:, E + 3 * D] = torch.from_numpy(np.minimum(np.arange(L) // 64, 3) * 0.625).float()
     qkv = qkv.half()
     segs, ratios = [300], [1]
     outs, lses = _run_attn(h, qkv, B, L, H, D, segs, ratios, prescaled=True)

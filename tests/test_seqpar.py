@@ -230,7 +230,7 @@ def _sp_model(segs, ratios):
     return m.eval(), cfg
 
 
-def _sp_forward_worker(rank, world, port, N, gp, q, local_first=False):
+def _sp_forward_worker(rank, world, port, N, gp, q, local_first=False, monitor=False):
     try:
         import sp_emulator
         sp_emulator.install()
@@ -241,12 +241,15 @@ def _sp_forward_worker(rank, world, port, N, gp, q, local_first=False):
         model, _ = _sp_model(*SP_SCHED)
         model.global_pool = gp
         model.enable_sequence_parallel()
+        mon = seqpar.ExchangeMonitor(bound_s=300, rank=rank) if monitor else None
+        model._sp.set_monitor(mon)
         x, coords = orc.synthetic_slide(N)
         with torch.no_grad():
             out = torch.stack(model._forward_sp(torch.from_numpy(x), torch.from_numpy(coords), True)).numpy()
             last = model._forward_sp(torch.from_numpy(x), torch.from_numpy(coords), False)[0].numpy()
         dist.destroy_process_group()
-        q.put((rank, (out, last)))
+        q.put((rank, (out, last, mon.summary(len(model.encoder.layers)) if mon else None,
+                      [(r["layer"], r["phase"]) for r in mon.records] if mon else None)))
     except Exception:  # pragma: no cover
         import traceback
         q.put((rank, traceback.format_exc()))
@@ -255,13 +258,14 @@ def _sp_forward_worker(rank, world, port, N, gp, q, local_first=False):
 @pytest.mark.parametrize("world,N,gp,local_first", [(2, 600, False, False), (3, 700, True, False),
                                                     (2, 600, False, True)])
 def test_sharded_forward_matches_oracle_with_cpu_kernels(world, N, gp, local_first):
+    monitor = world == 2 and not local_first
     """LongNetViT._forward_sp end to end over gloo with every HIP call replaced by an
     address-checking CPU stand-in (tests/sp_emulator.py): shard bounds, K/V and q-halo
     exchange, query windows, window merge, readouts, all-reduce/broadcast."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_sp_forward_worker, args=(r, world, port, N, gp, q, local_first))
+    procs = [ctx.Process(target=_sp_forward_worker, args=(r, world, port, N, gp, q, local_first, monitor))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -276,10 +280,38 @@ def test_sharded_forward_matches_oracle_with_cpu_kernels(world, N, gp, local_fir
     ref = torch.stack(orc.slide_encoder_forward(W, x, coords, cfg, all_layer_embed=True, global_pool=gp)).numpy()
     ref_last = orc.slide_encoder_forward(W, x, coords, cfg, global_pool=gp)[0].numpy()
     for r in range(world):
-        out, last = res[r]
+        out, last, summ, recs = res[r]
+        if monitor:      # every layer's three exchange phases timed, in both forwards
+            nl = cfg["depth"]
+            assert recs == [(li, ph) for _ in range(2) for li in range(nl) for ph in ("A", "B1", "B2")]
+            assert summ["forwards"] == 2 and summ["kind"] == ["host_exchange"]
+            assert set(summ["ms_per_layer_by_phase"]) == {"A", "B1", "B2"} and summ["ms_per_layer"] > 0
         for got, want in ((out, ref), (last, ref_last)):
             for idx in np.ndindex(*got.shape[:-1]):
                 g_, w_ = got[idx].astype(np.float64), want[idx].astype(np.float64)
                 rel = np.abs(g_ - w_).max() / np.abs(w_).max()
                 cos = (g_ * w_).sum() / np.sqrt((g_ * g_).sum() * (w_ * w_).sum())
                 assert rel <= 2e-2 and cos >= 0.9995, (r, idx, rel, cos)
+
+
+_WATCHDOG_CHILD = """
+import sys, time
+sys.path.insert(0, %r)
+from gigapath import seqpar
+m = seqpar.ExchangeMonitor(bound_s=0.5, rank=5)
+m.arm("layer 7 phase B1 branches [3, 4] peers [4, 6]")
+time.sleep(30)
+print("not reached")
+"""
+
+
+def test_exchange_watchdog_names_the_stuck_collective_and_exits():
+    """A wait that outlives the bound ends the process (exit 3) and says which layer / phase /
+    branches / peers it was stuck on -- instead of hanging until the launcher's timeout."""
+    import subprocess
+    import sys as _sys
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "prov-gigapath-replication_amd")
+    p = subprocess.run([_sys.executable, "-c", _WATCHDOG_CHILD % pkg], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 3, (p.returncode, p.stderr[-2000:])
+    assert "rank 5" in p.stderr and "layer 7 phase B1 branches [3, 4] peers [4, 6]" in p.stderr
+    assert "not reached" not in p.stdout

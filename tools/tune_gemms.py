@@ -18,6 +18,12 @@ import os
 import sys
 import time
 
+# A tuning run under HIPBLASLT_WORKSPACE_SIZE=0 (meant to rule out the stream-K candidates) ended
+# abnormally in round 2 with no fault text in its log: refused, before torch loads.
+if os.environ.get("HIPBLASLT_WORKSPACE_SIZE", "").strip() in ("0", "0K", "0k"):
+    sys.exit("tune_gemms.py: refusing to tune with HIPBLASLT_WORKSPACE_SIZE=0 (TunableOp still times the "
+             "workspace-using candidates; see DESIGN.md §6.3)")
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "prov-gigapath-replication_amd"))
 sys.path.insert(0, ROOT)
