@@ -442,9 +442,8 @@ constexpr uint32_t kLseRedo = 0x7fc0dead;
 //     K/V tiles (global loads, addresses computed once), for k / v layouts the descriptor cannot
 //     cover (the operator seam's separate q / k / v tensors) and for D = 64.
 //   kModeExact (D = 48, q pre-scaled): the LDS-DMA staging and work decomposition of kModeFast with the
-//     exact running-max arithmetic, the -m start as the accumulator's initial value (round 2's fp16
-//     product kernel; kept for lab A/B).  fp16 now runs kModeFast with a tile-0 offset (kM0 below) +
-//     kModeFix without the bf16 hi + lo MFMA start.
+//     exact running-max arithmetic, the -m start as the accumulator's initial value: the fp16 product
+//     kernel (GP_ATTN_FP16_EXACT below; the tile-0-offset fp16 fast mode, kM0, stays as the lab variant).
 enum AttnMode { kModeFast = 0, kModeFix = 1, kModeGen = 2, kModeExact = 3 };
 constexpr int kFixItems = 32;
 
@@ -472,6 +471,19 @@ static_assert(kNWFast == 4 || kNWFast == 8 || kNWFast == 16, "GP_ATTN_NW must be
 #endif
 #ifndef GP_ATTN_ONES_SPARSE
 #define GP_ATTN_ONES_SPARSE 1
+#endif
+// GP_ATTN_FP16_EXACT (product: 1): the fp16 LDS-DMA launch is kModeExact, the exact running-max kernel
+// (lazy rescale), with no fixup pass.  0 (lab) restores round 2's fp16 fast mode (kModeFast with the
+// tile-0 offset + kModeFix): 6 % faster on random-init weights, but a row whose later keys score > 16
+// log2 units above tile 0's max overflows fp16 and its whole fixup block is recomputed serially --
+// measured 2.6x / 4.5x / 4.6x the exact kernel's time when q is 2 / 4 / 8 times sharper than random init
+// (0.05 % / 17 % / 66 % of the rows flagged; tools/fp16_flag_rate.py, profiles/r03_b_fp16_flag_rate.json).
+// GP_ATTN_NOFIX (lab only) skips the fixup pass, so flagged rows keep the kLseRedo marker for the count.
+#ifndef GP_ATTN_NOFIX
+#define GP_ATTN_NOFIX 0
+#endif
+#ifndef GP_ATTN_FP16_EXACT
+#define GP_ATTN_FP16_EXACT 1
 #endif
 
 template <int D, bool kPre, int MODE, bool kTab, int NW, bool kH>
@@ -1347,10 +1359,15 @@ static int attn_fwd_impl(const uint16_t* q, int64_t q_row_stride, int64_t q_tok_
   GP_REQUIRE(items < (int64_t)0x7fffffff, "gp_dilated_attn_fwd: too many work items");
   hipStream_t s = gp_stream(stream);
   if (kh) {
-    if (fast) {        // fp16 fast mode (tile-0 offset), then the exact fixup pass
-      dilated_attn32_kernel<48, true, kModeFast, false, kNWFast, true><<<(unsigned)items, 64 * kNWFast, 0, s>>>(a);
-      dilated_attn32_kernel<48, true, kModeFix, false, kNWFast, true>
-          <<<(unsigned)((items + kFixItems - 1) / kFixItems), 64 * kNWFast, 0, s>>>(a);
+    if (fast) {        // fp16: the exact running-max kernel (GP_ATTN_FP16_EXACT above)
+      if constexpr (GP_ATTN_FP16_EXACT != 0) {
+        dilated_attn32_kernel<48, true, kModeExact, false, kNWFast, true><<<(unsigned)items, 64 * kNWFast, 0, s>>>(a);
+      } else {
+        dilated_attn32_kernel<48, true, kModeFast, false, kNWFast, true><<<(unsigned)items, 64 * kNWFast, 0, s>>>(a);
+        if constexpr (GP_ATTN_NOFIX == 0)
+          dilated_attn32_kernel<48, true, kModeFix, false, kNWFast, true>
+              <<<(unsigned)((items + kFixItems - 1) / kFixItems), 64 * kNWFast, 0, s>>>(a);
+      }
     } else if (D == 96) dilated_attn_kernel<96, true><<<(unsigned)items, 256, 0, s>>>(a);
     else if (D == 48 && q_log2_prescaled) dilated_attn32_kernel<48, true, kModeGen, false, 4, true><<<(unsigned)items, 256, 0, s>>>(a);
     else if (D == 48) dilated_attn32_kernel<48, false, kModeGen, false, 4, true><<<(unsigned)items, 256, 0, s>>>(a);
@@ -1361,8 +1378,9 @@ static int attn_fwd_impl(const uint16_t* q, int64_t q_row_stride, int64_t q_tok_
   } else if (fast) {
     // the product launch: no-max kernel, then the fixup pass (exits at once unless a row was flagged)
     dilated_attn32_kernel<48, true, kModeFast, false, kNWFast><<<(unsigned)items, 64 * kNWFast, 0, s>>>(a);
-    dilated_attn32_kernel<48, true, kModeFix, false, kNWFast>
-        <<<(unsigned)((items + kFixItems - 1) / kFixItems), 64 * kNWFast, 0, s>>>(a);
+    if constexpr (GP_ATTN_NOFIX == 0)
+      dilated_attn32_kernel<48, true, kModeFix, false, kNWFast>
+          <<<(unsigned)((items + kFixItems - 1) / kFixItems), 64 * kNWFast, 0, s>>>(a);
   } else if (D == 48) {
     if (q_log2_prescaled) dilated_attn32_kernel<48, true, kModeGen><<<(unsigned)items, 256, 0, s>>>(a);
     else dilated_attn32_kernel<48, false, kModeGen><<<(unsigned)items, 256, 0, s>>>(a);
@@ -1645,10 +1663,15 @@ extern "C" int gp_dilated_attn_fwd_varlen(const void* plan_host, const void* pla
   a.d_H = make_div_magic((uint32_t)h.H);
   // the single-slide default's variant, so each packed slide's outputs equal its own launch's
   if (fmt == GP_FMT_F16) {
-    dilated_attn32_kernel<48, true, kModeFast, true, kNWFast, true>
-        <<<(unsigned)h.total_items, 64 * kNWFast, 0, gp_stream(stream)>>>(a);
-    dilated_attn32_kernel<48, true, kModeFix, true, kNWFast, true>
-        <<<(unsigned)((h.total_items + kFixItems - 1) / kFixItems), 64 * kNWFast, 0, gp_stream(stream)>>>(a);
+    if constexpr (GP_ATTN_FP16_EXACT != 0) {
+      dilated_attn32_kernel<48, true, kModeExact, true, kNWFast, true>
+          <<<(unsigned)h.total_items, 64 * kNWFast, 0, gp_stream(stream)>>>(a);
+    } else {
+      dilated_attn32_kernel<48, true, kModeFast, true, kNWFast, true>
+          <<<(unsigned)h.total_items, 64 * kNWFast, 0, gp_stream(stream)>>>(a);
+      dilated_attn32_kernel<48, true, kModeFix, true, kNWFast, true>
+          <<<(unsigned)((h.total_items + kFixItems - 1) / kFixItems), 64 * kNWFast, 0, gp_stream(stream)>>>(a);
+    }
     return gp_check_launch("gp_dilated_attn_fwd_varlen");
   }
   dilated_attn32_kernel<48, true, kModeFast, true, kNWFast><<<(unsigned)h.total_items, 64 * kNWFast, 0, gp_stream(stream)>>>(a);
