@@ -445,7 +445,16 @@ constexpr uint32_t kLseRedo = 0x7fc0dead;
 //     exact running-max arithmetic, the -m start as the accumulator's initial value: the fp16 product
 //     kernel (GP_ATTN_FP16_EXACT below; the tile-0-offset fp16 fast mode, kM0, stays as the lab variant).
 enum AttnMode { kModeFast = 0, kModeFix = 1, kModeGen = 2, kModeExact = 3 };
-constexpr int kFixItems = 32;
+// work items per fixup-pass block: the block reads the lse rows of kFixItems consecutive (LPT-ordered)
+// items and recomputes the flagged ones in turn.  4 (round 3): no-flag cost 1.2506 ms per 70k launch
+// (fast + fixup) vs 1.2548 with 32 and 1.2652 with 1 (profiles/r03_g_ab_fixup_items.json); with sharp
+// attention the flagged items run nearly in parallel: 0.3 % flagged rows 2.69 ms, 96 % 3.19 ms, vs 7.2 /
+// 8.1 ms with round 2's 32 items per block, whose blocks ran up to 32 long items serially
+// (profiles/r03_g_flag_rate_bf16_fixup_items.json).  1 = one block per item.
+#ifndef GP_ATTN_FIX_ITEMS
+#define GP_ATTN_FIX_ITEMS 4
+#endif
+constexpr int kFixItems = GP_ATTN_FIX_ITEMS;
 
 // Waves per workgroup of the LDS-DMA kernels (each wave 32 queries; the K/V tile is shared by all):
 // a compile-time tunable (tools/attn_lab); the register-staged kernel always runs 4 waves.
@@ -1003,27 +1012,31 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   }
 }
 
-// One work item per block (XCD-grouped order), or, for the fixup pass (kModeFix), kFixItems
-// consecutive items per block: the block reads the lse of every needed row of all of them at once
-// (wave w: items 8w .. 8w + 7; 16 independent loads per lane) and exits unless some row holds the
-// kLseRedo marker, so the pass costs about one load latency per 32 items when nothing overflowed.
+// One work item per block (XCD-grouped order).  The fixup pass (kModeFix) with kFixItems = 1: one item
+// per block in item order, each block reading its item's lse rows and exiting unless one holds the
+// kLseRedo marker; with kFixItems > 1 (lab) a block reads the lse of every needed row of kFixItems
+// consecutive items at once (16 independent loads per lane) and recomputes the flagged ones in turn.
 template <int D, bool kPre, int MODE, bool kTab = false, int NW = 4, bool kH = false>
 __global__ __launch_bounds__(NW * 64, 2) void dilated_attn32_kernel(const AttnArgs a) {
-  if constexpr (MODE == kModeFix) {
+  if constexpr (MODE == kModeFix && kFixItems == 1) {
+    attn32_item<D, kPre, MODE, kTab, NW, kH>(a, (int)blockIdx.x);   // its own flagged-row check first
+  } else if constexpr (MODE == kModeFix) {
     constexpr int QB = NW * 32;
     const int it0 = (int)blockIdx.x * kFixItems;
     // wave index made provably uniform: the item decode then runs on the scalar unit (s_load from
     // the kernel arguments), not as a chain of dependent per-lane global loads
     const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), lane = (int)threadIdx.x & 63;
-    // every load is issued before any is compared (clamped in-bounds indices, masked after), so the
-    // 16 loads of a lane are in flight together
-    constexpr int NV = (kFixItems / NW) * (QB / 64);
+    // slot s = 64 rows of one item (item s / (QB / 64)); wave w reads slots w, w + NW, ...; every load is
+    // issued before any is compared (clamped in-bounds indices, masked after), so they are in flight together
+    constexpr int SLOTS = kFixItems * (QB / 64);
+    constexpr int NV = (SLOTS + NW - 1) / NW;
     uint32_t vals[NV];
     bool use[NV];
 #pragma unroll
-    for (int k = 0; k < kFixItems / NW; ++k) {
-      const int it = it0 + (kFixItems / NW) * w + k;
-      const bool live = it < a.total_items;
+    for (int n = 0; n < NV; ++n) {
+      const int sl = w + NW * n;
+      const int it = it0 + sl / (QB / 64), hf = sl % (QB / 64);
+      const bool live = sl < SLOTS && it < a.total_items;
       WorkItem wi;
       AttnBranch te;
       const int itc = live ? it : (int)a.total_items - 1;
@@ -1032,13 +1045,9 @@ __global__ __launch_bounds__(NW * 64, 2) void dilated_attn32_kernel(const AttnAr
       const AttnBranch& brr = kTab ? te : a.br[wi.bi];
       const int q0 = wi.i_lo + wi.qb * QB;
       const float* lrow = brr.lse + ((int64_t)wi.bn * a.H + wi.hh) * brr.g.m;
-#pragma unroll
-      for (int hf = 0; hf < QB / 64; ++hf) {
-        const int i = q0 + 64 * hf + lane;
-        const int n = k * (QB / 64) + hf;
-        use[n] = live && i < wi.i_hi;
-        vals[n] = __float_as_uint(lrow[use[n] ? i : 0]);
-      }
+      const int i = q0 + 64 * hf + lane;
+      use[n] = live && i < wi.i_hi;
+      vals[n] = __float_as_uint(lrow[use[n] ? i : 0]);
     }
     bool flagged = false;
 #pragma unroll

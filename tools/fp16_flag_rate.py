@@ -2,14 +2,16 @@
 fixup then costs (ADVICE r02 on gp_attn.hip's fixup pass).
 
     make -C tools/attn_lab tune NAME=f16fast DEFS="-DGP_ATTN_FP16_EXACT=0"
+    make -C tools/attn_lab tune NAME=fix32 DEFS="-DGP_ATTN_FIX_ITEMS=32"
     make -C tools/attn_lab tune NAME=nofix DEFS="-DGP_ATTN_FP16_EXACT=0 -DGP_ATTN_NOFIX=1"
     python tools/fp16_flag_rate.py [--fmt fp16|bf16] [--L 70001] [--out file.json]
 
 Builds of the same source, one process, interleaved rounds:
   prod      the product: fp16 = kModeExact (exact running max, no fixup; round 3); bf16 = kModeFast
-            (p = 2^s, no max, no offset) + kModeFix over the 32-item blocks holding a flagged row;
-  f16fast   (fp16 only) round 2's fp16 product: kModeFast with p = 2^(s - m0), m0 = tile 0's row max,
-            + kModeFix;
+            (p = 2^s, no max, no offset) + kModeFix with one block per work item (round 3);
+  f16fast   (fp16 only) the fp16 fast mode: kModeFast with p = 2^(s - m0), m0 = tile 0's row max,
+            + kModeFix (one block per item);
+  fix32     (bf16 only) round 2's fixup pass: 32 items per block, flagged ones recomputed in turn;
   nofix     kModeFast alone: flagged rows keep the lse marker 0x7fc0dead, which this tool counts.
 Inputs (one 70k layer's q / k / v, q pre-scaled by D^-1/2 log2 e as the product's QKV weight):
   random-init   q, k, v ~ N(0, 1), q x 0.35 (the scale the model's random-init q projection gives);
@@ -39,13 +41,18 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--libs", default=None, help="comma-separated lab builds (tools/attn_lab/liblab_<name>.so) "
+                    "to time beside prod; default f16fast,nofix (fp16) / fix32,nofix (bf16); nofix is required")
+    ap.add_argument("--scales", default=None, help="comma-separated q sharpness factors")
     ap.add_argument("--fmt", choices=["fp16", "bf16"], default="fp16",
                     help="bf16: the product's no-max bf16 kernel (flags rows whose sum leaves [2^-100, 2^100])")
     args = ap.parse_args()
     act = torch.float16 if args.fmt == "fp16" else torch.bfloat16
     prod = _hip.load_library()
     libs = [("prod", prod)]
-    for name in (("f16fast", "nofix") if args.fmt == "fp16" else ("nofix",)):
+    names = args.libs.split(",") if args.libs else (["f16fast", "nofix"] if args.fmt == "fp16" else ["fix32", "nofix"])
+    assert "nofix" in names
+    for name in names:
         libs.append((name, _hip.load_library(os.path.join(ROOT, "tools", "attn_lab", "liblab_%s.so" % name))))
     H, D, L = 16, 48, args.L
     E = H * D
@@ -54,6 +61,8 @@ def main():
     base = torch.randn(L, 3 * E, device="cuda", generator=g)
     cases = []
     scales = ((1.0, 2.0, 4.0, 8.0) if args.fmt == "fp16" else (1.0, 4.0, 8.0, 12.0, 16.0))
+    if args.scales:
+        scales = tuple(float(x) for x in args.scales.split(","))
     for s in scales:
         x = base.clone()
         x[:, :E] *= 0.35 * s
