@@ -79,26 +79,27 @@ def test_mixed_batch_graph_replays_bit_exact():
     assert len(model._graphs) == 5
 
 
-@pytest.mark.parametrize("fmt", ["bf16", "fp16_overflow"])
+@pytest.mark.parametrize("fmt", ["bf16", "bf16_overflow", "fp16_overflow"])
 def test_varlen_attention_and_merge_bit_exact_per_slide(fmt):
     """One varlen launch over packed slides == the single-slide kernels on each slide's rows,
-    bit for bit (same per-item math; each slide keeps its own segment schedule).  fp16_overflow: the
-    first slide's head-0 scores spike 200 log2 units above tile 0 (fp16 fast mode overflows, rows
-    flagged, the exact fixup pass recomputes them); the fixup rewrites only flagged rows, so the
-    other slides' rows -- which may share a fixup block with the flagged items -- keep the fast
-    kernel's bits and still equal their own launches."""
+    bit for bit (same per-item math; each slide keeps its own segment schedule).  *_overflow: the
+    first slide's head-0 scores spike 200 log2 units above the rest.  bf16: the no-max fast kernel's
+    row sum overflows, the rows are flagged and the fixup pass recomputes them exactly; it rewrites only
+    flagged rows, so the other slides' rows -- whose items may share a fixup block with the flagged
+    ones -- keep the fast kernel's bits and still equal their own launches.  fp16: the exact running-
+    max kernel (no fixup) on the same input."""
     H, D, E = 16, 48, 768
     Ls = [1025, 2897, 700, 6001, 12000]         # 6001 / 12000: several segments of branches 0-1
     T = sum(Ls)
     g = torch.Generator(device="cuda").manual_seed(5)
     qkv = torch.randn(T, 3 * E, device="cuda", generator=g)
     qkv[:, :E] *= 0.35
-    if fmt == "fp16_overflow":
+    if fmt.endswith("_overflow"):
         qkv[:1025, :D] = 0.0
         qkv[:1025, 0] = 8.0
         qkv[:1025, E:E + D] = 0.0
         qkv[150, E] = 25.0
-    qkv = qkv.to(torch.bfloat16 if fmt == "bf16" else torch.float16)
+    qkv = qkv.to(torch.float16 if fmt.startswith("fp16") else torch.bfloat16)
     vs = runtime.VarlenScratch(torch.device("cuda"), Ls, H, D, SEGS, RATIOS, qkv)
     for t in vs.outs + vs.lses:
         t.zero_()

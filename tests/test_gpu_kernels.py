@@ -232,13 +232,12 @@ def test_attention_no_max_overflow_fixup():
     assert (o[0, 0, 0] - v[0, 150, 0]).abs().max().item() <= 1e-2 * max(1.0, v[0, 150, 0].abs().max().item())
 
 
-def test_attention_fp16_fast_mode_overflow_fixup():
-    """fp16 product path (p = 2^(s - m0), m0 = the row max of the first 64-key tile only): head 0's
-    key 150 scores 200 log2 units above everything in tile 0, so its p overflows fp16 and the row is
-    recomputed by the exact fixup pass; head 1's scores climb 30 log2 units per tile (overflow at the
-    second tile); head 2 stays in range (the fast path itself); head 3's scores climb 5 log2 units per
-    tile for three tiles (+15 over tile 0's max: p reaches ~2^15 in fp16, the fast path's own large-P
-    range, no overflow, no fixup).  All must match the oracle."""
+def test_attention_fp16_large_scores():
+    """fp16 product path (the exact running-max kernel, kModeExact: round 3 moved fp16 off the
+    tile-0-offset fast mode, whose fixup pass made sharp attention 2-5x slower): head 0's key 150 scores
+    200 log2 units above everything in tile 0; head 1's scores climb 30 log2 units per tile; head 2 stays
+    in range; head 3's scores climb 5 log2 units per tile for three tiles (+15 over tile 0).  All must
+    match the oracle."""
     h = _hip()
     B, L, H, D = 1, 300, 16, 48
     E = H * D
@@ -352,7 +351,7 @@ def test_attention_other_head_dims(D):
 @pytest.mark.parametrize("name,B,L,segs,ratios", ATTN_CASES)
 def test_dilated_attention_fp16_vs_oracle(name, B, L, segs, ratios, prescaled):
     """fp16 q/k/v (the forward under the reference pipeline's fp16 autocast): pre-scaled q runs the
-    LDS-DMA fp16 fast kernel + fixup pass (the product layout), otherwise the register-staged one.  P is
+    LDS-DMA fp16 exact running-max kernel (the product layout), otherwise the register-staged one.  P is
     rounded to fp16 (11 significant bits): o within 2e-3, lse within 1.5e-3 of the fp32 oracle."""
     h = _hip()
     H, D = 16, 48

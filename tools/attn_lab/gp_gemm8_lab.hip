@@ -68,6 +68,10 @@ GP_DEV void wait_vmcnt() {
 }
 
 __shared__ __attribute__((aligned(16))) float g_bias[3072];        // the bias row (N <= 3072), fp32
+#ifndef GP_GEMM8_SCHED
+#define GP_GEMM8_SCHED 1       // 1: both W halves of K-tile v+2 staged in Q3 of v (weights 4 phases ahead);
+                               // 2: and both A halves of v+1 in Q0 of v (3 phases ahead)
+#endif
 #ifndef GP_GEMM8_SPLIT
 #define GP_GEMM8_SPLIT 1       // split the last partial round of tiles in K (a second, small reduce kernel)
 #endif
@@ -259,16 +263,17 @@ __global__ __launch_bounds__(kThreads, 1) void gemm8_kernel(const GemmArgs g) {
       read_a(bc, I0());
       read_w(bc, I0());
       stage(I0(), I0(), BN_(), v + 1);
+      if constexpr (GP_GEMM8_SCHED == 2) stage(I0(), I1(), BN_(), v + 1);   // both A halves in Q0
       sync();
       quadrant(I0(), I0());
       sync();
       read_w(bc, I1());
-      stage(I0(), I1(), BN_(), v + 1);
+      if constexpr (GP_GEMM8_SCHED != 2) stage(I0(), I1(), BN_(), v + 1);
       sync();
       quadrant(I0(), I1());
       sync();
       read_a(bc, I1());
-      stage(I1(), I1(), BN_(), v + 1);
+      if constexpr (GP_GEMM8_SCHED == 0) stage(I1(), I1(), BN_(), v + 1);
       sync();
       quadrant(I1(), I1());
       sync();
@@ -278,7 +283,12 @@ __global__ __launch_bounds__(kThreads, 1) void gemm8_kernel(const GemmArgs g) {
       }
       if (v + 2 < nk || has_next) {
         stage(I1(), I0(), bc, v + 2);
-        wait_vmcnt<2>();
+        if constexpr (GP_GEMM8_SCHED >= 1) {   // both W halves of v+2 here (4 phases of lead)
+          stage(I1(), I1(), bc, v + 2);
+          wait_vmcnt<4>();
+        } else {
+          wait_vmcnt<2>();
+        }
       } else {
         wait_vmcnt<0>();
       }
@@ -292,7 +302,12 @@ __global__ __launch_bounds__(kThreads, 1) void gemm8_kernel(const GemmArgs g) {
     issue(I1(), I0(), I0(), rw, kt0);
     issue(I1(), I1(), I0(), rw, kt0);
     issue(I1(), I0(), I1(), rw, kt0 + 1);
-    wait_vmcnt<2>();
+    if constexpr (GP_GEMM8_SCHED >= 1) {
+      issue(I1(), I1(), I1(), rw, kt0 + 1);
+      wait_vmcnt<4>();
+    } else {
+      wait_vmcnt<2>();
+    }
     sync();                         // (also publishes g_bias)
     for (int i = 0; i < count; ++i) {
       has_next = i + 1 < count;
@@ -394,7 +409,7 @@ extern "C" int gp_gemm_bf16_tn(const uint16_t* A, int64_t lda, const uint16_t* W
     const size_t need = (size_t)rem * S * kBM * kBN * sizeof(float);
     static size_t lab_ws_bytes = 0;
     if (lab_ws_bytes < need) {
-      if (lab_ws) hipFree(lab_ws);
+      if (lab_ws) (void)hipFree(lab_ws);
       GP_REQUIRE(hipMalloc(&lab_ws, need) == hipSuccess, "gp_gemm_bf16_tn: workspace");
       lab_ws_bytes = need;
     }
