@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GP_ABI_VERSION 5
+#define GP_ABI_VERSION 6
 #define GP_EARG (-1)
 #define GP_MAX_BRANCHES 8
 #define GP_MAX_DESTS 8
@@ -229,6 +229,40 @@ int gp_residual_layernorm(float* x, const uint16_t* y, const float* bias, const 
  * before the LN (gelu(x.float()).type_as(x), feedforward_network.py:135). */
 int gp_gelu_layernorm(const uint16_t* h, const float* ln_w, const float* ln_b, float eps,
                       uint16_t* out, int64_t rows, int cols, int fmt, void* stream);
+
+/* ---- Projection GEMMs on MFMAs (nn.Linear of torchscale/component/multihead_attention.py:43-48,
+ * feedforward_network.py:131-142, gigapath/slide_encoder.py:47-51).  A [M, K] and W [N, K] are
+ * K-contiguous act (row strides lda / ldw), C [M, N] act (ldc); fp32 accumulation.  N % 256 == 0,
+ * N <= 3072, K in {768, 1536, 3072}; strides multiples of 8, operands 16-byte aligned.
+ * ws: device workspace of gp_gemm_workspace_bytes(M, N, K) bytes (fp32 partials of the last, split
+ * round of tiles; the value depends on the current device's CU count); NULL disables the split. */
+int64_t gp_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K);
+
+/* C = A . W^T (+ bias).  bias: [N] fp32 or NULL. */
+int gp_linear(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, const float* bias,
+              uint16_t* C, int64_t ldc, int64_t M, int64_t N, int64_t K, void* ws, int64_t ws_bytes,
+              int fmt, void* stream);
+
+/* FFN first half (feedforward_network.py:131-135): fc1 with the GELU in its epilogue,
+ *   h = act(gelu(act(A . W1^T + b1)))     (gelu(x.float()).type_as(x), exact erf)
+ * and the LayerNorm statistics of h per 256-column group g:
+ *   stats[g][m] = (mean, sum of squared deviations) of h[m, 256 g : 256 g + 256]   (fp32 pairs)
+ * A: [M, K] act; W1: [F, K] act; b1: [F] fp32 or NULL; h: [M, F] act (ldh); stats: [F/256 + 1, M, 2]
+ * fp32 (the last plane is gp_ffn_fc2_ln's).  F % 256 == 0, F <= 3072. */
+int gp_ffn_fc1_gelu(const uint16_t* A, int64_t lda, const uint16_t* W1, int64_t ldw, const float* b1,
+                    uint16_t* h, int64_t ldh, float* stats, int64_t M, int64_t F, int64_t K, int fmt,
+                    void* stream);
+
+/* FFN second half (feedforward_network.py:136-142): fc2(ffn_layernorm(h)) with the LayerNorm folded
+ * into the GEMM epilogue:
+ *   y = act( rstd_m * (h . W2g^T - mean_m * c) + d )
+ * mean_m / rstd_m = LayerNorm statistics of row m merged from gp_ffn_fc1_gelu's stats (biased
+ * variance, + eps; written into the stats' last plane first); W2g [N, F] act = W2 * gamma (each column
+ * k scaled by the LN weight); c [N] fp32 = row sums of W2g (as rounded); d [N] fp32 = W2 . beta + b2.
+ * N <= 1536. */
+int gp_ffn_fc2_ln(const uint16_t* h, int64_t ldh, const uint16_t* W2g, int64_t ldw, float* stats,
+                  const float* c, const float* d, float eps, uint16_t* y, int64_t ldy, int64_t M, int64_t N,
+                  int64_t F, void* ws, int64_t ws_bytes, int fmt, void* stream);
 
 /* Plain fp32 LayerNorm over rows with a row stride (readout: encoder.py:387-388,
  * slide_encoder.py:213-221).  out: [rows, cols] fp32 contiguous.  cols = 64 * {12, 16, 24}. */

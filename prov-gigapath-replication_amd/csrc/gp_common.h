@@ -34,8 +34,16 @@ GP_DEV uint16_t f2e(float f) {
   if constexpr (kH) return __builtin_bit_cast(uint16_t, (_Float16)f);
   else return f2bf(f);
 }
+// two values rounded (to nearest even) and packed by one v_cvt_pk_bf16_f32 / v_cvt_pk_f16_f32
+typedef __bf16 gp_bf16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 gp_f16x2 __attribute__((ext_vector_type(2)));
+typedef float gp_f32x2 __attribute__((ext_vector_type(2)));
 template <bool kH>
-GP_DEV uint32_t pack2e(float lo, float hi) { return (uint32_t)f2e<kH>(lo) | ((uint32_t)f2e<kH>(hi) << 16); }
+GP_DEV uint32_t pack2e(float lo, float hi) {
+  const gp_f32x2 v = {lo, hi};
+  if constexpr (kH) return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, gp_f16x2));
+  else return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, gp_bf16x2));
+}
 
 template <bool kH, int N>
 GP_DEV void load_e(const uint16_t* p, float* out) {

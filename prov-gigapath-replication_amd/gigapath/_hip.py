@@ -15,7 +15,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_lib", "libgigapath_hip.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 MAX_BRANCHES = 8
 MAX_DESTS = 8
 
@@ -62,8 +62,13 @@ SIGNATURES = {
     "gp_varlen_plan": [c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp],
     "gp_dilated_attn_fwd_varlen": [c_vp, c_vp, c_i32, c_i32, c_vp],
     "gp_branch_merge_ln_varlen": [c_vp, c_vp, c_vp, c_vp, c_f32, c_vp, c_i32, c_vp],
+    "gp_gemm_workspace_bytes": [c_i64, c_i64, c_i64],
+    "gp_linear": [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i32, c_vp],
+    "gp_ffn_fc1_gelu": [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_i32, c_vp],
+    "gp_ffn_fc2_ln": [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_f32, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64,
+                      c_i32, c_vp],
 }
-_RESTYPES = {"gp_last_error_string": ctypes.c_char_p, "gp_varlen_plan_bytes": c_i64}
+_RESTYPES = {"gp_last_error_string": ctypes.c_char_p, "gp_varlen_plan_bytes": c_i64, "gp_gemm_workspace_bytes": c_i64}
 
 _lib = None
 
@@ -381,3 +386,77 @@ def branch_merge_ln_varlen(plan: VarlenPlan, ln_w, ln_b, eps, out):
         raise TypeError("branch_merge_ln_varlen: out must be in the plan's 16-bit format")
     _check(lib.gp_branch_merge_ln_varlen(plan.host, _ptr(plan.dev), _ptr(ln_w), _ptr(ln_b), eps, _ptr(out),
                                          plan.fmt, _stream()), "gp_branch_merge_ln_varlen")
+
+
+# ------------------------------------------------------------------------------------------
+# projection GEMMs (include/gigapath_hip.h "Projection GEMMs on MFMAs")
+# ------------------------------------------------------------------------------------------
+GEMM_K = (768, 1536, 3072)
+
+
+def gemm_supported(N: int, K: int) -> bool:
+    """Shapes the MFMA GEMM kernels are instantiated for (N a multiple of 256 up to 3072)."""
+    return N % 256 == 0 and 0 < N <= 3072 and K in GEMM_K
+
+
+def gemm_workspace_bytes(M: int, N: int, K: int) -> int:
+    return int(load_library().gp_gemm_workspace_bytes(M, N, K))
+
+
+def _rows(t, name):
+    if not t.is_cuda or t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError("gigapath HIP path: %s must be a row-major 2-D device tensor" % name)
+    return t
+
+
+def _ws(ws):
+    return (None, 0) if ws is None else (ws.data_ptr(), ws.numel() * ws.element_size())
+
+
+def linear(a, w, bias, out, ws=None):
+    """out = a . w^T (+ bias): a [M, K], w [N, K], out [M, N] act; bias [N] fp32 or None."""
+    lib = load_library()
+    fmt = fmt_of(a.dtype)
+    _rows(a, "a"); _rows(w, "w"); _rows(out, "out")
+    if w.dtype != a.dtype or out.dtype != a.dtype:
+        raise TypeError("linear: a, w and out must share one 16-bit dtype")
+    if bias is not None:
+        _dev(bias, torch.float32, "bias")
+    wp, wb = _ws(ws)
+    _check(lib.gp_linear(_ptr(a), a.stride(0), _ptr(w), w.stride(0), _ptr(bias), _ptr(out), out.stride(0), a.shape[0],
+                         w.shape[0], a.shape[1], wp, wb, fmt, _stream()), "gp_linear")
+
+
+def ffn_fc1_gelu(a, w1, b1, h, stats):
+    """h = act(gelu(a . w1^T + b1)), stats [F/256 + 1, M, 2] fp32 (per 256-column (mean, M2) of h; the
+    last plane is gp_ffn_fc2_ln's row (mean, rstd))."""
+    lib = load_library()
+    fmt = fmt_of(a.dtype)
+    _rows(a, "a"); _rows(w1, "w1"); _rows(h, "h")
+    if w1.dtype != a.dtype or h.dtype != a.dtype:
+        raise TypeError("ffn_fc1_gelu: a, w1 and h must share one 16-bit dtype")
+    _dev(stats, torch.float32, "stats")
+    M, F = a.shape[0], w1.shape[0]
+    if stats.numel() < (F // 256 + 1) * M * 2:
+        raise ValueError("ffn_fc1_gelu: stats must hold [F/256 + 1, M, 2] floats")
+    if b1 is not None:
+        _dev(b1, torch.float32, "b1")
+    _check(lib.gp_ffn_fc1_gelu(_ptr(a), a.stride(0), _ptr(w1), w1.stride(0), _ptr(b1), _ptr(h), h.stride(0),
+                               _ptr(stats), M, F, a.shape[1], fmt, _stream()), "gp_ffn_fc1_gelu")
+
+
+def ffn_fc2_ln(h, w2g, stats, c, d, eps, y, ws=None):
+    """y = act(LN(h) . w2^T + b2) through the fold: w2g = w2 * gamma, c = rowsum(w2g), d = w2 . beta + b2."""
+    lib = load_library()
+    fmt = fmt_of(h.dtype)
+    _rows(h, "h"); _rows(w2g, "w2g"); _rows(y, "y")
+    if w2g.dtype != h.dtype or y.dtype != h.dtype:
+        raise TypeError("ffn_fc2_ln: h, w2g and y must share one 16-bit dtype")
+    for nm, t in (("stats", stats), ("c", c), ("d", d)):
+        _dev(t, torch.float32, nm)
+    M, F, N = h.shape[0], h.shape[1], w2g.shape[0]
+    if stats.numel() < (F // 256 + 1) * M * 2:
+        raise ValueError("ffn_fc2_ln: stats must hold [F/256 + 1, M, 2] floats")
+    wp, wb = _ws(ws)
+    _check(lib.gp_ffn_fc2_ln(_ptr(h), h.stride(0), _ptr(w2g), w2g.stride(0), _ptr(stats), _ptr(c), _ptr(d), float(eps),
+                             _ptr(y), y.stride(0), M, N, F, wp, wb, fmt, _stream()), "gp_ffn_fc2_ln")

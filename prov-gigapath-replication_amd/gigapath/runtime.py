@@ -1,16 +1,18 @@
 """MI355X execution engine of the LongNet slide-encoder forward.
 
-Per layer the engine issues 9 launches on torch's current HIP stream (M = B*L tokens):
+Per layer the engine issues 8 launches on torch's current HIP stream (M = B*L tokens):
 
     qkv  = a . Wqkv^T + bqkv             hipBLASLt (bias epilogue)         [M, 3E] bf16
     attn = gp_dilated_attn_fwd(qkv)        ONE launch, all dilation branches  sparse o / lse
     a    = LN_inner(merge(attn))           gp_branch_merge_ln                 [M, E] bf16
     y    = a . Wo^T                        hipBLASLt                          [M, E] bf16
     x   += y + bo ; a = LN2(x)             gp_residual_layernorm (fp32 residual stream)
-    f    = a . W1^T + b1                   hipBLASLt (bias epilogue)          [M, F] bf16
-    f    = LN_ffn(gelu(f))                 gp_gelu_layernorm
-    y    = f . W2^T                        hipBLASLt
-    x   += y + b2 ; a = LN1(next layer)    gp_residual_layernorm
+    f    = gelu(a . W1^T + b1), stats      gp_ffn_fc1_gelu (MFMA GEMM, GELU + LN statistics epilogue)
+    y    = LN_ffn(f) . W2^T + b2           gp_ffn_fc2_ln   (MFMA GEMM, LayerNorm folded into the epilogue)
+    x   += y ; a = LN1(next layer)         gp_residual_layernorm
+
+(shapes outside the FFN kernels' instantiations, or GIGAPATH_FFN_FUSED=0: hipBLASLt fc1,
+gp_gelu_layernorm, hipBLASLt fc2 -- 9 launches)
 
 which is EncoderLayer.forward (torchscale/architecture/encoder.py:116-162) with
 DilatedAttention.forward (component/dilated_attention.py:133-217) and the FFN
@@ -237,11 +239,20 @@ class PackedLayer:
     fln_eps: float
     w2: torch.Tensor         # [E, F] act
     b2: torch.Tensor         # [E] fp32
+    # the fused FFN (gp_ffn_fc1_gelu / gp_ffn_fc2_ln), None when its kernels do not cover the shape:
+    b1_f32: Optional[torch.Tensor] = None   # [F] fp32
+    w2g: Optional[torch.Tensor] = None      # [E, F] act: W2 * gamma_ffn (LN weight folded into fc2)
+    c2: Optional[torch.Tensor] = None       # [E] fp32: row sums of w2g as rounded
+    d2: Optional[torch.Tensor] = None       # [E] fp32: W2 . beta_ffn + b2
+
+    @property
+    def ffn_fused(self) -> bool:
+        return self.w2g is not None
 
     @staticmethod
     def from_module(layer, dev, act: torch.dtype = torch.bfloat16) -> "PackedLayer":
         ffn = layer.ffn
-        return PackedLayer(
+        pl = PackedLayer(
             attn=PackedAttention.from_module(layer.self_attn, dev, act),
             ln1_w=_f32(layer.self_attn_layer_norm.weight, dev), ln1_b=_f32(layer.self_attn_layer_norm.bias, dev),
             ln1_eps=float(layer.self_attn_layer_norm.eps),
@@ -251,6 +262,54 @@ class PackedLayer:
             fln_w=_f32(ffn.ffn_layernorm.weight, dev), fln_b=_f32(ffn.ffn_layernorm.bias, dev),
             fln_eps=float(ffn.ffn_layernorm.eps),
             w2=_act(ffn.fc2.weight, dev, act), b2=_f32(ffn.fc2.bias, dev))
+        F, E = pl.w1.shape
+        if ffn_fusable(E, F):
+            # LN(h) . W2^T + b2 = rstd (h . (W2 gamma)^T - mean c) + d  (csrc/gp_gemm.hip, "LN fold")
+            w2 = ffn.fc2.weight.detach().to(device=dev, dtype=torch.float64)
+            g = ffn.ffn_layernorm.weight.detach().to(device=dev, dtype=torch.float64)
+            be = ffn.ffn_layernorm.bias.detach().to(device=dev, dtype=torch.float64)
+            pl.w2g = (w2 * g[None, :]).to(act).contiguous()
+            pl.c2 = pl.w2g.double().sum(1).float().contiguous()
+            pl.d2 = (w2 @ be + ffn.fc2.bias.detach().to(device=dev, dtype=torch.float64)).float().contiguous()
+            pl.b1_f32 = _f32(ffn.fc1.bias, dev)
+        return pl
+
+
+FFN_FUSED = os.environ.get("GIGAPATH_FFN_FUSED", "1") != "0"
+
+
+def ffn_fusable(E: int, F: int) -> bool:
+    """The fused FFN kernels cover fc1 [F, E] and fc2 [E, F] (gp_gemm.hip instantiations)."""
+    return FFN_FUSED and _hip.gemm_supported(F, E) and _hip.gemm_supported(E, F) and 2 * E <= 3072
+
+
+def ffn_forward(pl: "PackedLayer", a: torch.Tensor, f: torch.Tensor, y: torch.Tensor, fstats, gemm_ws,
+                M: int, F: int) -> Optional[torch.Tensor]:
+    """FeedForwardNetwork.forward (feedforward_network.py:131-142) without its residual: y = FFN(a).
+    Returns the bias the residual add still owes (b2 on the unfused path, None when fused)."""
+    if pl.ffn_fused and fstats is not None:
+        with TIMER.span("gemm_fc1"):
+            _hip.ffn_fc1_gelu(a, pl.w1, pl.b1_f32, f, fstats)
+        with TIMER.span("gemm_fc2"):
+            _hip.ffn_fc2_ln(f, pl.w2g, fstats, pl.c2, pl.d2, pl.fln_eps, y, gemm_ws)
+        return None
+    with TIMER.span("gemm_fc1"):
+        torch.addmm(pl.b1, a, pl.w1.t(), out=f)
+    with TIMER.span("gelu_ln"):
+        _hip.gelu_layernorm(f, pl.fln_w, pl.fln_b, pl.fln_eps, f, M, F)
+    with TIMER.span("gemm_fc2"):
+        torch.mm(f, pl.w2.t(), out=y)
+    return pl.b2
+
+
+def ffn_buffers(dev, M: int, E: int, F: int):
+    """(stats, GEMM workspace) of the fused FFN for M rows, or (None, None) when it does not apply."""
+    if not ffn_fusable(E, F):
+        return None, None
+    stats = torch.empty((F // 256 + 1) * M * 2, dtype=torch.float32, device=dev)
+    nb = _hip.gemm_workspace_bytes(M, E, F) if torch.device(dev).type == "cuda" else 0
+    gws = torch.empty(max(nb, 16), dtype=torch.uint8, device=dev)
+    return stats, gws
 
 
 def param_signature(module: torch.nn.Module) -> tuple:
@@ -316,6 +375,7 @@ class Workspace:
         self.qkv = torch.empty(M, 3 * E, dtype=act, device=dev)
         self.y = torch.empty(M, E, dtype=act, device=dev)
         self.f = torch.empty(M, F, dtype=act, device=dev)
+        self.fstats, self.gemm_ws = ffn_buffers(dev, M, E, F)
         self.attn = AttentionScratch(dev, B, L, H, E // H, segs, ratios, act)
 
 
@@ -334,6 +394,7 @@ class PackedWorkspace(Workspace):
         self.qkv = torch.empty(M, 3 * E, dtype=act, device=dev)
         self.y = torch.empty(M, E, dtype=act, device=dev)
         self.f = torch.empty(M, F, dtype=act, device=dev)
+        self.fstats, self.gemm_ws = ffn_buffers(dev, M, E, F)
         self.attn = VarlenScratch(dev, self.Ls, H, E // H, segs, ratios, self.qkv)
         self.tok_off = self.attn.plan.tok_off
         self.cls_idx = torch.tensor(self.tok_off[:-1], dtype=torch.int64, device=dev)
@@ -409,15 +470,10 @@ class EncoderEngine:
                 torch.mm(ws.a, pa.w_o.t(), out=ws.y)
             with TIMER.span("resid_ln"):
                 _hip.residual_layernorm(ws.x, ws.y, pa.b_o, pl.ln2_w, pl.ln2_b, pl.ln2_eps, ws.a, M, E)
-            with TIMER.span("gemm_fc1"):
-                torch.addmm(pl.b1, ws.a, pl.w1.t(), out=ws.f)
-            with TIMER.span("gelu_ln"):
-                _hip.gelu_layernorm(ws.f, pl.fln_w, pl.fln_b, pl.fln_eps, ws.f, M, F)
-            with TIMER.span("gemm_fc2"):
-                torch.mm(ws.f, pl.w2.t(), out=ws.y)
+            b2 = ffn_forward(pl, ws.a, ws.f, ws.y, ws.fstats, ws.gemm_ws, M, F)
             nxt = self.layers[li + 1] if li + 1 < nl else None
             with TIMER.span("resid_ln"):
-                _hip.residual_layernorm(ws.x, ws.y, pl.b2, nxt.ln1_w if nxt else None, nxt.ln1_b if nxt else None,
+                _hip.residual_layernorm(ws.x, ws.y, b2, nxt.ln1_w if nxt else None, nxt.ln1_b if nxt else None,
                                         nxt.ln1_eps if nxt else 1e-5, ws.a, M, E)
             if layer_hook is not None:
                 layer_hook(li + 1)

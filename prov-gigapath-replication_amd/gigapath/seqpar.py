@@ -417,6 +417,7 @@ class ShardWorkspace:
         self.qkv = self.qkv_ext[self.hq:]
         self.y = torch.empty(self.n, E, dtype=act, device=dev)
         self.f = torch.empty(self.n, F, dtype=act, device=dev)
+        self.fstats, self.gemm_ws = runtime.ffn_buffers(dev, self.n, E, F)
         # per branch: K/V receive buffer = the need range in token order; send buffer packed by peer
         self.kvs, self.kv_base, self.send, self.send_off = [], [], [], []
         for b in range(len(plan.geo)):
@@ -614,14 +615,9 @@ class SeqParallelEngine:
                     torch.mm(ws.a, pa.w_o.t(), out=ws.y)
                 with runtime.TIMER.span("resid_ln"):
                     _hip.residual_layernorm(ws.x, ws.y, pa.b_o, pl.ln2_w, pl.ln2_b, pl.ln2_eps, ws.a, M, E)
-                with runtime.TIMER.span("gemm_fc1"):
-                    torch.addmm(pl.b1, ws.a, pl.w1.t(), out=ws.f)
-                with runtime.TIMER.span("gelu_ln"):
-                    _hip.gelu_layernorm(ws.f, pl.fln_w, pl.fln_b, pl.fln_eps, ws.f, M, F)
-                with runtime.TIMER.span("gemm_fc2"):
-                    torch.mm(ws.f, pl.w2.t(), out=ws.y)
+                b2 = runtime.ffn_forward(pl, ws.a, ws.f, ws.y, ws.fstats, ws.gemm_ws, M, F)
                 with runtime.TIMER.span("resid_ln"):
-                    _hip.residual_layernorm(ws.x, ws.y, pl.b2, nxt.ln1_w if nxt else None,
+                    _hip.residual_layernorm(ws.x, ws.y, b2, nxt.ln1_w if nxt else None,
                                             nxt.ln1_b if nxt else None, nxt.ln1_eps if nxt else 1e-5, ws.a, M, E)
 
             self._segment(("head", li, wsig), head)

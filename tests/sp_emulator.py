@@ -70,6 +70,34 @@ def gelu_layernorm(h, ln_w, ln_b, eps, out, rows, cols):
     out[:rows] = _ln(v, ln_w, ln_b, eps).to(out.dtype)
 
 
+def ffn_fc1_gelu(a, w1, b1, h, stats):
+    """gp_ffn_fc1_gelu: h = act(gelu(act(a . w1^T + b1))), stats[g][m] = (mean, M2) of h's 256-column group g."""
+    M, F = a.shape[0], w1.shape[0]
+    assert h.shape[0] >= M and h.shape[1] == F and F % 256 == 0 and stats.numel() >= (F // 256 + 1) * M * 2
+    v = (a.float() @ w1.float().t() + (b1.float() if b1 is not None else 0)).to(h.dtype)
+    g = torch.nn.functional.gelu(v.float()).to(h.dtype)
+    h[:M] = g
+    gf = g.float().view(M, F // 256, 256)
+    mean = gf.mean(-1)
+    st = stats.view(-1)[:(F // 256) * M * 2].view(F // 256, M, 2)
+    st[..., 0] = mean.t()
+    st[..., 1] = ((gf - mean[..., None]) ** 2).sum(-1).t()
+
+
+def ffn_fc2_ln(h, w2g, stats, c, d, eps, y, ws=None):
+    """gp_ffn_fc2_ln: y = act(rstd (h . w2g^T - mean c) + d), the row statistics Chan-merged from stats."""
+    M, F = h.shape
+    N = w2g.shape[0]
+    assert y.shape[0] >= M and y.shape[1] == N and c.numel() == N and d.numel() == N
+    st = stats.view(-1)[:(F // 256) * M * 2].view(F // 256, M, 2)
+    mg = st[..., 0]
+    mean = mg.mean(0)
+    m2 = st[..., 1].sum(0) + 256.0 * ((mg - mean) ** 2).sum(0)
+    rstd = torch.rsqrt(m2 / F + eps)
+    acc = h.float() @ w2g.float().t()
+    y[:M] = (rstd[:, None] * (acc - mean[:, None] * c.float()[None]) + d.float()[None]).to(y.dtype)
+
+
 def dilated_sparsify(src, src_row_stride, k_col, v_col, tok_lo, n_tok, L, H, D, segs, ratios, dsts, dst_bases=None):
     assert src.shape[0] >= n_tok and src.shape[1] == src_row_stride
     p = torch.arange(tok_lo, tok_lo + n_tok)
@@ -193,7 +221,7 @@ def install():
     """Replace the _hip entry points in this process (call in a test subprocess only)."""
     from gigapath import _hip
     for name in ("coords_to_pos", "posembed_cls_ln", "layernorm_f32", "mean_tokens", "residual_layernorm",
-                 "gelu_layernorm", "dilated_sparsify", "dilated_sparsify_dests", "attn_branch", "dilated_attn_fwd_ex",
+                 "gelu_layernorm", "ffn_fc1_gelu", "ffn_fc2_ln", "dilated_sparsify", "dilated_sparsify_dests", "attn_branch", "dilated_attn_fwd_ex",
                  "branch_merge_ln_window"):
         setattr(_hip, name, globals()[name])
     _written.clear()
