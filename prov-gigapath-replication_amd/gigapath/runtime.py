@@ -1,18 +1,19 @@
 """MI355X execution engine of the LongNet slide-encoder forward.
 
-Per layer the engine issues 8 launches on torch's current HIP stream (M = B*L tokens):
+Per layer the engine issues 8 kernels on torch's current HIP stream (M = B*L tokens):
 
-    qkv  = a . Wqkv^T + bqkv             hipBLASLt (bias epilogue)         [M, 3E] bf16
+    qkv  = a . Wqkv^T + bqkv             gp_linear (MFMA GEMM, bias epilogue) [M, 3E] bf16
     attn = gp_dilated_attn_fwd(qkv)        ONE launch, all dilation branches  sparse o / lse
     a    = LN_inner(merge(attn))           gp_branch_merge_ln                 [M, E] bf16
-    y    = a . Wo^T                        hipBLASLt                          [M, E] bf16
+    y    = a . Wo^T                        gp_linear                          [M, E] bf16
     x   += y + bo ; a = LN2(x)             gp_residual_layernorm (fp32 residual stream)
     f    = gelu(a . W1^T + b1), stats      gp_ffn_fc1_gelu (MFMA GEMM, GELU + LN statistics epilogue)
     y    = LN_ffn(f) . W2^T + b2           gp_ffn_fc2_ln   (MFMA GEMM, LayerNorm folded into the epilogue)
     x   += y ; a = LN1(next layer)         gp_residual_layernorm
 
-(shapes outside the FFN kernels' instantiations, or GIGAPATH_FFN_FUSED=0: hipBLASLt fc1,
-gp_gelu_layernorm, hipBLASLt fc2 -- 9 launches)
+(plus a split-K reduce after a GEMM whose last round of tiles is split; shapes outside the GEMM
+kernels' instantiations, GIGAPATH_OWN_GEMMS=0 or GIGAPATH_FFN_FUSED=0: hipBLASLt for those GEMMs and,
+for the FFN, hipBLASLt fc1 + gp_gelu_layernorm + hipBLASLt fc2)
 
 which is EncoderLayer.forward (torchscale/architecture/encoder.py:116-162) with
 DilatedAttention.forward (component/dilated_attention.py:133-217) and the FFN
@@ -205,6 +206,7 @@ class PackedAttention:
     ln_eps: float
 
     prescaled: bool = True
+    b_qkv_f32: Optional[torch.Tensor] = None   # [3E] fp32 (gp_linear's bias)
 
     @staticmethod
     def from_module(m, dev, act: torch.dtype = torch.bfloat16) -> "PackedAttention":
@@ -213,10 +215,11 @@ class PackedAttention:
         qs = (D ** -0.5) * LOG2E if D in (48, 64) else 1.0   # D=96 uses the generic kernel
         wq = m.q_proj.weight.detach().to(device=dev, dtype=torch.float32) * qs
         bq = m.q_proj.bias.detach().to(device=dev, dtype=torch.float32) * qs
+        b_qkv = torch.cat([bq, _f32(m.k_proj.bias, dev), _f32(m.v_proj.bias, dev)], 0)
         return PackedAttention(
             E=E, H=H, D=D, segs=list(m.args.segment_length), ratios=list(m.args.dilated_ratio),
             w_qkv=_act(torch.cat([wq, _f32(m.k_proj.weight, dev), _f32(m.v_proj.weight, dev)], 0), dev, act),
-            b_qkv=_act(torch.cat([bq, _f32(m.k_proj.bias, dev), _f32(m.v_proj.bias, dev)], 0), dev, act),
+            b_qkv=_act(b_qkv, dev, act), b_qkv_f32=_act(b_qkv, dev, act).float().contiguous(),
             w_o=_act(m.out_proj.weight, dev, act), b_o=_f32(m.out_proj.bias, dev),
             b_o_act=_act(m.out_proj.bias, dev, act),
             ln_w=_f32(m.inner_attn_ln.weight, dev), ln_b=_f32(m.inner_attn_ln.bias, dev),
@@ -276,6 +279,26 @@ class PackedLayer:
 
 
 FFN_FUSED = os.environ.get("GIGAPATH_FFN_FUSED", "1") != "0"
+# the QKV / out-proj / patch projections on gp_linear (own MFMA GEMM, the default) instead of hipBLASLt.
+# With every GEMM of the forward on gp_gemm.hip kernels (persistent, data-parallel tiles, no workgroup ever
+# waits on another) concurrent HIP-graph replays on several streams run (tests/test_gpu_concurrent.py,
+# r03_p: 6.3 s); with hipBLASLt's stream-K QKV / patch GEMMs the same test hung (r03_o, > 180 s).
+OWN_GEMMS = os.environ.get("GIGAPATH_OWN_GEMMS", "1") == "1"
+
+
+def linear(a: torch.Tensor, w: torch.Tensor, b_act: Optional[torch.Tensor], b_f32: Optional[torch.Tensor],
+           out: torch.Tensor, gemm_ws: Optional[torch.Tensor] = None):
+    """out = a . w^T (+ b): nn.Linear on gp_linear when OWN_GEMMS and its instantiations cover the
+    shape, else hipBLASLt (torch.addmm / mm).  b_act / b_f32: the bias in the act format / fp32."""
+    N, K = w.shape
+    if OWN_GEMMS and a.is_cuda and _hip.gemm_supported(N, K) and (b_act is None or b_f32 is not None):
+        if gemm_ws is not None and gemm_ws.numel() < _hip.gemm_workspace_bytes(a.shape[0], N, K):
+            gemm_ws = None                   # (no split of the last round of tiles)
+        _hip.linear(a, w, b_f32, out, gemm_ws)
+    elif b_act is not None:
+        torch.addmm(b_act, a, w.t(), out=out)
+    else:
+        torch.mm(a, w.t(), out=out)
 
 
 def ffn_fusable(E: int, F: int) -> bool:
@@ -305,11 +328,18 @@ def ffn_forward(pl: "PackedLayer", a: torch.Tensor, f: torch.Tensor, y: torch.Te
 def ffn_buffers(dev, M: int, E: int, F: int):
     """(stats, GEMM workspace) of the fused FFN for M rows, or (None, None) when it does not apply."""
     if not ffn_fusable(E, F):
-        return None, None
+        return None, gemm_workspace(dev, M, E, F)
     stats = torch.empty((F // 256 + 1) * M * 2, dtype=torch.float32, device=dev)
-    nb = _hip.gemm_workspace_bytes(M, E, F) if torch.device(dev).type == "cuda" else 0
-    gws = torch.empty(max(nb, 16), dtype=torch.uint8, device=dev)
-    return stats, gws
+    return stats, gemm_workspace(dev, M, E, F)
+
+
+def gemm_workspace(dev, M: int, E: int, F: int) -> torch.Tensor:
+    """Split-K workspace of the own GEMMs of M rows: fc2 (E x F) and, with OWN_GEMMS, QKV / out-proj."""
+    nb = 0
+    if torch.device(dev).type == "cuda":
+        shapes = [(E, F)] + ([(3 * E, E), (E, E)] if OWN_GEMMS else [])
+        nb = max(_hip.gemm_workspace_bytes(M, n, k) for n, k in shapes if _hip.gemm_supported(n, k))
+    return torch.empty(max(nb, 16), dtype=torch.uint8, device=dev)
 
 
 def param_signature(module: torch.nn.Module) -> tuple:
@@ -464,10 +494,10 @@ class EncoderEngine:
         for li, pl in enumerate(self.layers):
             pa = pl.attn
             with TIMER.span("gemm_qkv"):
-                torch.addmm(pa.b_qkv, ws.a, pa.w_qkv.t(), out=ws.qkv)
+                linear(ws.a, pa.w_qkv, pa.b_qkv, pa.b_qkv_f32, ws.qkv, ws.gemm_ws)
             dilated_attention_core(pa, ws.qkv, B, L, ws.attn, ws.a)
             with TIMER.span("gemm_out"):
-                torch.mm(ws.a, pa.w_o.t(), out=ws.y)
+                linear(ws.a, pa.w_o, None, None, ws.y, ws.gemm_ws)
             with TIMER.span("resid_ln"):
                 _hip.residual_layernorm(ws.x, ws.y, pa.b_o, pl.ln2_w, pl.ln2_b, pl.ln2_eps, ws.a, M, E)
             b2 = ffn_forward(pl, ws.a, ws.f, ws.y, ws.fstats, ws.gemm_ws, M, F)

@@ -603,7 +603,7 @@ class SeqParallelEngine:
 
             def head(pa=pa):
                 with runtime.TIMER.span("gemm_qkv"):
-                    torch.addmm(pa.b_qkv, ws.a, pa.w_qkv.t(), out=ws.qkv)
+                    runtime.linear(ws.a, pa.w_qkv, pa.b_qkv, pa.b_qkv_f32, ws.qkv, ws.gemm_ws)
                 self.sparsify(ws)
 
             def tail(pa=pa, pl=pl, nxt=nxt):
@@ -612,7 +612,7 @@ class SeqParallelEngine:
                     _hip.branch_merge_ln_window(ws.attn.outs, ws.attn.lses, plan.segs, plan.ratios, 1, plan.L, a, M,
                                                 H, D, pa.ln_w, pa.ln_b, pa.ln_eps, ws.a)
                 with runtime.TIMER.span("gemm_out"):
-                    torch.mm(ws.a, pa.w_o.t(), out=ws.y)
+                    runtime.linear(ws.a, pa.w_o, None, None, ws.y, ws.gemm_ws)
                 with runtime.TIMER.span("resid_ln"):
                     _hip.residual_layernorm(ws.x, ws.y, pa.b_o, pl.ln2_w, pl.ln2_b, pl.ln2_eps, ws.a, M, E)
                 b2 = runtime.ffn_forward(pl, ws.a, ws.f, ws.y, ws.fstats, ws.gemm_ws, M, F)

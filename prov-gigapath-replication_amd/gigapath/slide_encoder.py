@@ -176,16 +176,17 @@ class LongNetViT(nn.Module):
             self._top_sig = sig
         return self._top
 
-    def _patch_gemm(self, top, x2d, out):
-        """out = x2d . Wp^T + bp in the call's activation format (hipBLASLt, bias epilogue)."""
+    def _patch_gemm(self, top, x2d, out, gemm_ws=None):
+        """out = x2d . Wp^T + bp in the call's activation format (runtime.linear: gp_linear or hipBLASLt,
+        bias in the epilogue either way)."""
         act = out.dtype
         if act not in top["patch"]:
             dev = out.device
-            top["patch"][act] = (runtime._act(self.patch_embed.proj.weight, dev, act),
-                                 runtime._act(self.patch_embed.proj.bias, dev, act))
-        wp, bp = top["patch"][act]
+            bp = runtime._act(self.patch_embed.proj.bias, dev, act)
+            top["patch"][act] = (runtime._act(self.patch_embed.proj.weight, dev, act), bp, bp.float().contiguous())
+        wp, bp, bpf = top["patch"][act]
         with runtime.TIMER.span("gemm_patch"):
-            torch.addmm(bp, x2d.to(act), wp.t(), out=out)
+            runtime.linear(x2d.to(act), wp, bp, bpf, out, gemm_ws)
 
     # ---------------------------------------------------------------- forward
     @runtime.compute_format
@@ -419,7 +420,7 @@ class LongNetViT(nn.Module):
         if not hasattr(ws, "pos"):
             ws.pos = torch.empty(Nt, dtype=torch.int64, device=dev)
         xp = ws.y[:Nt]
-        self._patch_gemm(top, x_cat, xp)
+        self._patch_gemm(top, x_cat, xp, ws.gemm_ws)
         _hip.coords_to_pos(c_cat.contiguous(), self.slide_ngrids, self.tile_size, ws.pos, None)
         with runtime.TIMER.span("posembed"):
             n0 = 0
@@ -469,9 +470,9 @@ class LongNetViT(nn.Module):
             ws.pos = torch.empty(B * N, dtype=torch.int64, device=dev)
             ws.err = torch.zeros(1, dtype=torch.int32, device=dev)
 
-        # patch embedding (hipBLASLt, bias epilogue) into the spare 16-bit buffer
+        # patch embedding (bias epilogue) into the spare 16-bit buffer
         xp = ws.y[:B * N]
-        self._patch_gemm(top, x.reshape(B * N, C), xp)
+        self._patch_gemm(top, x.reshape(B * N, C), xp, ws.gemm_ws)
         c = coords if coords.dtype in (torch.float32, torch.float64) else coords.float()
         ws.err.zero_()
         _hip.coords_to_pos(c.contiguous(), self.slide_ngrids, self.tile_size, ws.pos, ws.err)
@@ -533,7 +534,7 @@ class LongNetViT(nn.Module):
             ws.err = torch.zeros(1, dtype=torch.int32, device=dev)
         xp = ws.y[:nt]
         if nt > 0:
-            self._patch_gemm(top, x[0, t0:t1], xp)
+            self._patch_gemm(top, x[0, t0:t1], xp, ws.gemm_ws)
         c = coords if coords.dtype in (torch.float32, torch.float64) else coords.float()
         ws.err.zero_()
         if nt > 0:
