@@ -338,7 +338,7 @@ def gemm_workspace(dev, M: int, E: int, F: int) -> torch.Tensor:
     nb = 0
     if torch.device(dev).type == "cuda":
         shapes = [(E, F)] + ([(3 * E, E), (E, E)] if OWN_GEMMS else [])
-        nb = max(_hip.gemm_workspace_bytes(M, n, k) for n, k in shapes if _hip.gemm_supported(n, k))
+        nb = max([_hip.gemm_workspace_bytes(M, n, k) for n, k in shapes if _hip.gemm_supported(n, k)], default=0)
     return torch.empty(max(nb, 16), dtype=torch.uint8, device=dev)
 
 

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-3 pass: GPU tests (all but the 4-stream concurrency test, run on its own), smoke, the 70k bench
+# Round-3 pass: GPU tests (all, the 4-stream concurrency test included), smoke, the 70k bench
 # (C3) + rocprof kernel stats, the 256k single-GPU slide, the C5 packed batch, the fp16 caller timing.
 # Usage: bash tools/gpu_round_r3.sh <tag>
 set -o pipefail
@@ -7,7 +7,7 @@ TAG=${1:-r03_round}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 1200 python -u -m pytest tests -m gpu -x -v --timeout 900 --timeout-method thread -k "not four_stream" > $OUT/pytest_gpu.log 2>&1
+timeout -k 10 1200 python -u -m pytest tests -m gpu -x -v --timeout 900 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 $OUT/pytest_gpu.log; cp gpurun_out/parity_metrics.json $OUT/ 2>/dev/null
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
