@@ -8,6 +8,7 @@ and the plain projection GEMMs, gp_linear against tuned hipBLASLt.  Reports medi
 FFN outputs relative to max |y|.
 
     python tools/ffn_bench.py [--M 70001] [--rounds 7] [--iters 10] [--half] [--out file.json]
+        [--lab tools/attn_lab/liblab_gemm9.so]   # also time a lab build of the same GEMM ABI, interleaved
 """
 import argparse
 import json
@@ -42,8 +43,21 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--half", action="store_true", help="fp16 (the reference pipeline's autocast) instead of bf16")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--lab", default=None, help="a lab library exporting the GEMM ABI (liblab_gemm9.so)")
     args = ap.parse_args()
-    _hip.load_library()
+    prod = _hip.load_library()
+    lab = _hip.load_library(os.path.join(ROOT, args.lab) if args.lab and not os.path.isabs(args.lab) else args.lab) \
+        if args.lab else None
+
+    def using(lib, fn):
+        """fn() with the typed wrappers bound to lib (the product library otherwise)."""
+        def run():
+            _hip._lib = lib
+            try:
+                fn()
+            finally:
+                _hip._lib = prod
+        return run
     dev = torch.device("cuda")
     runtime.use_tuned_gemms(dev)
     act = torch.float16 if args.half else torch.bfloat16
@@ -75,11 +89,18 @@ def main():
     unfused(); fused(); torch.cuda.synchronize()
     diff = ((y0.float() - y1.float()).abs().max() / y0.float().abs().max()).item()
     res = {"M": M, "act": str(act), "ffn_rel_diff": diff, "ffn": {}, "parts": {}, "linear": []}
-    tu, tf = [], []
+    variants = [("unfused", unfused), ("fused", fused)]
+    if lab is not None:
+        y2 = y1.clone()
+        using(lab, fused)()
+        torch.cuda.synchronize()
+        res["lab_vs_product_ffn_rel_diff"] = ((y1.float() - y2.float()).abs().max() / y2.float().abs().max()).item()
+        variants.append(("lab_fused", using(lab, fused)))
+    ts = {k: [] for k, _ in variants}
     for _ in range(args.rounds):
-        tu += timed(unfused, 1, args.iters)
-        tf += timed(fused, 1, args.iters)
-    res["ffn"] = {"unfused_ms": round(statistics.median(tu), 4), "fused_ms": round(statistics.median(tf), 4)}
+        for k, fn in variants:
+            ts[k] += timed(fn, 1, args.iters)
+    res["ffn"] = {k + "_ms": round(statistics.median(v), 4) for k, v in ts.items()}
     parts = {
         "hipblaslt_fc1": lambda: torch.addmm(b1a, a, w1.t(), out=f),
         "gelu_ln": lambda: _hip.gelu_layernorm(f, gam, bet, 1e-5, f, M, F),
@@ -87,6 +108,9 @@ def main():
         "fc1_gelu": lambda: _hip.ffn_fc1_gelu(a, w1, b1, f, stats),
         "fc2_ln": lambda: _hip.ffn_fc2_ln(f, w2g, stats, c2, d2, 1e-5, y1, gws),
     }
+    if lab is not None:
+        parts["lab_fc1_gelu"] = using(lab, parts["fc1_gelu"])
+        parts["lab_fc2_ln"] = using(lab, parts["fc2_ln"])
     for k, fn in parts.items():
         res["parts"][k + "_ms"] = round(statistics.median(timed(fn, args.rounds, args.iters)), 4)
     for name, N, K, has_bias in (("qkv", 3 * E, E, True), ("out", E, E, False), ("fc1", F, E, True),
@@ -104,15 +128,26 @@ def main():
         ours = lambda: _hip.linear(x, w, b, c1, ws)  # noqa: E731
         ref(); ours(); torch.cuda.synchronize()
         d = ((c0.float() - c1.float()).abs().max() / c0.float().abs().max()).item()
-        t0, t1 = [], []
+        fns = [("hipblaslt", ref), ("gp_linear", ours)]
+        row = {"gemm": name, "M": Mi, "N": N, "K": K, "rel_diff": d}
+        if lab is not None:
+            nbl = int(lab.gp_gemm_workspace_bytes(Mi, N, K))
+            wsl = torch.empty(max(nbl, 16), dtype=torch.uint8, device=dev)
+            c2 = torch.empty(Mi, N, dtype=act, device=dev)
+            labf = using(lab, lambda: _hip.linear(x, w, b, c2, wsl))  # noqa: E731
+            labf(); torch.cuda.synchronize()
+            row["lab_rel_diff"] = ((c0.float() - c2.float()).abs().max() / c0.float().abs().max()).item()
+            fns.append(("lab_linear", labf))
+        tt = {k: [] for k, _ in fns}
         for _ in range(args.rounds):
-            t0 += timed(ref, 1, args.iters)
-            t1 += timed(ours, 1, args.iters)
+            for k, fn in fns:
+                tt[k] += timed(fn, 1, args.iters)
         fl = 2.0 * Mi * N * K
-        m0, m1 = statistics.median(t0), statistics.median(t1)
-        res["linear"].append({"gemm": name, "M": Mi, "N": N, "K": K, "rel_diff": d,
-                              "hipblaslt_ms": round(m0, 4), "hipblaslt_tflops": round(fl / m0 / 1e9, 1),
-                              "gp_linear_ms": round(m1, 4), "gp_linear_tflops": round(fl / m1 / 1e9, 1)})
+        for k, v in tt.items():
+            m = statistics.median(v)
+            row[k + "_ms"] = round(m, 4)
+            row[k + "_tflops"] = round(fl / m / 1e9, 1)
+        res["linear"].append(row)
         del x, w, c0, c1
     print(json.dumps(res, indent=1), flush=True)
     if args.out:
