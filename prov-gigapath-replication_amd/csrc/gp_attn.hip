@@ -494,6 +494,32 @@ static_assert(kNWFast == 4 || kNWFast == 8 || kNWFast == 16, "GP_ATTN_NW must be
 #ifndef GP_ATTN_FP16_EXACT
 #define GP_ATTN_FP16_EXACT 1
 #endif
+// GP_ATTN_RING3 (lab; the bf16 fast kernel): a 3-slot K/V ring, tile t+2's LDS-DMA issued at tile t's
+// start and a counted vmcnt before each barrier that retires tile t+1 only, the V^T fragments read by
+// inline asm (the ds_read_tr builtin carries no alias information, so the compiler puts a vmcnt(0) -- a
+// wait for the in-flight staging of the next tile -- before the first V read of every tile) with explicit
+// lgkmcnt waits, and the softmax + P.V split by 32-key sub-tile.  Bit-identical outputs and the same time
+// (r03_s: 1.2811 vs 1.2816 ms per 70k launch, profiles/r03_s_ab_ring3.json): the staging latency is
+// already covered by the other waves of the SIMD, so the product keeps the 2-slot kernel.
+#ifndef GP_ATTN_RING3
+#define GP_ATTN_RING3 0
+#endif
+
+template <int OFF>
+GP_DEV s16x4 ds_read_tr_asm(uint32_t addr) {
+  s16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
+  return r;
+}
+// s_waitcnt with vmcnt(n) (n <= 15) and no lgkm / exp wait
+GP_DEV void wait_vm_only(int n) {
+  switch (n) {
+    case 0: __builtin_amdgcn_s_waitcnt(0x0f70); break;
+    case 1: __builtin_amdgcn_s_waitcnt(0x0f71); break;
+    case 2: __builtin_amdgcn_s_waitcnt(0x0f72); break;
+    default: __builtin_amdgcn_s_waitcnt(0x0f73); break;
+  }
+}
 
 template <int D, bool kPre, int MODE, bool kTab, int NW, bool kH>
 __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_idx) {
@@ -528,8 +554,15 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   constexpr int LPT = (MODE == kModeGen) ? TOT / NT : 1;
   static_assert(MODE != kModeGen || TOT % NT == 0, "");
   constexpr float kThr = 8.0f;               // lazy-rescale threshold (log2 units)
-  constexpr int NBUF = 2;                    // double-buffered K/V tiles
+  constexpr bool kR3 = GP_ATTN_RING3 != 0 && MODE == kModeFast && !kH && !kPV16;
+  constexpr int NBUF = kR3 ? 3 : 2;          // K/V tile buffers (double-buffered, or the kR3 ring)
   __shared__ __attribute__((aligned(16))) char smem[NBUF * BUF];
+  auto bufc = [&](auto bc) -> char* {        // tile buffer B (compile time)
+    return smem + decltype(bc)::value * BUF;
+  };
+  using IB0 = std::integral_constant<int, 0>;
+  using IB1 = std::integral_constant<int, 1>;
+  using IB2 = std::integral_constant<int, 2>;
 
   // ---- work item (32-bit index math: items < 2^31, checked on the host)
   WorkItem wi;
@@ -577,6 +610,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   if constexpr (kOnes) {
     for (int idx = threadIdx.x; idx < NBUF * KT * 2; idx += NT) {   // NBUF bufs x KT rows x 2 chunks
       const int buf = idx / (2 * KT), rem = idx % (2 * KT), row = rem >> 1, half = rem & 1;
+      char* const bb = smem + buf * BUF;
 #if GP_ATTN_ONES_SPARSE
       constexpr uint32_t one = kH ? 0x3C00u : 0x3F80u;   // 1.0 in the operand format
       const uint4 ones = half ? make_uint4(0u, 0u, 0u, 0u) : make_uint4(one, 0u, one, 0u);
@@ -584,7 +618,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
       constexpr uint32_t one2 = kH ? 0x3C003C00u : 0x3F803F80u;
       const uint4 ones = make_uint4(one2, one2, one2, one2);
 #endif
-      *reinterpret_cast<uint4*>(smem + buf * BUF + KTILE + row * VROWB + 32 * (3 ^ (row & 3)) + 16 * half) = ones;
+      *reinterpret_cast<uint4*>(bb + KTILE + row * VROWB + 32 * (3 ^ (row & 3)) + 16 * half) = ones;
     }
   }
 
@@ -642,13 +676,14 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
       loff[u] = tsel ? KTILE + row * VROWB + 32 * ((ch >> 1) ^ (row & 3)) + 16 * (ch & 1) : row * KROWB + ch * 16;
     }
   }
-  auto load_tile = [&](int kv0) {
+  // kDMA: tile kv0 / KT goes to buffer (kv0 / KT) % 2 = the compile-time bc
+  auto load_tile = [&](int kv0, auto bc) {
     if constexpr (kDMA) {
       const int64_t tb = (int64_t)kv0 * kvstride * 2;
       const int64_t nrec = (int64_t)(c - kv0 - 1) * kvstride * 2 + kv_dv + 2 * D;
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
           (void*)((const char*)kbase + tb), (short)0, (int)(nrec < 0x7fffffff ? nrec : 0x7fffffff), 0x00020000);
-      char* bufp = smem + ((kv0 / KT) % NBUF) * BUF;
+      char* bufp = bufc(bc);
 #pragma unroll
       for (int sl = 0; sl < PPW; ++sl) {
         const int pc = w + NW * sl;
@@ -697,16 +732,37 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
     for (int dt = 0; dt < 3; ++dt) o16[nb][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int ntiles = (c + KT - 1) / KT;
+  // kR3: LDS-DMA instructions this wave issues per tile (pieces w, w + NW, ... below kPieces)
+  int npw = 0;
+#pragma unroll
+  for (int sl = 0; sl < PPW; ++sl) npw += (__builtin_amdgcn_readfirstlane(w) + NW * sl < kPieces) ? 1 : 0;
   if (ntiles > 0) {
-    load_tile(0);
+    load_tile(0, IB0());
     store_tile(0);
   }
+  if constexpr (kR3) {
+    if (ntiles > 1) load_tile(KT, IB1());
+    // tile 0 and the ones block landed (tile 1 stays in flight), then the workgroup barrier
+    wait_vm_only(ntiles > 1 ? npw : 0);
+    __builtin_amdgcn_s_waitcnt(0xc07f);      // lgkmcnt(0): the ones-block ds_writes
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  } else
   __syncthreads();
   // every vector load so far (Q fragments, tile 0) is complete here; saying so with a real
   // s_waitcnt (vmcnt 0) lets the compiler's wait insertion drop its "Q may still be in flight"
   // state at the loop head, which otherwise forces vmcnt(0) -- a wait on the next tile's
   // prefetch -- before the first MFMA of every tile
-  __builtin_amdgcn_s_waitcnt(0x0f70);
+  if constexpr (!kR3) __builtin_amdgcn_s_waitcnt(0x0f70);
+  // kR3: the lane part of the V^T fragment addresses (row & 3, the swizzle, the 8-byte column)
+  uint32_t vlane[2] = {0u, 0u};
+  if constexpr (kR3) {
+    const int row_l = 4 * (lane >> 5) + ((lane >> 2) & 3);
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+      vlane[mt] = (uint32_t)(row_l * VROWB + 32 * ((2 * mt + ((lane >> 4) & 1)) ^ (row_l & 3)) + 8 * (lane & 3));
+  }
 
   if constexpr (GP_ATTN_PRIO != 0 && NW >= 8) {
     if (__builtin_amdgcn_readfirstlane((int)threadIdx.x) >= NT / 2) __builtin_amdgcn_s_setprio(1);
@@ -719,11 +775,14 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   const bool wact = !GP_ATTN_SKIP_IDLE || __builtin_amdgcn_readfirstlane(q0 + w * 32) < rows_needed;
   auto tile_step = [&](int t, auto setc) {
     constexpr int SET = decltype(setc)::value;
-    if (t + 1 < ntiles) load_tile((t + 1) * KT);
+    if constexpr (kR3) {
+      if (t + 2 < ntiles) load_tile((t + 2) * KT, std::integral_constant<int, (SET + 2) % 3>());
+    } else {
+      if (t + 1 < ntiles) load_tile((t + 1) * KT, std::integral_constant<int, 1 - SET>());
+    }
     const int kv0 = t * KT;
-    const int bsel = kDMA ? SET : (t & 1);
-    const char* Kb = smem + bsel * BUF;
-    const char* Vb = smem + bsel * BUF + KTILE;
+    const char* Kb = kDMA ? (const char*)bufc(setc) : smem + (t & 1) * BUF;
+    const char* Vb = Kb + KTILE;
     if (wact) {   // (GP_ATTN_SKIP_IDLE) waves with no needed query only stage K/V and join the barriers
       // ---- S^T for two 32-key sub-tiles.  kPre (q pre-multiplied by scale*log2 e): the
       // accumulator starts at -m_run, so it already holds log2-domain scores minus the max.
@@ -774,7 +833,31 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
         mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
       }
       bf16x8 pf[2][2];
-      if constexpr (kPre) {
+      if constexpr (kR3) {
+        // per 32-key sub-tile u: V^T reads (asm), the sub-tile's 16 exp2, one lgkmcnt wait, 4 MFMAs
+        const uint32_t vbase = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const char*)Vb);
+        const uint32_t va0 = vbase + vlane[0], va1 = vbase + vlane[1];
+        auto sub = [&](auto uc) {
+          constexpr int u = decltype(uc)::value;
+          constexpr int R0 = 32 * u * VROWB, R1 = (32 * u + 16) * VROWB, H8 = 8 * VROWB;
+          s16x4 v00l = ds_read_tr_asm<R0>(va0), v00h = ds_read_tr_asm<R0 + H8>(va0);
+          s16x4 v01l = ds_read_tr_asm<R0>(va1), v01h = ds_read_tr_asm<R0 + H8>(va1);
+          s16x4 v10l = ds_read_tr_asm<R1>(va0), v10h = ds_read_tr_asm<R1 + H8>(va0);
+          s16x4 v11l = ds_read_tr_asm<R1>(va1), v11h = ds_read_tr_asm<R1 + H8>(va1);
+  #pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2)
+  #pragma unroll
+            for (int e = 0; e < 8; ++e) pf[u][s2][e] = f2e_slot<kH>(fast_exp2(sacc[u][8 * s2 + e]));
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v00l), "+v"(v00h), "+v"(v01l), "+v"(v01h), "+v"(v10l),
+                       "+v"(v10h), "+v"(v11l), "+v"(v11h));
+          oacc[0] = mfma_32x32x16<kH>(__builtin_bit_cast(bf16x8, __builtin_shufflevector(v00l, v00h, 0, 1, 2, 3, 4, 5, 6, 7)), pf[u][0], oacc[0]);
+          oacc[1] = mfma_32x32x16<kH>(__builtin_bit_cast(bf16x8, __builtin_shufflevector(v01l, v01h, 0, 1, 2, 3, 4, 5, 6, 7)), pf[u][0], oacc[1]);
+          oacc[0] = mfma_32x32x16<kH>(__builtin_bit_cast(bf16x8, __builtin_shufflevector(v10l, v10h, 0, 1, 2, 3, 4, 5, 6, 7)), pf[u][1], oacc[0]);
+          oacc[1] = mfma_32x32x16<kH>(__builtin_bit_cast(bf16x8, __builtin_shufflevector(v11l, v11h, 0, 1, 2, 3, 4, 5, 6, 7)), pf[u][1], oacc[1]);
+        };
+        sub(std::integral_constant<int, 0>());
+        sub(std::integral_constant<int, 1>());
+      } else if constexpr (kPre) {
         if constexpr (!kZM) {
           // scores are s*c - m_run; rescale only when a query's max moved up by > kThr
           // (tile 0: always, which sets m_run to that tile's exact max)
@@ -890,7 +973,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
             for (int nb = 0; nb < 2; ++nb) o16[nb][dt] = mfma_16x16x32<kH>(vf, bq[nb], o16[nb][dt]);
           }
         }
-      } else
+      } else if constexpr (!kR3)
   #pragma unroll
       for (int u = 0; u < 2; ++u)
   #pragma unroll
@@ -909,11 +992,24 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
         }
 
     }
+    if constexpr (kR3) {
+      wait_vm_only(t + 2 < ntiles ? npw : 0);   // tile t+1 landed (this wave's pieces); t+2 stays in flight
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      return;
+    }
     if (t + 1 < ntiles) store_tile((t + 1) & 1);
     if constexpr (kDMA) __builtin_amdgcn_s_waitcnt(0x0f70);   // this wave's DMA pieces landed
     __syncthreads();
   };
-  if constexpr (kDMA) {
+  if constexpr (kR3) {
+    for (int t = 0; t < ntiles; t += 3) {
+      tile_step(t, IB0());
+      if (t + 1 < ntiles) tile_step(t + 1, IB1());
+      if (t + 2 < ntiles) tile_step(t + 2, IB2());
+    }
+  } else if constexpr (kDMA) {
     for (int t = 0; t < ntiles; t += 2) {
       tile_step(t, std::integral_constant<int, 0>());
       if (t + 1 < ntiles) tile_step(t + 1, std::integral_constant<int, 1>());
