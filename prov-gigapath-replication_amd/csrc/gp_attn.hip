@@ -3,12 +3,13 @@
 // scattering (torchscale/component/dilated_attention.py:16-131, flash_attention.py:13-16).
 //
 // Attention kernel design (one launch covers every branch of a layer):
-//   * work item = (branch, batch*segment, head, 128-row q-block); items ordered heaviest
+//   * work item = (branch, batch*segment, head, q-block of NW*32 rows); items ordered heaviest
 //     branch first (LPT) and regrouped so that 8 consecutive q-blocks of one (segment, head)
 //     run on one XCD and share its L2 for K/V;
-//   * 4 waves x 32 query rows; K/V tiles of 64 keys staged in LDS, double buffered (one barrier
-//     per tile).  The dilated gather is folded into the addressing: sparse row i of (segment n,
-//     head h) is token n*s + i*r + h/(Hp/r);
+//   * NW waves x 32 query rows (8 for the LDS-DMA kernels, 4 for the register-staged kModeGen);
+//     K/V tiles of 64 keys staged in LDS, double buffered (one barrier per tile).  The dilated
+//     gather is folded into the addressing: sparse row i of (segment n, head h) is token
+//     n*s + i*r + h/(Hp/r);
 //   * D = 48 / 64 (v2 kernel, dilated_attn32_kernel): S^T = K.Q^T and O^T += V^T.P^T with
 //     v_mfma_f32_32x32x16_bf16; D = 96 (dilated_attn_kernel): v_mfma_f32_16x16x32_bf16;
 //   * the reference's zero-padded keys (dilated_attention.py:85-91, unmasked in flash-attn)
