@@ -44,6 +44,7 @@
 
 #include "gp_api.h"
 #include "gp_common.h"
+#include "gp_gelu_lut.h"
 
 namespace {
 
@@ -128,6 +129,47 @@ GP_DEV float gelu_g(float x) {
   return fmaf(-fabsf(x) * p, e, fmaxf(x, 0.f));
 }
 
+// bf16 GELU by table (gp_gelu_lut.h): h = bf16(gelu(float(x))) is a function of x's 16 bits, so the bf16
+// epilogue looks it up in LDS instead of evaluating gelu_g -- the reference's own fp32 GELU bit for bit
+// (the table is torch's F.gelu) and ~11 VALU per pair of elements (packed 16-bit index arithmetic, two
+// ds_read_u16) instead of ~26.  LDS copy: x = sign | m at byte 8192 sign + 2 (m - LO) -- the sign bit
+// shifted right by 2 is that offset in both 16-bit halves -- the table first in LDS (largest alignment),
+// so the ds_read address is the offset itself.  Halves outside [LO, HI] read a clamped entry and raise
+// `bad`; gelu_fix then applies the generator-checked rules to them.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+constexpr int kLutNegB = 8192;
+static_assert(2 * kGeluLutN <= kLutNegB, "");
+__shared__ __attribute__((aligned(16384))) uint16_t g_lut[(kLutNegB + 2 * kGeluLutN) / 2];
+
+GP_DEV uint32_t gelu_lut_pair(uint32_t xp, bool& bad) {
+  const uint32_t m = xp & 0x7fff7fffu;
+  const u16x2 t = __builtin_bit_cast(u16x2, m) - (u16x2)kGeluLutLo;   // wraps for m < LO
+  const u16x2 tc = __builtin_elementwise_min(t, (u16x2)(kGeluLutN - 1));
+  bad |= __builtin_bit_cast(uint32_t, tc) != __builtin_bit_cast(uint32_t, t);
+  // byte offsets of both halves (2 tc < 2^12: no carry into the high half)
+  const uint32_t off = (__builtin_bit_cast(uint32_t, tc) << 1) | ((xp ^ m) >> 2);
+  const uint32_t lo = *reinterpret_cast<const uint16_t*>(reinterpret_cast<const char*>(g_lut) + (off & 0xffff));
+  const uint32_t hi = *reinterpret_cast<const uint16_t*>(reinterpret_cast<const char*>(g_lut) + (off >> 16));
+  return lo | (hi << 16);
+}
+
+// the halves of xp outside the table: |x| < 2^-16 -> x / 2 (half: the pair's fp32 accumulators halved and
+// rounded, = bf16(x) / 2 exactly), x > HI -> x (+inf from 2^127 up, as torch's formula overflows there),
+// x < -HI -> -0 (NaN for -inf / NaN)
+GP_DEV uint32_t gelu_fix(uint32_t xp, uint32_t hv, uint32_t half) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const uint32_t b = (xp >> (16 * j)) & 0xffff, m = b & 0x7fff;
+    const uint32_t big = (b & 0x8000) ? (m >= 0x7f80 ? 0x7fc0u : 0x8000u) : (m - 0x7f00u < 0x80u ? 0x7f80u : b);
+    uint32_t v = (hv >> (16 * j)) & 0xffff;
+    v = m > (uint32_t)kGeluLutHi ? big : v;
+    v = m < (uint32_t)kGeluLutLo ? (half >> (16 * j)) & 0xffff : v;
+    r |= v << (16 * j);
+  }
+  return r;
+}
+
 // Chan merge of nst (mean, M2) groups of 256 values -> (mean, rstd) of the row (biased variance + eps)
 GP_DEV float2 merge_row_stats(const float2* st, int64_t stride, int nst, float eps) {
   float msum = 0.f;
@@ -181,6 +223,14 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
   } else {
     if (g.colp0 != nullptr)
       for (int c = threadIdx.x; c < g.N; c += kThreads) g_colp[c] = g.colp0[c];
+  }
+  if constexpr (EPI == kEpiGelu && !kH) {   // the GELU table (published by run_seq's first barrier)
+    static_assert(kGeluLutN % 2 == 0, "");
+    for (int i = threadIdx.x; i < kGeluLutN; i += kThreads) {   // dword i: entries 2i, 2i+1
+      const int half = i >= kGeluLutN / 2;
+      reinterpret_cast<uint32_t*>(g_lut)[i - half * (kGeluLutN / 2) + half * (kLutNegB / 4)] =
+          reinterpret_cast<const uint32_t*>(gp_gelu_lut_bf16)[i];
+    }
   }
 
   // buffer descriptors of tile T: A rows past M read as zero (record count ends at row M)
@@ -296,15 +346,45 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
 #pragma unroll
       for (int mi = 0; mi < 8; ++mi) {
         float s = 0.f, s2 = 0.f;
+        if constexpr (!kH) {   // bf16: table lookup, sums by v_dot2 (exact bf16 products, fp32 adds)
+          uint32_t xp[4][2];
+          bool bad = false;
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) {
+          for (int ni = 0; ni < 4; ++ni)
 #pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            const uint32_t xp = pack2e<kH>(acc[mi][ni][2 * e], acc[mi][ni][2 * e + 1]);
-            hp[mi][ni][e] = pack2e<kH>(gelu_g(e2f<kH>(xp)), gelu_g(e2f_hi<kH>(xp)));
-            const float h0 = e2f<kH>(hp[mi][ni][e]), h1 = e2f_hi<kH>(hp[mi][ni][e]);
-            s += h0 + h1;
-            s2 = fmaf(h0, h0, fmaf(h1, h1, s2));
+            for (int e = 0; e < 2; ++e) {
+              xp[ni][e] = pack2e<false>(acc[mi][ni][2 * e], acc[mi][ni][2 * e + 1]);
+              hp[mi][ni][e] = gelu_lut_pair(xp[ni][e], bad);
+            }
+          if (__builtin_amdgcn_ballot_w64(bad) != 0) {   // a |x| < 2^-16 or > 5.53 in this m-frag (rare)
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+              for (int e = 0; e < 2; ++e)
+                hp[mi][ni][e] = gelu_fix(xp[ni][e], hp[mi][ni][e],
+                                         pack2e<false>(acc[mi][ni][2 * e] * 0.5f, acc[mi][ni][2 * e + 1] * 0.5f));
+          }
+          typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+          const bf16x2v one2 = __builtin_bit_cast(bf16x2v, 0x3f803f80u);
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+              const bf16x2v hv = __builtin_bit_cast(bf16x2v, hp[mi][ni][e]);
+              s = __builtin_amdgcn_fdot2_f32_bf16(hv, one2, s, false);
+              s2 = __builtin_amdgcn_fdot2_f32_bf16(hv, hv, s2, false);
+            }
+        } else {
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni) {
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+              const uint32_t xp = pack2e<kH>(acc[mi][ni][2 * e], acc[mi][ni][2 * e + 1]);
+              hp[mi][ni][e] = pack2e<kH>(gelu_g(e2f<kH>(xp)), gelu_g(e2f_hi<kH>(xp)));
+              const float h0 = e2f<kH>(hp[mi][ni][e]), h1 = e2f_hi<kH>(hp[mi][ni][e]);
+              s += h0 + h1;
+              s2 = fmaf(h0, h0, fmaf(h1, h1, s2));
+            }
           }
         }
         s += __shfl_xor(s, 16, 64);
@@ -375,7 +455,15 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
         }
         typedef int i32x4 __attribute__((ext_vector_type(4)));
         const i32x4 v4 = {(int)pk[0][0], (int)pk[0][1], (int)pk[1][0], (int)pk[1][1]};
+        // Store-data hazard: hipcc spaces a VALU write of a store's data registers from a b128 store only
+        // when soffset is not an SGPR, yet on gfx950 the store can still read such a register after the
+        // next instruction has rewritten it (measured: the GELU epilogue's m-frag 1 store, 4 rows of every
+        // tile wrong, timing-dependent).  Two wait states after every store, as the model
+        // gives the other case.
         __builtin_amdgcn_raw_buffer_store_b128(v4, rc, c_lane + pr * 64, mi * c_mi, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_nop 1");
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
   };

@@ -7,7 +7,8 @@ the same ops on the same 16-bit inputs (run with -m gpu on an MI355X).
 
 Tolerances: outputs are 16-bit (one rounding: max |d| <= 1e-2 of max |ref|); h is compared
 elementwise with the reference's two roundings (>= 97 % bit-identical, the rest within the propagation
-of one 16-bit ulp of the pre-activation); the statistics to 1e-5 relative of the kernel's own h.
+of one 16-bit ulp of the pre-activation) and, for bf16, bit for bit with torch's GELU of the kernel's own
+pre-activation (every bf16 input value included); the statistics to 1e-5 relative of the kernel's own h.
 """
 import pytest
 import torch
@@ -115,6 +116,17 @@ def test_ffn_fc1_gelu_and_statistics(act, M):
     torch.cuda.synchronize()
     x = a.float() @ w1.float().t() + b1
     ref = torch.nn.functional.gelu(x.to(act).float()).to(act)
+    if act == torch.bfloat16:
+        # bf16 h comes from torch's own GELU table: bit-identical to gelu(pre.float()).type_as(pre) of the
+        # kernel's pre-activation, which gp_linear (same tiles, same accumulation order, no K split)
+        # reproduces
+        pre = torch.empty(M, F, dtype=act, device=DEV)
+        h.linear(a, w1, b1, pre, None)
+        torch.cuda.synchronize()
+        # (torch's CPU GELU, the oracle's and the table's; the GPU build of F.gelu rounds ~0.4 % of bf16
+        # inputs differently)
+        exact = torch.nn.functional.gelu(pre.float().cpu()).to(act)
+        assert torch.equal(hh.cpu(), exact), int((hh.cpu() != exact).sum())
     # the same two roundings as the reference: identical wherever the MFMA sums (accumulation order and
     # the matrix core's internal adds, as in any MFMA GEMM) and the fp32 sums of the restatement round the
     # pre-activation alike (measured ~98.8 %); elsewhere the pre-activation differs by one 16-bit ulp or by
@@ -134,6 +146,32 @@ def test_ffn_fc1_gelu_and_statistics(act, M):
     m2 = ((hg - hg.mean(-1, keepdim=True)) ** 2).sum(-1).t()
     assert torch.allclose(st[..., 0], mean, rtol=1e-5, atol=1e-6)
     assert torch.allclose(st[..., 1], m2, rtol=1e-4, atol=1e-4)
+
+
+def test_ffn_fc1_gelu_every_bf16_value():
+    """Every finite normal bf16 pre-activation (and +-0) through the bf16 GELU epilogue -- the table, its
+    clamped edges and the out-of-table rules (|x| < 2^-13, |x| > 5.53): A = the 768 x 768 identity (one
+    exact product per output), so pre-activation (m, n) is W1[n, m], and the 65,536 bit patterns fill
+    W1 [3072, 768]."""
+    h = _hip()
+    E, F = 768, 3072
+    bits = torch.arange(0, 65536, dtype=torch.int32)
+    mag = bits & 0x7FFF
+    keep = ((mag >= 0x80) & (mag < 0x7F80)) | (mag == 0)          # normal finite, +-0
+    vals = bits[keep].to(torch.int16).view(torch.bfloat16)
+    w1 = vals.repeat((F * E) // vals.numel() + 1)[:F * E].view(F, E).to(DEV)
+    a = torch.eye(E, dtype=torch.bfloat16, device=DEV)
+    hh = torch.empty(E, F, dtype=torch.bfloat16, device=DEV)
+    stats = torch.empty((F // 256 + 1) * E * 2, device=DEV)
+    h.ffn_fc1_gelu(a, w1, None, hh, stats)
+    pre = torch.empty(E, F, dtype=torch.bfloat16, device=DEV)
+    h.linear(a, w1, None, pre, None)
+    torch.cuda.synchronize()
+    assert torch.equal(pre.float(), w1.t().float())                  # every pattern reached the epilogue
+    exact = torch.nn.functional.gelu(pre.float().cpu()).to(torch.bfloat16)
+    hh = hh.cpu()
+    bad = hh.view(torch.int16) != exact.view(torch.int16)           # bit patterns: -0 is not +0
+    assert not bad.any(), (pre.cpu()[bad][:8].float().tolist(), hh[bad][:8].float().tolist(), int(bad.sum()))
 
 
 @pytest.mark.parametrize("act", ACTS)
