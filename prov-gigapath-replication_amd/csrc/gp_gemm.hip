@@ -200,7 +200,7 @@ __global__ __launch_bounds__(256) void row_stats_kernel(float* stats, int M, int
 // takes sid, sid + G, ...  Tiles [n_dp, ntiles) -- the last, partial round -- are split S ways in K when
 // the host asks for it (n_dp a multiple of G, (ntiles - n_dp) * S <= G): unit u = sid takes tile
 // n_dp + u / S, K-tiles [(u % S) NK/S, +NK/S), and writes its fp32 partial tile to the workspace.
-template <int NK, int S, int EPI, bool kH>
+template <int NK, int S, int EPI, bool kH, bool NT = false>
 __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
   static_assert(NK % 2 == 0 && NK >= 2 && (S == 1 || (NK % (2 * S) == 0)), "");
   const int tiles_n = g.N / kBN;
@@ -460,13 +460,21 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
         // next instruction has rewritten it (measured: the GELU epilogue's m-frag 1 store, 4 rows of every
         // tile wrong, timing-dependent).  Two wait states after every store, as the model
         // gives the other case.
-        __builtin_amdgcn_raw_buffer_store_b128(v4, rc, c_lane + pr * 64, mi * c_mi, 0);
+#ifdef GP_EXP_NOSTORE
+        if (g.ldc < 0)   // lab: never true -- the epilogue without its stores
+#endif
+        // (NT: non-temporal stores for wide, short-K outputs, see launch())
+        __builtin_amdgcn_raw_buffer_store_b128(v4, rc, c_lane + pr * 64, mi * c_mi, NT ? 2 : 0);
         __builtin_amdgcn_sched_barrier(0);
         asm volatile("s_nop 1");
         __builtin_amdgcn_sched_barrier(0);
       }
     }
   };
+  // the VMEM instructions EVERY wave issues in epilogue_tile: 8 m-frags x 2 stores (waves 0-3 of the GELU
+  // epilogue add a statistics store, wave 0 of the LN fold two LDS-DMA pieces in init_tile: a wait
+  // counted with the minimum is only stricter for them)
+  constexpr int kEpiVmem = 16;
   // accumulators start at zero, or at the bias (linear, GELU): the epilogue then has no add
   auto zero_acc = [&]() {
 #pragma unroll
@@ -529,7 +537,10 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
     // stage half H of operand OP of the tile-local K-tile vv (vv >= nk: the next tile's K-tile vv - nk)
     auto stage = [&](auto opc, auto hc, auto bc, int vv) {
       constexpr int OP = decltype(opc)::value;
-      if (vv < nk || has_next) issue(opc, hc, bc, OP == 0 ? ra : rw, kt0 + (vv < nk ? vv : vv - nk));
+      // (unconditional: past the last tile the descriptors still name the current one and the pieces
+      // re-load consumed K-tiles -- a DMA issued on one path only made hipcc put a vmcnt(0) before
+      // later LDS reads)
+      issue(opc, hc, bc, OP == 0 ? ra : rw, kt0 + (vv < nk ? vv : vv - nk));
     };
     // one K-tile v of the current output tile, in buffer B (v even: B = 0).  Phases (quadrant; fragments
     // read; DMA issued): Q0 (m0, n0; A m-half 0 + W n-half 0; A half 0 of K-tile v+1), Q1 (m0, n1; W
@@ -540,14 +551,15 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
     auto ktile = [&](auto bc, int v) {
       constexpr int B = decltype(bc)::value;
       using BN_ = std::integral_constant<int, 1 - B>;
+      const bool pre = v == 0;   // K-tile 1's A halves are already in flight (see the tile loop)
       read_a(bc, I0());
       read_w(bc, I0());
-      stage(I0(), I0(), BN_(), v + 1);
+      if (!pre) stage(I0(), I0(), BN_(), v + 1);   // (pre: compile-time after the unroll)
       sync();
       quadrant(I0(), I0());
       sync();
       read_w(bc, I1());
-      stage(I0(), I1(), BN_(), v + 1);
+      if (!pre) stage(I0(), I1(), BN_(), v + 1);
       sync();
       quadrant(I0(), I1());
       sync();
@@ -555,29 +567,38 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
       sync();
       quadrant(I1(), I1());
       sync();
-      if (v + 2 == nk && has_next) {   // every DMA of this tile is issued: switch to the next tile's
-        ra = rsrc_a(tile_of(i_cur + 1));
-        rw = rsrc_w(tile_of(i_cur + 1));
+      if (v + 2 == nk) {   // every DMA of this tile is issued: switch to the next tile's (if any)
+        const int Tn = tile_of(has_next ? i_cur + 1 : i_cur);
+        ra = rsrc_a(Tn);
+        rw = rsrc_w(Tn);
       }
-      if (v + 2 < nk || has_next) {
-        stage(I1(), I0(), bc, v + 2);
-        stage(I1(), I1(), bc, v + 2);
-        wait_vmcnt<4>();
-      } else {
-        wait_vmcnt<0>();
-      }
+      stage(I1(), I0(), bc, v + 2);
+      stage(I1(), I1(), bc, v + 2);
+      // retire K-tile v+1 (the weights of v+2 stay in flight); at v = 0 K-tile 1's A halves are older
+      // than the previous tile's epilogue stores (or the prologue's stand-ins), which may stay in flight
+      if (pre) wait_vmcnt<4 + kEpiVmem>();
+      else wait_vmcnt<4>();
       sync();
       quadrant(I1(), I0());
       sync();
     };
-    // prologue: K-tile 0 whole, K-tile 1's W halves (its A halves come in K-tile 0's Q0-Q1)
+    // prologue: K-tile 0 whole, K-tile 1 whole, then kEpiVmem stores through an empty descriptor
+    // (dropped by the hardware) standing in for an epilogue's: every tile then starts in the same
+    // VMEM state, and K-tile 0's counted wait is one compile-time constant
     issue(I0(), I0(), I0(), ra, kt0);
     issue(I0(), I1(), I0(), ra, kt0);
     issue(I1(), I0(), I0(), rw, kt0);
     issue(I1(), I1(), I0(), rw, kt0);
     issue(I1(), I0(), I1(), rw, kt0 + 1);
     issue(I1(), I1(), I1(), rw, kt0 + 1);
-    wait_vmcnt<4>();
+    issue(I0(), I0(), I1(), ra, kt0 + 1);
+    issue(I0(), I1(), I1(), ra, kt0 + 1);
+    {
+      const __amdgpu_buffer_rsrc_t none = __builtin_amdgcn_make_buffer_rsrc(g.ws, (short)0, 0, 0x00020000);
+#pragma unroll
+      for (int j = 0; j < kEpiVmem; ++j) __builtin_amdgcn_raw_buffer_store_b32(0, none, 0, 0, 0);
+    }
+    wait_vmcnt<8 + kEpiVmem>();     // K-tile 0 landed
     lds_barrier();                  // (also publishes the column parameters)
     for (int i = 0; i < count; ++i) {
       has_next = i + 1 < count;
@@ -593,6 +614,13 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
         ktile(I1(), v + 1);
       }
       if (wm == 0) sync();          // realign
+      // The next tile's K-tile 1 A halves go out BEFORE this tile's stores.  vmcnt counts stores too and
+      // retires in order, so a wait for a load issued after the stores waits for the stores; issued
+      // before them, the next tile's first wait (K-tile 0's Q3) can leave the stores in flight, and they
+      // drain behind a whole K-tile of MFMAs instead of stalling it.  (Buffer 1's A halves were last read
+      // in this tile's last Q2; every wave is past its last MFMA here.)
+      issue(I0(), I0(), I1(), ra, kt0 + 1);
+      issue(I0(), I1(), I1(), ra, kt0 + 1);
       epilogue(i);
     }
     wait_vmcnt<0>();   // no LDS-DMA in flight past the sequence (LDS reuse, hand-off)
@@ -710,20 +738,36 @@ template <int EPI, bool kH>
 int launch(GemmArgs g, const Plan& p, hipStream_t s) {
   g.n_dp = p.n_dp;
   g.split = p.S > 1;
+  // Output stores: every CU finishes a tile at about the same moment, so each round of tiles writes
+  // G x 128 KiB at once (a whole XCD's L2 per round).  For wide, short-K outputs (QKV 2304 x 768, fc1
+  // 3072 x 768) non-temporal stores drain that burst faster: -14 % per launch; for N = 768 or K = 3072
+  // they are 4-10 % slower (r03_w probe).
+  const bool nt = g.N >= 2048 && g.K <= 1536;
   const dim3 grid((unsigned)p.G), block(kThreads);
   constexpr bool kSplit = EPI != kEpiGelu;   // (the GELU plan never splits)
+  auto go = [&](auto nkc, auto ntc) {
+    constexpr int NKc = decltype(nkc)::value;
+    constexpr bool NTc = decltype(ntc)::value;
+    if (kSplit && p.S > 1) gemm_kernel<NKc, kSplit ? (NKc == 12 ? 2 : 4) : 1, EPI, kH, NTc><<<grid, block, 0, s>>>(g);
+    else gemm_kernel<NKc, 1, EPI, kH, NTc><<<grid, block, 0, s>>>(g);
+  };
+  using F_ = std::false_type;
+  using T_ = std::true_type;
   switch (g.K) {
     case 768:
-      if (kSplit && p.S > 1) gemm_kernel<12, kSplit ? 2 : 1, EPI, kH><<<grid, block, 0, s>>>(g);
-      else gemm_kernel<12, 1, EPI, kH><<<grid, block, 0, s>>>(g);
+      if constexpr (EPI != kEpiLnFold) {
+        if (nt) { go(std::integral_constant<int, 12>(), T_()); break; }
+      }
+      go(std::integral_constant<int, 12>(), F_());
       break;
     case 1536:
-      if (kSplit && p.S > 1) gemm_kernel<24, kSplit ? 4 : 1, EPI, kH><<<grid, block, 0, s>>>(g);
-      else gemm_kernel<24, 1, EPI, kH><<<grid, block, 0, s>>>(g);
+      if constexpr (EPI != kEpiLnFold) {
+        if (nt) { go(std::integral_constant<int, 24>(), T_()); break; }
+      }
+      go(std::integral_constant<int, 24>(), F_());
       break;
     default:
-      if (kSplit && p.S > 1) gemm_kernel<48, kSplit ? 4 : 1, EPI, kH><<<grid, block, 0, s>>>(g);
-      else gemm_kernel<48, 1, EPI, kH><<<grid, block, 0, s>>>(g);
+      go(std::integral_constant<int, 48>(), F_());
       break;
   }
   if constexpr (EPI != kEpiGelu) {
