@@ -461,7 +461,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
         // tile wrong, timing-dependent).  Two wait states after every store, as the model
         // gives the other case.
 #ifdef GP_EXP_NOSTORE
-        if (g.ldc < 0)   // lab: never true -- the epilogue without its stores
+        if (g.ldc < 0)   // lab (tools/gemm_overhead_probe.py): never true -- the epilogue without its stores
 #endif
         // (NT: non-temporal stores for wide, short-K outputs, see launch())
         __builtin_amdgcn_raw_buffer_store_b128(v4, rc, c_lane + pr * 64, mi * c_mi, NT ? 2 : 0);
