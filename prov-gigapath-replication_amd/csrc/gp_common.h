@@ -139,6 +139,24 @@ GP_DEV void st_x4_f32(float* row, int lane, const float* v) {
   for (int k = 0; k < EPL / 4; ++k)
     *reinterpret_cast<float4*>(row + k * 256 + 4 * lane) = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
 }
+// non-temporal variants (streamed rows that the next kernels do not read back soon)
+typedef float gp_f4v __attribute__((ext_vector_type(4)));
+template <int EPL>
+GP_DEV void ld_x4_f32_nt(const float* row, int lane, float* v) {
+#pragma unroll
+  for (int k = 0; k < EPL / 4; ++k) {
+    const gp_f4v u = __builtin_nontemporal_load(reinterpret_cast<const gp_f4v*>(row + k * 256 + 4 * lane));
+    v[4 * k] = u.x; v[4 * k + 1] = u.y; v[4 * k + 2] = u.z; v[4 * k + 3] = u.w;
+  }
+}
+template <int EPL>
+GP_DEV void st_x4_f32_nt(float* row, int lane, const float* v) {
+#pragma unroll
+  for (int k = 0; k < EPL / 4; ++k) {
+    const gp_f4v u = {v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]};
+    __builtin_nontemporal_store(u, reinterpret_cast<gp_f4v*>(row + k * 256 + 4 * lane));
+  }
+}
 template <int EPL>
 GP_DEV void ld_x4_bf16(const uint16_t* row, int lane, float* v) {
 #pragma unroll

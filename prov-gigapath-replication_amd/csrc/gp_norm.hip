@@ -117,11 +117,14 @@ __global__ __launch_bounds__(256) void residual_ln_kernel(float* __restrict__ x,
   for (int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6); row < rows;
        row += (int64_t)gridDim.x * kRowsPerBlock) {
     float v[EPL], yv[EPL];
-    ld_x4_f32<EPL>(x + row * cols, lane, v);
+    // the fp32 residual stream is read and written back once per half-layer and not touched again until
+    // the next one (~15 ms later at 70k): non-temporal both ways, the caches keep y and the LN output
+    // the next GEMM reads (−13 % per launch in isolation, profiles/r03_y_resid_ab.json)
+    ld_x4_f32_nt<EPL>(x + row * cols, lane, v);
     ld_x4_e<kH, EPL>(y + row * cols, lane, yv);
 #pragma unroll
     for (int i = 0; i < EPL; ++i) v[i] += yv[i] + bb[i];
-    st_x4_f32<EPL>(x + row * cols, lane, v);
+    st_x4_f32_nt<EPL>(x + row * cols, lane, v);
     if (ln_w != nullptr) {
       wave_layernorm_regs<EPL>(v, cols, wv, bv, eps);
       st_x4_e<kH, EPL>(out + row * cols, lane, v);
