@@ -244,7 +244,8 @@ int gp_linear(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, co
               int fmt, void* stream);
 
 /* FFN first half (feedforward_network.py:131-135): fc1 with the GELU in its epilogue,
- *   h = act(gelu(act(A . W1^T + b1)))     (gelu(x.float()).type_as(x), exact erf)
+ *   h = act(gelu(act(A . W1^T + b1)))     (gelu(x.float()).type_as(x), exact erf; for bf16 h is
+ *                                          torch's CPU F.gelu bit for bit, a table of the 16-bit inputs)
  * and the LayerNorm statistics of h per 256-column group g:
  *   stats[g][m] = (mean, sum of squared deviations) of h[m, 256 g : 256 g + 256]   (fp32 pairs)
  * A: [M, K] act; W1: [F, K] act; b1: [F] fp32 or NULL; h: [M, F] act (ldh); stats: [F/256 + 1, M, 2]
