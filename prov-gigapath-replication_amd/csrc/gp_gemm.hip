@@ -429,10 +429,20 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
     const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
         reinterpret_cast<void*>(cpu), (short)0, __builtin_amdgcn_readfirstlane((int)(c_rows * g.ldc * 2)),
         0x00020000);
-    const int c_lane = (int)((r16 * g.ldc + 16 * (q & 1) + 8 * (q >> 1)) * 2);
+    // Full-line stores: after the v_permlane16_swap below, lane (r16, q) holds for m-frag mi two 16-byte
+    // column chunks of row r16 (V[0]: the wave's columns 0-31, V[1]: 32-63).  One DPP row_ror:8 per dword
+    // hands rows 8-15's V[0] to lanes 0-7 and rows 0-7's V[1] to lanes 8-15 of every 16-lane row, so each
+    // 16-byte store then writes 8 rows x the whole 128-byte line of the wave's 64 columns (8 lanes per
+    // row) instead of 16 rows x half lines -- half-line non-temporal writes cost 1.5x the bytes in HBM
+    // (PMC r03_z: QKV WRITE_SIZE 488 MB for a 322 MB output).
+    const int c_lane = (int)(((r16 & 7) * g.ldc + 16 * (q & 1) + 8 * (q >> 1) + 32 * (r16 >> 3)) * 2);
     const int c_mi = (int)(16 * g.ldc * 2);
+    const int c_hi = (int)(8 * g.ldc * 2);
+    const bool lo8 = r16 < 8;
 #pragma unroll
     for (int mi = 0; mi < 8; ++mi) {
+      typedef int i32x4 __attribute__((ext_vector_type(4)));
+      i32x4 V[2];
 #pragma unroll
       for (int pr = 0; pr < 2; ++pr) {
         uint32_t pk[2][2];
@@ -453,18 +463,27 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
           pk[0][d] = r[0];
           pk[1][d] = r[1];
         }
-        typedef int i32x4 __attribute__((ext_vector_type(4)));
-        const i32x4 v4 = {(int)pk[0][0], (int)pk[0][1], (int)pk[1][0], (int)pk[1][1]};
-        // Store-data hazard: hipcc spaces a VALU write of a store's data registers from a b128 store only
-        // when soffset is not an SGPR, yet on gfx950 the store can still read such a register after the
-        // next instruction has rewritten it (measured: the GELU epilogue's m-frag 1 store, 4 rows of every
-        // tile wrong, timing-dependent).  Two wait states after every store, as the model
-        // gives the other case.
+        V[pr] = i32x4{(int)pk[0][0], (int)pk[0][1], (int)pk[1][0], (int)pk[1][1]};
+      }
+      i32x4 X, Y;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const int r0 = __builtin_amdgcn_update_dpp(0, V[0][d], 0x128, 0xf, 0xf, false);   // row_ror:8
+        const int r1 = __builtin_amdgcn_update_dpp(0, V[1][d], 0x128, 0xf, 0xf, false);
+        X[d] = lo8 ? V[0][d] : r1;   // rows 0-7
+        Y[d] = lo8 ? r0 : V[1][d];   // rows 8-15
+      }
+      // Store-data hazard: hipcc spaces a VALU write of a store's data registers from a b128 store only
+      // when soffset is not an SGPR, yet on gfx950 the store can still read such a register after the
+      // next instruction has rewritten it (measured: the GELU epilogue's m-frag 1 store, 4 rows of every
+      // tile wrong, timing-dependent).  Two wait states after every store, as the model
+      // gives the other case.  (NT: non-temporal stores for wide, short-K outputs, see launch().)
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
 #ifdef GP_EXP_NOSTORE
         if (g.ldc < 0)   // lab (tools/gemm_overhead_probe.py): never true -- the epilogue without its stores
 #endif
-        // (NT: non-temporal stores for wide, short-K outputs, see launch())
-        __builtin_amdgcn_raw_buffer_store_b128(v4, rc, c_lane + pr * 64, mi * c_mi, NT ? 2 : 0);
+        __builtin_amdgcn_raw_buffer_store_b128(hh ? Y : X, rc, c_lane, mi * c_mi + hh * c_hi, NT ? 2 : 0);
         __builtin_amdgcn_sched_barrier(0);
         asm volatile("s_nop 1");
         __builtin_amdgcn_sched_barrier(0);
@@ -742,7 +761,10 @@ int launch(GemmArgs g, const Plan& p, hipStream_t s) {
   // G x 128 KiB at once (a whole XCD's L2 per round).  For wide, short-K outputs (QKV 2304 x 768, fc1
   // 3072 x 768) non-temporal stores drain that burst faster: -14 % per launch; for N = 768 or K = 3072
   // they are 4-10 % slower (r03_w probe).
-  const bool nt = g.N >= 2048 && g.K <= 1536;
+#ifndef GP_NT_MIN_N
+#define GP_NT_MIN_N 2048   // (lab builds probe other thresholds)
+#endif
+  const bool nt = g.N >= GP_NT_MIN_N && g.K <= 1536;
   const dim3 grid((unsigned)p.G), block(kThreads);
   constexpr bool kSplit = EPI != kEpiGelu;   // (the GELU plan never splits)
   auto go = [&](auto nkc, auto ntc) {
