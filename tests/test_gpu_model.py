@@ -23,9 +23,16 @@ def close_enough(got, ref, ref_bf16_dev=0.0):
     return rel, cos, rel <= max(2e-2, 1.5 * ref_bf16_dev) and cos >= 0.9995
 
 
-def check_vectors(test, name, got, ref, ref_bf16_dev=0.0):
+# the north star's stated bf16 tolerance on slide embeddings (BASELINE.json: "max-rel 1e-2"): the C3 / C4
+# headline goldens must also stay inside it -- a regression guard below the survey's 2e-2 acceptance,
+# since every moved rounding point (LN folds, residual epilogues) spends headroom
+NORTH_STAR_REL = 1e-2
+
+
+def check_vectors(test, name, got, ref, ref_bf16_dev=0.0, north_star=False):
     """Every output vector (last axis) within the model tolerance; the worst rel / cos is recorded
-    (conftest.record_parity) so the headroom is on record, not only the pass."""
+    (conftest.record_parity) so the headroom is on record, not only the pass.  north_star: the worst
+    vector must also be within NORTH_STAR_REL (the C3 / C4 headline slides)."""
     got, ref = np.asarray(got), np.asarray(ref)
     assert got.shape == ref.shape, (name, got.shape, ref.shape)
     worst_rel, worst_cos = 0.0, 1.0
@@ -33,8 +40,10 @@ def check_vectors(test, name, got, ref, ref_bf16_dev=0.0):
         rel, cos, ok = close_enough(got[idx], ref[idx], ref_bf16_dev)
         assert ok, (test, name, idx, rel, cos)
         worst_rel, worst_cos = max(worst_rel, rel), min(worst_cos, cos)
-    record_parity(test, name, worst_rel, worst_cos, max(2e-2, 1.5 * ref_bf16_dev), 0.9995,
-                  int(np.prod(got.shape[:-1])))
+    tol = NORTH_STAR_REL if north_star else max(2e-2, 1.5 * ref_bf16_dev)
+    record_parity(test, name, worst_rel, worst_cos, tol, 0.9995, int(np.prod(got.shape[:-1])))
+    if north_star:
+        assert worst_rel <= NORTH_STAR_REL, (test, name, "north-star max-rel", worst_rel)
 
 
 @pytest.fixture(scope="module")
@@ -141,7 +150,7 @@ def test_c3_70k_end_to_end_vs_reference_golden(model):
             model.global_pool = False
     assert all(np.array_equal(r, allv) for r in rep)
     for name, got in (("all_layer", allv), ("last", last), ("gp_all_layer", gp_all), ("gp_last", gp_last)):
-        check_vectors("C3 e2e N=70000", name, got, g[name])
+        check_vectors("C3 e2e N=70000", name, got, g[name], north_star=True)
 
 
 def test_fp16_autocast_caller_vs_reference_golden(model, golden_meta):

@@ -470,12 +470,15 @@ constexpr int kNWFast = GP_ATTN_NW;
 #define GP_ATTN_PRIO 1
 #endif
 static_assert(kNWFast == 4 || kNWFast == 8 || kNWFast == 16, "GP_ATTN_NW must be 4, 8 or 16");
-#ifndef GP_ATTN_SKIP_IDLE
-#define GP_ATTN_SKIP_IDLE 1
-#endif
 // GP_ATTN_ONES_SPARSE: the V image's spare d-block carries 1.0 only in the two rows the epilogue reads
 // (d = 48 and 52) and 0 elsewhere: same outputs, fewer toggling MFMA operand bits (same-box A/B
 // 1.276 -> 1.262 ms per 70k layer, profiles/r02_s6_ab_ones.json)
+#ifndef GP_ATTN_PV16
+#define GP_ATTN_PV16 0
+#endif
+#ifndef GP_ATTN_SKIP_IDLE
+#define GP_ATTN_SKIP_IDLE 1
+#endif
 #ifndef GP_ATTN_ONES_SPARSE
 #define GP_ATTN_ONES_SPARSE 1
 #endif
@@ -492,8 +495,32 @@ static_assert(kNWFast == 4 || kNWFast == 8 || kNWFast == 16, "GP_ATTN_NW must be
 #ifndef GP_ATTN_FP16_EXACT
 #define GP_ATTN_FP16_EXACT 1
 #endif
-// Measured lab variants of this kernel (the 16x16x32 P.V GP_ATTN_PV16, the 3-slot ring GP_ATTN_RING3) live
-// in tools/attn_lab/gp_attn_r3_lab.hip.
+// GP_ATTN_RING3 (lab; the bf16 fast kernel): a 3-slot K/V ring, tile t+2's LDS-DMA issued at tile t's
+// start and a counted vmcnt before each barrier that retires tile t+1 only, the V^T fragments read by
+// inline asm (the ds_read_tr builtin carries no alias information, so the compiler puts a vmcnt(0) -- a
+// wait for the in-flight staging of the next tile -- before the first V read of every tile) with explicit
+// lgkmcnt waits, and the softmax + P.V split by 32-key sub-tile.  Bit-identical outputs and the same time
+// (r03_s: 1.2811 vs 1.2816 ms per 70k launch, profiles/r03_s_ab_ring3.json): the staging latency is
+// already covered by the other waves of the SIMD, so the product keeps the 2-slot kernel.
+#ifndef GP_ATTN_RING3
+#define GP_ATTN_RING3 0
+#endif
+
+template <int OFF>
+GP_DEV s16x4 ds_read_tr_asm(uint32_t addr) {
+  s16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
+  return r;
+}
+// s_waitcnt with vmcnt(n) (n <= 15) and no lgkm / exp wait
+GP_DEV void wait_vm_only(int n) {
+  switch (n) {
+    case 0: __builtin_amdgcn_s_waitcnt(0x0f70); break;
+    case 1: __builtin_amdgcn_s_waitcnt(0x0f71); break;
+    case 2: __builtin_amdgcn_s_waitcnt(0x0f72); break;
+    default: __builtin_amdgcn_s_waitcnt(0x0f73); break;
+  }
+}
 
 template <int D, bool kPre, int MODE, bool kTab, int NW, bool kH>
 __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_idx) {
@@ -505,7 +532,11 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   constexpr int QB = NW * 32;                // query rows per workgroup
   constexpr int KT = 64;                     // keys per staged tile
   constexpr int KS = D / 16;                 // k-steps of Q.K^T
-  constexpr bool kOnes = (D % 32) != 0;      // spare d rows carry the row-sum ones
+  // GP_ATTN_PV16 (lab A/B of the verdict's 16x16x32 question): P.V of the fast kernel on
+  // v_mfma_f32_16x16x32 over the 3 real d-blocks (no padding; P regrouped by v_permlane16_swap), the
+  // row sum by VALU adds of the fp32 p
+  constexpr bool kPV16 = GP_ATTN_PV16 != 0 && MODE == kModeFast && D == 48;
+  constexpr bool kOnes = (D % 32) != 0 && !kPV16;   // spare d rows carry the row-sum ones
   constexpr bool kDMA = MODE != kModeGen;
   constexpr bool kZM = MODE == kModeFast && !kH;   // no max, no offset
   // fp16 fast mode: p = 2^(s - m0) with m0 the row max of tile 0 only (fp16's range ends at 2^16, so
@@ -524,12 +555,15 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   constexpr int LPT = (MODE == kModeGen) ? TOT / NT : 1;
   static_assert(MODE != kModeGen || TOT % NT == 0, "");
   constexpr float kThr = 8.0f;               // lazy-rescale threshold (log2 units)
-  constexpr int NBUF = 2;                    // K/V tile buffers (double-buffered)
+  constexpr bool kR3 = GP_ATTN_RING3 != 0 && MODE == kModeFast && !kH && !kPV16;
+  constexpr int NBUF = kR3 ? 3 : 2;          // K/V tile buffers (double-buffered, or the kR3 ring)
   __shared__ __attribute__((aligned(16))) char smem[NBUF * BUF];
   auto bufc = [&](auto bc) -> char* {        // tile buffer B (compile time)
     return smem + decltype(bc)::value * BUF;
   };
   using IB0 = std::integral_constant<int, 0>;
+  using IB1 = std::integral_constant<int, 1>;
+  using IB2 = std::integral_constant<int, 2>;
 
   // ---- work item (32-bit index math: items < 2^31, checked on the host)
   WorkItem wi;
@@ -687,23 +721,49 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   }
   float m_run = -INFINITY;   // running max, log2 domain, of query l32
   float lsum = 0.f;          // row sum (VALU path, D % 32 == 0 only)
-  f32x16 oacc[2];
+  f32x16 oacc[kPV16 ? 1 : 2];
 #pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
+  for (int mt = 0; mt < (kPV16 ? 1 : 2); ++mt)
 #pragma unroll
     for (int r = 0; r < 16; ++r) oacc[mt][r] = 0.f;
+  f32x4 o16[2][3];              // kPV16: O^T blocks [query half][d-block]
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+    for (int dt = 0; dt < 3; ++dt) o16[nb][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int ntiles = (c + KT - 1) / KT;
+  // kR3: LDS-DMA instructions this wave issues per tile (pieces w, w + NW, ... below kPieces)
+  int npw = 0;
+#pragma unroll
+  for (int sl = 0; sl < PPW; ++sl) npw += (__builtin_amdgcn_readfirstlane(w) + NW * sl < kPieces) ? 1 : 0;
   if (ntiles > 0) {
     load_tile(0, IB0());
     store_tile(0);
   }
+  if constexpr (kR3) {
+    if (ntiles > 1) load_tile(KT, IB1());
+    // tile 0 and the ones block landed (tile 1 stays in flight), then the workgroup barrier
+    wait_vm_only(ntiles > 1 ? npw : 0);
+    __builtin_amdgcn_s_waitcnt(0xc07f);      // lgkmcnt(0): the ones-block ds_writes
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  } else
   __syncthreads();
   // every vector load so far (Q fragments, tile 0) is complete here; saying so with a real
   // s_waitcnt (vmcnt 0) lets the compiler's wait insertion drop its "Q may still be in flight"
   // state at the loop head, which otherwise forces vmcnt(0) -- a wait on the next tile's
   // prefetch -- before the first MFMA of every tile
-  __builtin_amdgcn_s_waitcnt(0x0f70);
+  if constexpr (!kR3) __builtin_amdgcn_s_waitcnt(0x0f70);
+  // kR3: the lane part of the V^T fragment addresses (row & 3, the swizzle, the 8-byte column)
+  uint32_t vlane[2] = {0u, 0u};
+  if constexpr (kR3) {
+    const int row_l = 4 * (lane >> 5) + ((lane >> 2) & 3);
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+      vlane[mt] = (uint32_t)(row_l * VROWB + 32 * ((2 * mt + ((lane >> 4) & 1)) ^ (row_l & 3)) + 8 * (lane & 3));
+  }
 
   if constexpr (GP_ATTN_PRIO != 0 && NW >= 8) {
     if (__builtin_amdgcn_readfirstlane((int)threadIdx.x) >= NT / 2) __builtin_amdgcn_s_setprio(1);
@@ -716,7 +776,11 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   const bool wact = !GP_ATTN_SKIP_IDLE || __builtin_amdgcn_readfirstlane(q0 + w * 32) < rows_needed;
   auto tile_step = [&](int t, auto setc) {
     constexpr int SET = decltype(setc)::value;
-    if (t + 1 < ntiles) load_tile((t + 1) * KT, std::integral_constant<int, 1 - SET>());
+    if constexpr (kR3) {
+      if (t + 2 < ntiles) load_tile((t + 2) * KT, std::integral_constant<int, (SET + 2) % 3>());
+    } else {
+      if (t + 1 < ntiles) load_tile((t + 1) * KT, std::integral_constant<int, 1 - SET>());
+    }
     const int kv0 = t * KT;
     const char* Kb = kDMA ? (const char*)bufc(setc) : smem + (t & 1) * BUF;
     const char* Vb = Kb + KTILE;
@@ -770,7 +834,31 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
         mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
       }
       bf16x8 pf[2][2];
-      if constexpr (kPre) {
+      if constexpr (kR3) {
+        // per 32-key sub-tile u: V^T reads (asm), the sub-tile's 16 exp2, one lgkmcnt wait, 4 MFMAs
+        const uint32_t vbase = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const char*)Vb);
+        const uint32_t va0 = vbase + vlane[0], va1 = vbase + vlane[1];
+        auto sub = [&](auto uc) {
+          constexpr int u = decltype(uc)::value;
+          constexpr int R0 = 32 * u * VROWB, R1 = (32 * u + 16) * VROWB, H8 = 8 * VROWB;
+          s16x4 v00l = ds_read_tr_asm<R0>(va0), v00h = ds_read_tr_asm<R0 + H8>(va0);
+          s16x4 v01l = ds_read_tr_asm<R0>(va1), v01h = ds_read_tr_asm<R0 + H8>(va1);
+          s16x4 v10l = ds_read_tr_asm<R1>(va0), v10h = ds_read_tr_asm<R1 + H8>(va0);
+          s16x4 v11l = ds_read_tr_asm<R1>(va1), v11h = ds_read_tr_asm<R1 + H8>(va1);
+  #pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2)
+  #pragma unroll
+            for (int e = 0; e < 8; ++e) pf[u][s2][e] = f2e_slot<kH>(fast_exp2(sacc[u][8 * s2 + e]));
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v00l), "+v"(v00h), "+v"(v01l), "+v"(v01h), "+v"(v10l),
+                       "+v"(v10h), "+v"(v11l), "+v"(v11h));
+          oacc[0] = mfma_32x32x16<kH>(__builtin_bit_cast(bf16x8, __builtin_shufflevector(v00l, v00h, 0, 1, 2, 3, 4, 5, 6, 7)), pf[u][0], oacc[0]);
+          oacc[1] = mfma_32x32x16<kH>(__builtin_bit_cast(bf16x8, __builtin_shufflevector(v01l, v01h, 0, 1, 2, 3, 4, 5, 6, 7)), pf[u][0], oacc[1]);
+          oacc[0] = mfma_32x32x16<kH>(__builtin_bit_cast(bf16x8, __builtin_shufflevector(v10l, v10h, 0, 1, 2, 3, 4, 5, 6, 7)), pf[u][1], oacc[0]);
+          oacc[1] = mfma_32x32x16<kH>(__builtin_bit_cast(bf16x8, __builtin_shufflevector(v11l, v11h, 0, 1, 2, 3, 4, 5, 6, 7)), pf[u][1], oacc[1]);
+        };
+        sub(std::integral_constant<int, 0>());
+        sub(std::integral_constant<int, 1>());
+      } else if constexpr (kPre) {
         if constexpr (!kZM) {
           // scores are s*c - m_run; rescale only when a query's max moved up by > kThr
           // (tile 0: always, which sets m_run to that tile's exact max)
@@ -860,6 +948,33 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
       }
 
       // ---- O^T += V^T . P^T  (2 sub-tiles x 2 k-steps x 2 d-tiles)
+      if constexpr (kPV16) {
+        // pf[u][s] lane (h, j) holds keys 16s + 8(e/4) + 4h + e%4 of query j; one permlane16_swap per
+        // dword pair gives x = queries 0-15, y = queries 16-31, 16-lane group G = (s = G&1, h = G>>1):
+        // the 16x16x32 B operand (n = lane % 16, k-slots of group G)
+        typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+  #pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          u32x4v xa = __builtin_bit_cast(u32x4v, pf[u][0]), ya = __builtin_bit_cast(u32x4v, pf[u][1]);
+  #pragma unroll
+          for (int d = 0; d < 4; ++d) {
+            const auto r = __builtin_amdgcn_permlane16_swap(xa[d], ya[d], false, false);
+            xa[d] = r[0];
+            ya[d] = r[1];
+          }
+          const bf16x8 bq[2] = {__builtin_bit_cast(bf16x8, xa), __builtin_bit_cast(bf16x8, ya)};
+          const int row = 32 * u + 16 * ((lane >> 4) & 1) + 4 * (lane >> 5) + ((lane >> 2) & 3);
+  #pragma unroll
+          for (int dt = 0; dt < 3; ++dt) {
+            const char* p0 = Vb + row * VROWB + 32 * (dt ^ (row & 3)) + 8 * (lane & 3);
+            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
+            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0 + 8 * VROWB));
+            const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  #pragma unroll
+            for (int nb = 0; nb < 2; ++nb) o16[nb][dt] = mfma_16x16x32<kH>(vf, bq[nb], o16[nb][dt]);
+          }
+        }
+      } else if constexpr (!kR3)
   #pragma unroll
       for (int u = 0; u < 2; ++u)
   #pragma unroll
@@ -878,11 +993,24 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
         }
 
     }
+    if constexpr (kR3) {
+      wait_vm_only(t + 2 < ntiles ? npw : 0);   // tile t+1 landed (this wave's pieces); t+2 stays in flight
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      return;
+    }
     if (t + 1 < ntiles) store_tile((t + 1) & 1);
     if constexpr (kDMA) __builtin_amdgcn_s_waitcnt(0x0f70);   // this wave's DMA pieces landed
     __syncthreads();
   };
-  if constexpr (kDMA) {
+  if constexpr (kR3) {
+    for (int t = 0; t < ntiles; t += 3) {
+      tile_step(t, IB0());
+      if (t + 1 < ntiles) tile_step(t + 1, IB1());
+      if (t + 2 < ntiles) tile_step(t + 2, IB2());
+    }
+  } else if constexpr (kDMA) {
     for (int t = 0; t < ntiles; t += 2) {
       tile_step(t, std::integral_constant<int, 0>());
       if (t + 1 < ntiles) tile_step(t + 1, std::integral_constant<int, 1>());
@@ -918,7 +1046,23 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   }
   const float inv = so / l;
   const int i = q0 + w * 32 + l32;
-  if constexpr (GP_ATTN_WIDE_STORE != 0) {
+  if constexpr (kPV16) {
+    // lane (G = lane / 16, c = lane % 16) holds O^T rows 16dt + 4G + 0..3 of queries c and c + 16
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      const int qq = (lane & 15) + 16 * nb;
+      const float iv = __shfl(inv, qq, 64);
+      const int iq = q0 + w * 32 + qq;
+      if (iq < rows_needed && __shfl(fixrow ? 1 : 0, qq, 64)) {
+        uint16_t* orow = brr.o + (((int64_t)bn * g.m + iq) * a.H + hh) * (int64_t)D + 4 * (lane >> 4);
+#pragma unroll
+        for (int dt = 0; dt < 3; ++dt) {
+          float vv[4] = {o16[nb][dt][0] * iv, o16[nb][dt][1] * iv, o16[nb][dt][2] * iv, o16[nb][dt][3] * iv};
+          store_e<kH, 4>(orow + 16 * dt, vv);
+        }
+      }
+    }
+  } else if constexpr (GP_ATTN_WIDE_STORE != 0) {
     // lane (q, h) holds d = 8k + 4h .. +3 for the D/8 groups k.  For each pair of groups (k, k+1)
     // one permlane32_swap per dword gives lanes 0-31 d = 8k .. 8k+7 and lanes 32-63 d = 8k+8 .. 8k+15
     // (T21): one 16-byte store per pair.  The swap needs EXEC full: it runs before the row check.
@@ -965,10 +1109,10 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   }
 }
 
-// One work item per block (XCD-grouped order).  The fixup pass (kModeFix), product layout kFixItems = 4
-// (GP_ATTN_FIX_ITEMS): a block reads the lse of every needed row of its kFixItems consecutive items at
-// once (independent loads per lane), exits unless one holds the kLseRedo marker, and recomputes the
-// flagged items in turn; kFixItems = 1 (lab builds) is one item per block in item order.
+// One work item per block (XCD-grouped order).  The fixup pass (kModeFix) with kFixItems = 1: one item
+// per block in item order, each block reading its item's lse rows and exiting unless one holds the
+// kLseRedo marker; with kFixItems > 1 (lab) a block reads the lse of every needed row of kFixItems
+// consecutive items at once (16 independent loads per lane) and recomputes the flagged ones in turn.
 template <int D, bool kPre, int MODE, bool kTab = false, int NW = 4, bool kH = false>
 __global__ __launch_bounds__(NW * 64, 2) void dilated_attn32_kernel(const AttnArgs a) {
   if constexpr (MODE == kModeFix && kFixItems == 1) {

@@ -211,6 +211,13 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
   const int n_my = sid < n_dp ? (n_dp - 1 - sid) / G + 1 : 0;
   const bool tail = S > 1 && g.split && sid < (ntiles - n_dp) * S;
   if (n_my == 0 && !tail) return;
+#if GP_GEMM_DESYNC
+  // lab: the workgroups with one tile fewer than the busiest (idle in the last round anyway) start about
+  // half a tile late, so their epilogue stores fall between the others' bursts
+  if (n_my < (n_dp - 1) / G + 1 && !tail) {
+    for (int z = 0; z < (NK * GP_GEMM_DESYNC) / 8; ++z) __builtin_amdgcn_s_sleep(127);
+  }
+#endif
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const int wm = w >> 2, wn = w & 3;
@@ -480,6 +487,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
       // gives the other case.  (NT: non-temporal stores for wide, short-K outputs, see launch().)
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
+#ifdef GP_EXP_NOSTORE
+        if (g.ldc < 0)   // lab (tools/gemm_overhead_probe.py): never true -- the epilogue without its stores
+#endif
         __builtin_amdgcn_raw_buffer_store_b128(hh ? Y : X, rc, c_lane, mi * c_mi + hh * c_hi, NT ? 2 : 0);
         __builtin_amdgcn_sched_barrier(0);
         asm volatile("s_nop 1");
