@@ -422,6 +422,8 @@ def main():
             result["cpu_full_forwards"] = cpu_full_forwards([("C1", 1024), ("C2", 16384)], threads)
     if rank == 0:
         print(json.dumps(result), flush=True)
+    if monitor is not None:
+        monitor.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GP_ABI_VERSION 6
+#define GP_ABI_VERSION 7
 #define GP_EARG (-1)
 #define GP_MAX_BRANCHES 8
 #define GP_MAX_DESTS 8
@@ -58,6 +58,8 @@ int gp_coords_to_pos(const void* coords, int coords_is_f64, int64_t n_tiles, int
  *   x_out[b, 0, :]   = cls                                  (pos_embed row 0 is zero)
  *   x_out[b, 1+t, :] = xp[b, t, :] + [tab[(p-1) % G] | tab[(p-1) / G]],  p = pos[b, t]
  *   ln_out           = LayerNorm(x_out; ln_w, ln_b, eps)    (skipped if ln_w == NULL)
+ *   row_mean[row]    = mean of x_out's row                  (skipped if row_mean == NULL: the shift of
+ *                                                             the first gp_linear_resid)
  * xp: [B, N, E] act (patch projection incl. bias); tab: [G, E/2] fp32 one-axis sin-cos
  * table (fp64-built); cls: [E] fp32; x_out: [B, N+1, E] fp32; ln_out: [B, N+1, E] act.
  * cls == NULL: no CLS row (a sequence-parallel shard that does not hold token 0):
@@ -65,7 +67,7 @@ int gp_coords_to_pos(const void* coords, int coords_is_f64, int64_t n_tiles, int
  * E must be 64 * {12, 16, 24}. */
 int gp_posembed_cls_ln(const uint16_t* xp, const int64_t* pos, const float* tab, const float* cls,
                        int64_t B, int64_t N, int E, int G, const float* ln_w, const float* ln_b,
-                       float eps, float* x_out, uint16_t* ln_out, int fmt, void* stream);
+                       float eps, float* x_out, uint16_t* ln_out, float* row_mean, int fmt, void* stream);
 
 /* Dilated sparsify of one branch (DilatedAttention.gathering / dense_to_sparse,
  * torchscale/component/dilated_attention.py:16-31, 76-98), bit-exact:
@@ -232,10 +234,12 @@ int gp_gelu_layernorm(const uint16_t* h, const float* ln_w, const float* ln_b, f
 
 /* ---- Projection GEMMs on MFMAs (nn.Linear of torchscale/component/multihead_attention.py:43-48,
  * feedforward_network.py:131-142, gigapath/slide_encoder.py:47-51).  A [M, K] and W [N, K] are
- * K-contiguous act (row strides lda / ldw), C [M, N] act (ldc); fp32 accumulation.  N % 256 == 0,
- * N <= 3072, K in {768, 1536, 3072}; strides multiples of 8, operands 16-byte aligned.
+ * K-contiguous act (row strides lda / ldw), C [M, N] act (ldc); fp32 accumulation.  N % 256 == 0;
+ * strides multiples of 8, operands 16-byte aligned.
  * ws: device workspace of gp_gemm_workspace_bytes(M, N, K) bytes (fp32 partials of the last, split
- * round of tiles; the value depends on the current device's CU count); NULL disables the split. */
+ * round of tiles; the value depends on the current device's CU count); NULL disables the split.
+ * (ABI 7: N any multiple of 256, K in {768, 1024, 1536, 3072, 4096, 6144} -- the three registered
+ * archs, slide_encoder.py:261-270.) */
 int64_t gp_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K);
 
 /* C = A . W^T (+ bias).  bias: [N] fp32 or NULL. */
@@ -249,7 +253,7 @@ int gp_linear(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, co
  * and the LayerNorm statistics of h per 256-column group g:
  *   stats[g][m] = (mean, sum of squared deviations) of h[m, 256 g : 256 g + 256]   (fp32 pairs)
  * A: [M, K] act; W1: [F, K] act; b1: [F] fp32 or NULL; h: [M, F] act (ldh); stats: [F/256 + 1, M, 2]
- * fp32 (the last plane is gp_ffn_fc2_ln's).  F % 256 == 0, F <= 3072. */
+ * fp32 (the last plane is gp_ffn_fc2_ln's).  F % 256 == 0. */
 int gp_ffn_fc1_gelu(const uint16_t* A, int64_t lda, const uint16_t* W1, int64_t ldw, const float* b1,
                     uint16_t* h, int64_t ldh, float* stats, int64_t M, int64_t F, int64_t K, int fmt,
                     void* stream);
@@ -260,10 +264,52 @@ int gp_ffn_fc1_gelu(const uint16_t* A, int64_t lda, const uint16_t* W1, int64_t 
  * mean_m / rstd_m = LayerNorm statistics of row m merged from gp_ffn_fc1_gelu's stats (biased
  * variance, + eps; written into the stats' last plane first); W2g [N, F] act = W2 * gamma (each column
  * k scaled by the LN weight); c [N] fp32 = row sums of W2g (as rounded); d [N] fp32 = W2 . beta + b2.
- * N <= 1536. */
+ */
 int gp_ffn_fc2_ln(const uint16_t* h, int64_t ldh, const uint16_t* W2g, int64_t ldw, float* stats,
                   const float* c, const float* d, float eps, uint16_t* y, int64_t ldy, int64_t M, int64_t N,
                   int64_t F, void* ws, int64_t ws_bytes, int fmt, void* stream);
+
+/* ---- The residual stream inside the GEMMs (ABI 7).  EncoderLayer.forward's residual adds and the pre-LNs
+ * that follow them (encoder.py:141,147 -> final_layer_norm; :159 -> the next layer's self_attn_layer_norm
+ * at :126) without a separate pass: the producing GEMM (out-proj, fc2) adds its output into the fp32
+ * residual stream x and writes the next LayerNorm's input as
+ *   xb = act(gamma * (x - s))   (s [M] = a per-row shift: the row's mean of x BEFORE the add, so the 16-bit
+ *                                rounding sees a nearly centred row; gamma = that LayerNorm's weight)
+ * with (mean, M2) of x - s per 256-column group; the consuming GEMM (QKV, fc1) folds the LayerNorm:
+ *   LN(x) . W^T + b = rstd * (xb . W^T - mean' c) + d,  c = W . gamma (fp32), d = W . beta + b,
+ * mean' / rstd of x - s merged from the groups (the merge also writes s_out = s_in + mean' = the row's
+ * mean of x, the next producer's shift).  The reference rounds LN(x) to act before the GEMM; here
+ * gamma * (x - s) is rounded instead. */
+
+/* out-proj + residual (multihead_attention.py:48 + encoder.py:141,147):
+ *   x += A . W^T + bias  (fp32, in place; x [M, ldx]);  xb [M, ldxb] act, xstats [N/256, M, 2] fp32 as above.
+ * gamma == NULL: no xb / xstats (x only).  shift: [M] fp32. */
+int gp_linear_resid(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, const float* bias,
+                    float* x, int64_t ldx, const float* shift, const float* gamma, uint16_t* xb,
+                    int64_t ldxb, float* xstats, int64_t M, int64_t N, int64_t K, void* ws,
+                    int64_t ws_bytes, int fmt, void* stream);
+
+/* QKV with the pre-LN folded (encoder.py:126 + multihead_attention.py:43-45): merges stats planes
+ * 0 .. nst-1 ([nst + 1, M, 2] fp32, gp_linear_resid / gp_ffn_fc2_ln_resid's xstats) into plane nst
+ * (mean', rstd; s_out = s_in + mean' when s_out != NULL), then C = act(rstd (A . W^T - mean' c) + d). */
+int gp_linear_ln(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, float* stats, int nst,
+                 const float* c, const float* d, float eps, const float* s_in, float* s_out, uint16_t* C,
+                 int64_t ldc, int64_t M, int64_t N, int64_t K, void* ws, int64_t ws_bytes, int fmt,
+                 void* stream);
+
+/* fc1 + GELU with final_layer_norm folded (encoder.py:147-150 + feedforward_network.py:131-135): the fold
+ * of gp_linear_ln, then gp_ffn_fc1_gelu's GELU and hstats ([F/256 + 1, M, 2]).  No F limit. */
+int gp_ffn_fc1_gelu_ln(const uint16_t* A, int64_t lda, const uint16_t* W1, int64_t ldw, float* xstats,
+                       int nst, const float* c1, const float* d1, float eps, const float* s_in, float* s_out,
+                       uint16_t* h, int64_t ldh, float* hstats, int64_t M, int64_t F, int64_t K, int fmt,
+                       void* stream);
+
+/* fc2 with ffn_layernorm folded (gp_ffn_fc2_ln) + residual (encoder.py:157-159): x += fc2(LN(h)),
+ * xb / xstats for the next layer's pre-LN as gp_linear_resid (gamma == NULL: the last layer, x only). */
+int gp_ffn_fc2_ln_resid(const uint16_t* h, int64_t ldh, const uint16_t* W2g, int64_t ldw, float* hstats,
+                        const float* c, const float* d, float eps, float* x, int64_t ldx, const float* shift,
+                        const float* gamma, uint16_t* xb, int64_t ldxb, float* xstats, int64_t M, int64_t N,
+                        int64_t F, void* ws, int64_t ws_bytes, int fmt, void* stream);
 
 /* Plain fp32 LayerNorm over rows with a row stride (readout: encoder.py:387-388,
  * slide_encoder.py:213-221).  out: [rows, cols] fp32 contiguous.  cols = 64 * {12, 16, 24}. */

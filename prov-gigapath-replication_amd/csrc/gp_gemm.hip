@@ -1,801 +1,5 @@
-// The slide encoder's projection GEMMs on gfx950 MFMAs, with the FFN's row passes fused into them.
-//
-//   gp_linear        C = A . W^T (+ bias)                               nn.Linear
-//   gp_ffn_fc1_gelu  h = act(gelu(act(A . W1^T + b1))) + per-row LN statistics of h
-//                    (feedforward_network.py:131-135: fc1, gelu(x.float()).type_as(x))
-//   gp_ffn_fc2_ln    y = act(LayerNorm_F(h) . W2^T + b2) with the LN folded into the epilogue
-//                    (feedforward_network.py:136-142: ffn_layernorm, fc2)
-//
-// A [M, K] and W [N, K] are both K-contiguous 16-bit (bf16, or fp16 under the caller's fp16 autocast),
-// fp32 accumulation.  The FFN pair replaces hipBLASLt fc1 + gp_gelu_layernorm + hipBLASLt fc2: the
-// GELU+LN pass (one read and one write of the [M, F] activation) disappears.
-//
-// LN fold (fc2).  With per-row mean mu and rstd s of h, gamma/beta the ffn_layernorm affine:
-//   LN(h) . W2^T + b2 = s * (h . W2g^T - mu * c) + d,   W2g = W2 * gamma (column-scaled, act),
-//   c[n] = sum_k W2g[n, k] (of the rounded W2g),        d[n] = sum_k W2[n, k] beta[k] + b2[n]
-// -- packed once per weight version (runtime.PackedLayer).  The reference rounds LN(h) to act before
-// fc2; here the rounding sits on W2g instead (one act rounding per product term either way).
-//
-// Statistics.  fc1's epilogue writes, for every 256-column group g of h and every row m,
-// stats[g][m] = (mean, M2) of the 256 act-rounded GELU values; fc2 first merges the F/256 groups (Chan et
-// al.'s pairwise update, row_stats_kernel) into plane F/256: the row's mean and 1/sqrt(biased variance +
-// eps), as torch's LayerNorm computes them in fp32; its epilogue reads them from LDS, where an LDS-DMA
-// issued at the tile's start has put them.
-//
-// GEMM structure (cdna_hip_programming.md §5, "the 256² 8-phase template"):
-//   * 256 x 256 output tile per workgroup of 8 waves as 2 (M) x 4 (N); a wave owns 128 x 64 = 8 x 4
-//     v_mfma_f32_16x16x32 tiles (128 fp32 accumulators per lane); BK = 64;
-//   * LDS: two K-tile buffers (distinct __shared__ objects, so the compiler sees that a fragment read of
-//     one never aliases the LDS-DMA in flight into the other) of [A 256 x 64 | W 256 x 64], rows of
-//     128 B whose 16-byte chunk c sits at c ^ ((row >> 1) & 7): the 16 rows x 4 chunks of every
-//     ds_read_b128 lane group land on 16 distinct bank slots;
-//   * staging by LDS-DMA (buffer_load_dwordx4 ... lds, 1 KiB per wave-instruction, lane-linear; the
-//     swizzle lives in the per-lane SOURCE address), rows past M read as zero through the descriptor;
-//   * a K-tile = 4 phases, one C quadrant (4 m-frags x 2 n-frags x K 64 = 16 MFMAs) each; each phase is
-//     fragment reads + DMA issue | s_barrier | 16 MFMAs at s_setprio 1 | s_barrier, and waves 4-7 run
-//     one barrier behind waves 0-3: on each SIMD one wave's MFMAs overlap the other's reads and issue;
-//   * persistent: one workgroup per CU walks its tiles, the next tile's first K-tiles streaming in
-//     during the current tile's last phases; XCD-grouped tile order (one A row panel's N-tiles on one
-//     XCD's L2); the last partial round of tiles split in K when it is at most half full (fp32
-//     partials in the caller's workspace, summed by gemm_reduce_kernel with the same epilogue).
-#include <math.h>
-
-#include <type_traits>
-
-#include "gp_api.h"
-#include "gp_common.h"
-#include "gp_gelu_lut.h"
-
-namespace {
-
-constexpr int kBM = 256, kBN = 256, kBK = 64;
-constexpr int kThreads = 512;
-constexpr int kRowB = kBK * 2;                // 128-byte LDS rows
-constexpr int kOpT = 256 * kRowB;             // one operand's K-tile: 32 KiB
-constexpr int kHalf = 128 * kRowB;            // one operand half-tile: 16 KiB
-constexpr int kMaxN = 3072;                   // column parameters staged in LDS (fp32)
-
-enum { kEpiLinear = 0, kEpiGelu = 1, kEpiLnFold = 2 };
-
-typedef float f32x4v __attribute__((ext_vector_type(4)));
-typedef _Float16 f16x8g __attribute__((ext_vector_type(8)));
-
-__shared__ __attribute__((aligned(1024))) char g_buf0[2 * kOpT];   // K-tiles 0, 2, 4, ...
-__shared__ __attribute__((aligned(1024))) char g_buf1[2 * kOpT];   // K-tiles 1, 3, 5, ...
-template <int B>
-GP_DEV char* bufp() {
-  if constexpr (B == 0) return g_buf0;
-  else return g_buf1;
-}
-// column parameters: bias [N] (linear, gelu) or c [N] | d [N] (LN fold), fp32
-__shared__ __attribute__((aligned(16))) float g_colp[kMaxN];
-// epilogue row exchange: GELU statistics (sums, then M2) per (tile row, wave column) / LN-fold (mean, rstd)
-__shared__ __attribute__((aligned(16))) float g_rsum[kBM * 4];
-__shared__ __attribute__((aligned(16))) float g_rm2[kBM * 4];
-// LN fold: (mean, rstd) of the tile's 256 rows, LDS-DMA'd at the tile's start, two tiles in flight
-__shared__ __attribute__((aligned(1024))) float2 g_rowst[2][kBM];
-
-GP_DEV int xcd_remap(int b, int nwg) {
-  const int q = nwg / 8, r = nwg % 8, x = b % 8;
-  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
-}
-
-struct GemmArgs {
-  const uint16_t* A;
-  const uint16_t* W;
-  const float* colp0;   // bias (linear / gelu, may be null) or c (LN fold)
-  const float* colp1;   // d (LN fold)
-  uint16_t* C;
-  float* stats;         // gelu: written [N/256][M] float2; LN fold: (mean, rstd) [M] float2 (plane nst)
-  int64_t lda, ldw, ldc;
-  int M, N, K;
-  int nst;              // LN fold: statistics groups per row (F / 256)
-  float eps;
-  int n_dp;             // tiles run data-parallel
-  int split;            // 1: the remaining tiles are split in K (workspace ws)
-  float* ws;
-};
-
-template <int n>
-GP_DEV void wait_vmcnt() {
-  __builtin_amdgcn_s_waitcnt((n & 15) | ((n >> 4) << 14) | (0x7 << 4) | (0xf << 8));
-}
-
-// the wave's LDS writes visible to the workgroup, then a workgroup barrier (no wait on the LDS-DMA /
-// global loads in flight: an LDS-only release)
-GP_DEV void lds_barrier() {
-  __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-template <bool kH>
-GP_DEV float round_act(float v) { return e2f<kH>(f2e<kH>(v)); }
-
-// Exact-erf GELU (torch's F.gelu default), x Phi(x) = max(x, 0) - |x|/2 erfc(|x|/sqrt 2), with erfc from
-// Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7 exp(-z^2)-relative; the arithmetic of gp_norm.hip's
-// gelu_erf rearranged to 13 operations with one v_rcp and one v_exp: the 1/2 folded into the polynomial)
-GP_DEV float gelu_g(float x) {
-  const float z = fabsf(x) * 0.70710678118654752440f;
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
-  float p = fmaf(0.5307027145f, t, -0.7265760135f);
-  p = fmaf(p, t, 0.7107068705f);
-  p = fmaf(p, t, -0.142248368f);
-  p = fmaf(p, t, 0.127414796f);
-  p *= t;
-  const float e = __builtin_amdgcn_exp2f((x * -0.72134752044448170368f) * x);   // exp(-x^2 / 2)
-  return fmaf(-fabsf(x) * p, e, fmaxf(x, 0.f));
-}
-
-// bf16 GELU by table (gp_gelu_lut.h): h = bf16(gelu(float(x))) is a function of x's 16 bits, so the bf16
-// epilogue looks it up in LDS instead of evaluating gelu_g -- the reference's own fp32 GELU bit for bit
-// (the table is torch's F.gelu) and ~11 VALU per pair of elements (packed 16-bit index arithmetic, two
-// ds_read_u16) instead of ~26.  LDS copy: x = sign | m at byte 8192 sign + 2 (m - LO) -- the sign bit
-// shifted right by 2 is that offset in both 16-bit halves -- the table first in LDS (largest alignment),
-// so the ds_read address is the offset itself.  Halves outside [LO, HI] read a clamped entry and raise
-// `bad`; gelu_fix then applies the generator-checked rules to them.
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-constexpr int kLutNegB = 8192;
-static_assert(2 * kGeluLutN <= kLutNegB, "");
-__shared__ __attribute__((aligned(16384))) uint16_t g_lut[(kLutNegB + 2 * kGeluLutN) / 2];
-
-GP_DEV uint32_t gelu_lut_pair(uint32_t xp, bool& bad) {
-  const uint32_t m = xp & 0x7fff7fffu;
-  const u16x2 t = __builtin_bit_cast(u16x2, m) - (u16x2)kGeluLutLo;   // wraps for m < LO
-  const u16x2 tc = __builtin_elementwise_min(t, (u16x2)(kGeluLutN - 1));
-  bad |= __builtin_bit_cast(uint32_t, tc) != __builtin_bit_cast(uint32_t, t);
-  // byte offsets of both halves (2 tc < 2^12: no carry into the high half)
-  const uint32_t off = (__builtin_bit_cast(uint32_t, tc) << 1) | ((xp ^ m) >> 2);
-  const uint32_t lo = *reinterpret_cast<const uint16_t*>(reinterpret_cast<const char*>(g_lut) + (off & 0xffff));
-  const uint32_t hi = *reinterpret_cast<const uint16_t*>(reinterpret_cast<const char*>(g_lut) + (off >> 16));
-  return lo | (hi << 16);
-}
-
-// the halves of xp outside the table: |x| < 2^-16 -> x / 2 (half: the pair's fp32 accumulators halved and
-// rounded, = bf16(x) / 2 exactly), x > HI -> x (+inf from 2^127 up, as torch's formula overflows there),
-// x < -HI -> -0 (NaN for -inf / NaN)
-GP_DEV uint32_t gelu_fix(uint32_t xp, uint32_t hv, uint32_t half) {
-  uint32_t r = 0;
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const uint32_t b = (xp >> (16 * j)) & 0xffff, m = b & 0x7fff;
-    const uint32_t big = (b & 0x8000) ? (m >= 0x7f80 ? 0x7fc0u : 0x8000u) : (m - 0x7f00u < 0x80u ? 0x7f80u : b);
-    uint32_t v = (hv >> (16 * j)) & 0xffff;
-    v = m > (uint32_t)kGeluLutHi ? big : v;
-    v = m < (uint32_t)kGeluLutLo ? (half >> (16 * j)) & 0xffff : v;
-    r |= v << (16 * j);
-  }
-  return r;
-}
-
-// Chan merge of nst (mean, M2) groups of 256 values -> (mean, rstd) of the row (biased variance + eps)
-GP_DEV float2 merge_row_stats(const float2* st, int64_t stride, int nst, float eps) {
-  float msum = 0.f;
-  for (int g = 0; g < nst; ++g) msum += st[g * stride].x;
-  const float mean = msum / (float)nst;
-  float m2 = 0.f;
-  for (int g = 0; g < nst; ++g) {
-    const float2 p = st[g * stride];
-    const float dm = p.x - mean;
-    m2 += p.y + 256.f * dm * dm;
-  }
-  return make_float2(mean, rsqrtf(m2 / (float)(256 * nst) + eps));
-}
-
-// plane nst of the statistics = (mean, rstd) of each row, merged from planes 0 .. nst-1 (one thread per row)
-__global__ __launch_bounds__(256) void row_stats_kernel(float* stats, int M, int nst, float eps) {
-  const int row = (int)blockIdx.x * 256 + (int)threadIdx.x;
-  if (row >= M) return;
-  float2* st = reinterpret_cast<float2*>(stats);
-  st[(int64_t)nst * M + row] = merge_row_stats(st + row, M, nst, eps);
-}
-
-// NK = K / 64 as a template constant: the K loop is unrolled completely, so no loop header merges the
-// LDS-DMA state of two paths (hipcc's wait insertion then put a vmcnt(0) before every iteration's first
-// fragment read although the pending DMA targets the other buffer).
-//
-// Work: persistent, one workgroup per CU (G = grid).  Tiles [0, n_dp) run data-parallel: workgroup sid
-// takes sid, sid + G, ...  Tiles [n_dp, ntiles) -- the last, partial round -- are split S ways in K when
-// the host asks for it (n_dp a multiple of G, (ntiles - n_dp) * S <= G): unit u = sid takes tile
-// n_dp + u / S, K-tiles [(u % S) NK/S, +NK/S), and writes its fp32 partial tile to the workspace.
-template <int NK, int S, int EPI, bool kH, bool NT = false>
-__global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
-  static_assert(NK % 2 == 0 && NK >= 2 && (S == 1 || (NK % (2 * S) == 0)), "");
-  const int tiles_n = g.N / kBN;
-  const int ntiles = ((g.M + kBM - 1) / kBM) * tiles_n;
-  const int G = (int)gridDim.x;
-  const int sid = xcd_remap((int)blockIdx.x, G);
-  const int n_dp = g.n_dp;
-  const int n_my = sid < n_dp ? (n_dp - 1 - sid) / G + 1 : 0;
-  const bool tail = S > 1 && g.split && sid < (ntiles - n_dp) * S;
-  if (n_my == 0 && !tail) return;
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-  const int wm = w >> 2, wn = w & 3;
-
-  if constexpr (EPI == kEpiLnFold) {
-    for (int c = threadIdx.x; c < g.N; c += kThreads) {
-      g_colp[c] = g.colp0[c];
-      g_colp[g.N + c] = g.colp1[c];
-    }
-  } else {
-    if (g.colp0 != nullptr)
-      for (int c = threadIdx.x; c < g.N; c += kThreads) g_colp[c] = g.colp0[c];
-  }
-  if constexpr (EPI == kEpiGelu && !kH) {   // the GELU table (published by run_seq's first barrier)
-    static_assert(kGeluLutN % 2 == 0, "");
-    for (int i = threadIdx.x; i < kGeluLutN; i += kThreads) {   // dword i: entries 2i, 2i+1
-      const int half = i >= kGeluLutN / 2;
-      reinterpret_cast<uint32_t*>(g_lut)[i - half * (kGeluLutN / 2) + half * (kLutNegB / 4)] =
-          reinterpret_cast<const uint32_t*>(gp_gelu_lut_bf16)[i];
-    }
-  }
-
-  // buffer descriptors of tile T: A rows past M read as zero (record count ends at row M)
-  auto rsrc_a = [&](int T) {
-    const int m0 = (T / tiles_n) * kBM;
-    const int64_t a_bytes = (int64_t)(g.M - m0) * g.lda * 2;
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(g.A + (int64_t)m0 * g.lda), (short)0,
-                                             (int)(a_bytes < 0x7fffffff ? a_bytes : 0x7fffffff), 0x00020000);
-  };
-  auto rsrc_w = [&](int T) {
-    const int n0 = (T % tiles_n) * kBN;
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(g.W + (int64_t)n0 * g.ldw), (short)0,
-                                             (int)((int64_t)kBN * g.ldw * 2), 0x00020000);
-  };
-
-  // LDS-DMA: instruction j of wave w for half h covers rows h*128 + (2w + j)*8 .. +7; lane l writes row
-  // + l/8, physical chunk l%8, which holds logical chunk (l%8) ^ ((row >> 1) & 7) (the half's 128-row
-  // offset leaves that XOR unchanged: it rides in the scalar offset)
-  int voff[2][2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int r = (2 * w + j) * 8 + (lane >> 3);
-    const int c = (lane & 7) ^ ((r >> 1) & 7);
-    voff[0][j] = (int)((int64_t)r * g.lda * 2) + c * 16;
-    voff[1][j] = (int)((int64_t)r * g.ldw * 2) + c * 16;
-  }
-  int hoff[2] = {(int)(128 * g.lda * 2), (int)(128 * g.ldw * 2)};
-  auto issue = [&](auto opc, auto hc, auto bc, const __amdgpu_buffer_rsrc_t& rs, int kt) {
-    constexpr int OP = decltype(opc)::value, H = decltype(hc)::value, B = decltype(bc)::value;
-    char* dst = bufp<B>() + OP * kOpT + H * kHalf;
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + (2 * w + j) * 1024),
-                                               16, voff[OP][j], kt * kRowB + H * hoff[OP], 0, 0);
-  };
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-
-  // fragment reads: lane (r16 = lane & 15, q = lane >> 4) reads row R0 + r16, logical chunk 4 ks + q,
-  // physical (q ^ (r16 >> 1)) ^ 4 ks  (R0 a multiple of 16)
-  const int r16 = lane & 15, q = lane >> 4;
-  const int lo0 = r16 * kRowB + ((q ^ (r16 >> 1)) << 4);
-  const int lo1 = r16 * kRowB + (((q ^ (r16 >> 1)) ^ 4) << 4);
-  bf16x8 as[4][2], ws[2][2][2];     // one A m-half (8 frags), both W n-halves (16-bit patterns)
-  auto read_a = [&](auto bc, auto mqc) {
-    constexpr int B = decltype(bc)::value, MQ = decltype(mqc)::value;
-    const char* base = bufp<B>() + (wm * 128 + MQ * 64) * kRowB;
-#pragma unroll
-    for (int f = 0; f < 4; ++f) {
-      as[f][0] = *reinterpret_cast<const bf16x8*>(base + f * 16 * kRowB + lo0);
-      as[f][1] = *reinterpret_cast<const bf16x8*>(base + f * 16 * kRowB + lo1);
-    }
-  };
-  auto read_w = [&](auto bc, auto nqc) {
-    constexpr int B = decltype(bc)::value, NQ = decltype(nqc)::value;
-    const char* base = bufp<B>() + kOpT + (wn * 64 + NQ * 32) * kRowB;
-#pragma unroll
-    for (int f = 0; f < 2; ++f) {
-      ws[NQ][f][0] = *reinterpret_cast<const bf16x8*>(base + f * 16 * kRowB + lo0);
-      ws[NQ][f][1] = *reinterpret_cast<const bf16x8*>(base + f * 16 * kRowB + lo1);
-    }
-  };
-
-  f32x4v acc[8][4];
-  auto mfma = [](const bf16x8& a, const bf16x8& b, const f32x4v& c) -> f32x4v {
-    if constexpr (kH)
-      return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8g, a), __builtin_bit_cast(f16x8g, b), c,
-                                                    0, 0, 0);
-    else
-      return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-  };
-  auto quadrant = [&](auto mqc, auto nqc) {
-    constexpr int MQ = decltype(mqc)::value, NQ = decltype(nqc)::value;
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int f = 0; f < 4; ++f)
-#pragma unroll
-      for (int e = 0; e < 2; ++e)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-          acc[MQ * 4 + f][NQ * 2 + e] = mfma(ws[NQ][e][ks], as[f][ks], acc[MQ * 4 + f][NQ * 2 + e]);
-    __builtin_amdgcn_s_setprio(0);
-  };
-  auto sync = [&]() {
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  };
-
-  // Epilogue of tile T.  Lane (r16, q) of wave (wm, wn) holds, for m-frag mi and n-frag ni, row
-  // mw + 16 mi + r16 and columns nw + 16 ni + 4q .. +3 (v_mfma_f32_16x16x32 D layout with W as srcA).
-  // Stores are 16 bytes (T21 with v_permlane16_swap): for each n-frag pair (2p, 2p+1) one swap per dword
-  // gives lane groups q = 0 / 2 the 8 columns 8(q>>1) .. +7 of n-frag 2p and q = 1 / 3 those of n-frag
-  // 2p+1; through a per-wave buffer descriptor whose record count ends at row M (rows past it are
-  // dropped by the hardware), the row group in the scalar offset.
-  auto epilogue_tile = [&](int i_tile, int T) {
-    const int tm = T / tiles_n, tn = T % tiles_n;
-    const int m0 = tm * kBM;
-    const int mw = m0 + wm * 128, nw = tn * kBN + wn * 64;
-    float2 rs[8];                    // LN fold: (mean, rstd) of the lane's 8 rows
-    uint32_t hp[8][4][2];            // GELU: h as packed 16-bit pairs
-    if constexpr (EPI == kEpiLnFold) {   // landed during the K loop (init_tile's DMA, retired by wave 0's
-                                           // first counted wait, published by the barriers after it)
-#pragma unroll
-      for (int mi = 0; mi < 8; ++mi) rs[mi] = g_rowst[i_tile & 1][wm * 128 + mi * 16 + r16];
-    }
-    if constexpr (EPI == kEpiGelu) {
-      // GELU (the bias is the accumulators' initial value) and the row sums of h and h^2 over the lane's
-      // 16 columns, one m-frag at a time (the GELU temporaries of only one are live); h is kept as
-      // packed 16-bit pairs (64 registers: an m-frag's accumulators die as it is converted).  Per tile
-      // and row, M2 = sum h^2 - (sum h)^2 / 256 over 256 bounded activation values: the fp32
-      // cancellation is ~1e-7 * (1 + mean^2 / var), far below the act rounding of h itself.
-#pragma unroll
-      for (int mi = 0; mi < 8; ++mi) {
-        float s = 0.f, s2 = 0.f;
-        if constexpr (!kH) {   // bf16: table lookup, sums by v_dot2 (exact bf16 products, fp32 adds)
-          uint32_t xp[4][2];
-          bool bad = false;
-#pragma unroll
-          for (int ni = 0; ni < 4; ++ni)
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-              xp[ni][e] = pack2e<false>(acc[mi][ni][2 * e], acc[mi][ni][2 * e + 1]);
-              hp[mi][ni][e] = gelu_lut_pair(xp[ni][e], bad);
-            }
-          if (__builtin_amdgcn_ballot_w64(bad) != 0) {   // a |x| < 2^-16 or > 5.53 in this m-frag (rare)
-#pragma unroll
-            for (int ni = 0; ni < 4; ++ni)
-#pragma unroll
-              for (int e = 0; e < 2; ++e)
-                hp[mi][ni][e] = gelu_fix(xp[ni][e], hp[mi][ni][e],
-                                         pack2e<false>(acc[mi][ni][2 * e] * 0.5f, acc[mi][ni][2 * e + 1] * 0.5f));
-          }
-          typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
-          const bf16x2v one2 = __builtin_bit_cast(bf16x2v, 0x3f803f80u);
-#pragma unroll
-          for (int ni = 0; ni < 4; ++ni)
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-              const bf16x2v hv = __builtin_bit_cast(bf16x2v, hp[mi][ni][e]);
-              s = __builtin_amdgcn_fdot2_f32_bf16(hv, one2, s, false);
-              s2 = __builtin_amdgcn_fdot2_f32_bf16(hv, hv, s2, false);
-            }
-        } else {
-#pragma unroll
-          for (int ni = 0; ni < 4; ++ni) {
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-              const uint32_t xp = pack2e<kH>(acc[mi][ni][2 * e], acc[mi][ni][2 * e + 1]);
-              hp[mi][ni][e] = pack2e<kH>(gelu_g(e2f<kH>(xp)), gelu_g(e2f_hi<kH>(xp)));
-              const float h0 = e2f<kH>(hp[mi][ni][e]), h1 = e2f_hi<kH>(hp[mi][ni][e]);
-              s += h0 + h1;
-              s2 = fmaf(h0, h0, fmaf(h1, h1, s2));
-            }
-          }
-        }
-        s += __shfl_xor(s, 16, 64);
-        s2 += __shfl_xor(s2, 16, 64);
-        s += __shfl_xor(s, 32, 64);
-        s2 += __shfl_xor(s2, 32, 64);
-        if (q == 0) {
-          g_rsum[(wm * 128 + mi * 16 + r16) * 4 + wn] = s;
-          g_rm2[(wm * 128 + mi * 16 + r16) * 4 + wn] = s2;
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      lds_barrier();
-      if (threadIdx.x < kBM) {
-        const int row = m0 + (int)threadIdx.x;
-        if (row < g.M) {
-          const float4 s4 = *reinterpret_cast<const float4*>(g_rsum + threadIdx.x * 4);
-          const float4 q4 = *reinterpret_cast<const float4*>(g_rm2 + threadIdx.x * 4);
-          const float sum = (s4.x + s4.y) + (s4.z + s4.w), sq = (q4.x + q4.y) + (q4.z + q4.w);
-          const float mean = sum * (1.f / 256.f);
-          reinterpret_cast<float2*>(g.stats)[(int64_t)tn * g.M + row] = make_float2(mean, fmaxf(fmaf(-sum, mean, sq), 0.f));
-        }
-      }
-    } else if constexpr (EPI == kEpiLnFold) {   // s * (acc - mu c) + d
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni) {
-        const float4 c = *reinterpret_cast<const float4*>(g_colp + nw + ni * 16 + 4 * q);
-        const float4 d = *reinterpret_cast<const float4*>(g_colp + g.N + nw + ni * 16 + 4 * q);
-        const float cc[4] = {c.x, c.y, c.z, c.w}, dd[4] = {d.x, d.y, d.z, d.w};
-#pragma unroll
-        for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc[mi][ni][j] = fmaf(rs[mi].y, fmaf(-rs[mi].x, cc[j], acc[mi][ni][j]), dd[j]);
-      }
-    }
-    const int64_t c_rows = g.M - mw < 128 ? (g.M - mw > 0 ? g.M - mw : 0) : 128;
-    // (readfirstlane: wave-uniform values the compiler cannot prove uniform would put every store in a
-    // waterfall loop over the descriptor)
-    const uint64_t cp = reinterpret_cast<uint64_t>(g.C + (int64_t)mw * g.ldc + nw);
-    const uint64_t cpu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(cp >> 32)) << 32) |
-                         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)cp);
-    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<void*>(cpu), (short)0, __builtin_amdgcn_readfirstlane((int)(c_rows * g.ldc * 2)),
-        0x00020000);
-    // Full-line stores: after the v_permlane16_swap below, lane (r16, q) holds for m-frag mi two 16-byte
-    // column chunks of row r16 (V[0]: the wave's columns 0-31, V[1]: 32-63).  One DPP row_ror:8 per dword
-    // hands rows 8-15's V[0] to lanes 0-7 and rows 0-7's V[1] to lanes 8-15 of every 16-lane row, so each
-    // 16-byte store then writes 8 rows x the whole 128-byte line of the wave's 64 columns (8 lanes per
-    // row) instead of 16 rows x half lines -- half-line non-temporal writes cost 1.5x the bytes in HBM
-    // (PMC r03_z: QKV WRITE_SIZE 488 MB for a 322 MB output).
-    const int c_lane = (int)(((r16 & 7) * g.ldc + 16 * (q & 1) + 8 * (q >> 1) + 32 * (r16 >> 3)) * 2);
-    const int c_mi = (int)(16 * g.ldc * 2);
-    const int c_hi = (int)(8 * g.ldc * 2);
-    const bool lo8 = r16 < 8;
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi) {
-      typedef int i32x4 __attribute__((ext_vector_type(4)));
-      i32x4 V[2];
-#pragma unroll
-      for (int pr = 0; pr < 2; ++pr) {
-        uint32_t pk[2][2];
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const int ni = 2 * pr + e;
-          if constexpr (EPI == kEpiGelu) {
-            pk[e][0] = hp[mi][ni][0];
-            pk[e][1] = hp[mi][ni][1];
-          } else {
-            pk[e][0] = pack2e<kH>(acc[mi][ni][0], acc[mi][ni][1]);
-            pk[e][1] = pack2e<kH>(acc[mi][ni][2], acc[mi][ni][3]);
-          }
-        }
-#pragma unroll
-        for (int d = 0; d < 2; ++d) {
-          const auto r = __builtin_amdgcn_permlane16_swap(pk[0][d], pk[1][d], false, false);
-          pk[0][d] = r[0];
-          pk[1][d] = r[1];
-        }
-        V[pr] = i32x4{(int)pk[0][0], (int)pk[0][1], (int)pk[1][0], (int)pk[1][1]};
-      }
-      i32x4 X, Y;
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        const int r0 = __builtin_amdgcn_update_dpp(0, V[0][d], 0x128, 0xf, 0xf, false);   // row_ror:8
-        const int r1 = __builtin_amdgcn_update_dpp(0, V[1][d], 0x128, 0xf, 0xf, false);
-        X[d] = lo8 ? V[0][d] : r1;   // rows 0-7
-        Y[d] = lo8 ? r0 : V[1][d];   // rows 8-15
-      }
-      // Store-data hazard: hipcc spaces a VALU write of a store's data registers from a b128 store only
-      // when soffset is not an SGPR, yet on gfx950 the store can still read such a register after the
-      // next instruction has rewritten it (measured: the GELU epilogue's m-frag 1 store, 4 rows of every
-      // tile wrong, timing-dependent).  Two wait states after every store, as the model
-      // gives the other case.  (NT: non-temporal stores for wide, short-K outputs, see launch().)
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        __builtin_amdgcn_raw_buffer_store_b128(hh ? Y : X, rc, c_lane, mi * c_mi + hh * c_hi, NT ? 2 : 0);
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_nop 1");
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-  };
-  // the VMEM instructions EVERY wave issues in epilogue_tile: 8 m-frags x 2 stores (waves 0-3 of the GELU
-  // epilogue add a statistics store, wave 0 of the LN fold two LDS-DMA pieces in init_tile: a wait
-  // counted with the minimum is only stricter for them)
-  constexpr int kEpiVmem = 16;
-  // accumulators start at zero, or at the bias (linear, GELU): the epilogue then has no add
-  auto zero_acc = [&]() {
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = f32x4v{0.f, 0.f, 0.f, 0.f};
-  };
-  // (the column offset of a workgroup's tiles changes from tile to tile unless G % tiles_n == 0, so the
-  // bias is read per tile from LDS: 4 ds_read_b128 per lane)
-  auto init_tile = [&](int i_tile, int T) {
-    if constexpr (EPI == kEpiLnFold) {
-      zero_acc();
-      // (mean, rstd) of the tile's 256 rows -> g_rowst[i_tile & 1]: 2 KiB, two 1-KiB LDS-DMA pieces of
-      // wave 0 (lane l: rows 2l, 2l+1 of the piece); rows past M read as zero
-      if (w == 0) {
-        const int m0 = (T / tiles_n) * kBM;
-        const int64_t nb = (int64_t)(g.M - m0) * 8;
-        const __amdgpu_buffer_rsrc_t rs_ = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(reinterpret_cast<const float2*>(g.stats) + (int64_t)g.nst * g.M + m0), (short)0,
-            (int)(nb < 2048 ? nb : 2048), 0x00020000);
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(
-              rs_, (__attribute__((address_space(3))) void*)((char*)g_rowst[i_tile & 1] + j * 1024), 16, lane * 16,
-              j * 1024, 0, 0);
-      }
-    } else {
-      if (g.colp0 == nullptr) {
-        zero_acc();
-      } else {
-        const int nw = (T % tiles_n) * kBN + wn * 64;
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni) {
-          const float4 b = *reinterpret_cast<const float4*>(g_colp + nw + ni * 16 + 4 * q);
-#pragma unroll
-          for (int mi = 0; mi < 8; ++mi) acc[mi][ni] = f32x4v{b.x, b.y, b.z, b.w};
-        }
-      }
-    }
-  };
-  // fp32 partial of split unit u: [256][256] floats at ws + u * 65536, lane's 4 columns as one 16-B store
-  auto store_partial = [&](int u) {
-    float* base = g.ws + (int64_t)u * (kBM * kBN);
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni) {
-        const int row = wm * 128 + mi * 16 + r16, col = wn * 64 + ni * 16 + 4 * q;
-        *reinterpret_cast<f32x4v*>(base + row * kBN + col) = acc[mi][ni];
-      }
-  };
-
-  // One sequence of `count` tiles of nk K-tiles each (K-tiles kt0 .. kt0 + nk - 1), tile_of(i) giving
-  // the i-th; the DMA of tile i+1's first K-tiles runs during tile i's last phases.
-  auto run_seq = [&](auto nkc, int count, int kt0, auto&& tile_of, auto&& epilogue, auto&& init_acc) {
-    constexpr int nk = decltype(nkc)::value;
-    __amdgpu_buffer_rsrc_t ra = rsrc_a(tile_of(0)), rw = rsrc_w(tile_of(0));
-    bool has_next = false;
-    int i_cur = 0;
-    // stage half H of operand OP of the tile-local K-tile vv (vv >= nk: the next tile's K-tile vv - nk)
-    auto stage = [&](auto opc, auto hc, auto bc, int vv) {
-      constexpr int OP = decltype(opc)::value;
-      // (unconditional: past the last tile the descriptors still name the current one and the pieces
-      // re-load consumed K-tiles -- a DMA issued on one path only made hipcc put a vmcnt(0) before
-      // later LDS reads)
-      issue(opc, hc, bc, OP == 0 ? ra : rw, kt0 + (vv < nk ? vv : vv - nk));
-    };
-    // one K-tile v of the current output tile, in buffer B (v even: B = 0).  Phases (quadrant; fragments
-    // read; DMA issued): Q0 (m0, n0; A m-half 0 + W n-half 0; A half 0 of K-tile v+1), Q1 (m0, n1; W
-    // n-half 1; A half 1 of v+1), Q2 (m1, n1; A m-half 1; none), Q3 (m1, n0; none; both W halves of
-    // v+2).  A halves are last read in Q2, W halves in Q1, so every restage comes >= 2 phases after the
-    // last read of its buffer half; one counted vmcnt(4) in Q3 retires all of K-tile v+1, which is read
-    // one phase later (the weights of K-tile v+2 stay in flight: 4 phases of lead)
-    auto ktile = [&](auto bc, int v) {
-      constexpr int B = decltype(bc)::value;
-      using BN_ = std::integral_constant<int, 1 - B>;
-      const bool pre = v == 0;   // K-tile 1's A halves are already in flight (see the tile loop)
-      read_a(bc, I0());
-      read_w(bc, I0());
-      if (!pre) stage(I0(), I0(), BN_(), v + 1);   // (pre: compile-time after the unroll)
-      sync();
-      quadrant(I0(), I0());
-      sync();
-      read_w(bc, I1());
-      if (!pre) stage(I0(), I1(), BN_(), v + 1);
-      sync();
-      quadrant(I0(), I1());
-      sync();
-      read_a(bc, I1());
-      sync();
-      quadrant(I1(), I1());
-      sync();
-      if (v + 2 == nk) {   // every DMA of this tile is issued: switch to the next tile's (if any)
-        const int Tn = tile_of(has_next ? i_cur + 1 : i_cur);
-        ra = rsrc_a(Tn);
-        rw = rsrc_w(Tn);
-      }
-      stage(I1(), I0(), bc, v + 2);
-      stage(I1(), I1(), bc, v + 2);
-      // retire K-tile v+1 (the weights of v+2 stay in flight); at v = 0 K-tile 1's A halves are older
-      // than the previous tile's epilogue stores (or the prologue's stand-ins), which may stay in flight
-      if (pre) wait_vmcnt<4 + kEpiVmem>();
-      else wait_vmcnt<4>();
-      sync();
-      quadrant(I1(), I0());
-      sync();
-    };
-    // prologue: K-tile 0 whole, K-tile 1 whole, then kEpiVmem stores through an empty descriptor
-    // (dropped by the hardware) standing in for an epilogue's: every tile then starts in the same
-    // VMEM state, and K-tile 0's counted wait is one compile-time constant
-    issue(I0(), I0(), I0(), ra, kt0);
-    issue(I0(), I1(), I0(), ra, kt0);
-    issue(I1(), I0(), I0(), rw, kt0);
-    issue(I1(), I1(), I0(), rw, kt0);
-    issue(I1(), I0(), I1(), rw, kt0 + 1);
-    issue(I1(), I1(), I1(), rw, kt0 + 1);
-    issue(I0(), I0(), I1(), ra, kt0 + 1);
-    issue(I0(), I1(), I1(), ra, kt0 + 1);
-    {
-      const __amdgpu_buffer_rsrc_t none = __builtin_amdgcn_make_buffer_rsrc(g.ws, (short)0, 0, 0x00020000);
-#pragma unroll
-      for (int j = 0; j < kEpiVmem; ++j) __builtin_amdgcn_raw_buffer_store_b32(0, none, 0, 0, 0);
-    }
-    wait_vmcnt<8 + kEpiVmem>();     // K-tile 0 landed
-    lds_barrier();                  // (also publishes the column parameters)
-    for (int i = 0; i < count; ++i) {
-      has_next = i + 1 < count;
-      i_cur = i;
-      // opaque per tile: the DMA scalar offsets derived from these are then computed where they are used
-      // instead of being hoisted out of the tile loop (~100 loop-invariant SGPRs for K = 3072 -> spills)
-      asm volatile("" : "+s"(hoff[0]), "+s"(hoff[1]));
-      init_acc(i, tile_of(i));
-      if (wm == 1) sync();          // waves 4-7 one barrier behind
-#pragma unroll
-      for (int v = 0; v < nk; v += 2) {
-        ktile(I0(), v);
-        ktile(I1(), v + 1);
-      }
-      if (wm == 0) sync();          // realign
-      // The next tile's K-tile 1 A halves go out BEFORE this tile's stores.  vmcnt counts stores too and
-      // retires in order, so a wait for a load issued after the stores waits for the stores; issued
-      // before them, the next tile's first wait (K-tile 0's Q3) can leave the stores in flight, and they
-      // drain behind a whole K-tile of MFMAs instead of stalling it.  (Buffer 1's A halves were last read
-      // in this tile's last Q2; every wave is past its last MFMA here.)
-      issue(I0(), I0(), I1(), ra, kt0 + 1);
-      issue(I0(), I1(), I1(), ra, kt0 + 1);
-      epilogue(i);
-    }
-    wait_vmcnt<0>();   // no LDS-DMA in flight past the sequence (LDS reuse, hand-off)
-  };
-
-  if (n_my > 0)
-    run_seq(std::integral_constant<int, NK>(), n_my, 0, [&](int i) { return sid + i * G; },
-            [&](int i) { epilogue_tile(i, sid + i * G); }, [&](int i, int T) { init_tile(i, T); });
-  if constexpr (S > 1) {
-    if (tail) {
-      constexpr int NKS = NK / S;
-      if (n_my > 0) sync();         // every wave done reading the last data-parallel tile's buffers
-      const int T = n_dp + sid / S, part = sid % S;
-      run_seq(std::integral_constant<int, NKS>(), 1, part * NKS, [&](int) { return T; },
-              [&](int) { store_partial(sid); }, [&](int, int) { zero_acc(); });
-    }
-  }
-}
-
-// Split tail: sum of the S fp32 partials of each tail tile, then the linear or LN-fold epilogue -> act C.
-// One thread per 8 columns of a row (the GELU epilogue, whose statistics span the tile, is never split).
-template <int EPI, bool kH>
-__global__ __launch_bounds__(256) void gemm_reduce_kernel(const GemmArgs g, int S) {
-  static_assert(EPI != kEpiGelu, "");
-  const int tiles_n = g.N / kBN;
-  const int unit = blockIdx.x / (kBM * kBN / 8 / 256);          // tail tile ordinal
-  const int idx = (blockIdx.x % (kBM * kBN / 8 / 256)) * 256 + threadIdx.x;
-  const int row = idx / (kBN / 8), col = (idx % (kBN / 8)) * 8;
-  const int T = g.n_dp + unit;
-  const int m = (T / tiles_n) * kBM + row, n = (T % tiles_n) * kBN + col;
-  if (m >= g.M) return;
-  float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int s = 0; s < S; ++s) {
-    const float* p = g.ws + (int64_t)(unit * S + s) * (kBM * kBN) + row * kBN + col;
-    const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
-    v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
-  }
-  if constexpr (EPI == kEpiLinear) {
-    if (g.colp0 != nullptr)
-      for (int e = 0; e < 8; ++e) v[e] += g.colp0[n + e];
-  } else {
-    const float2 mr = reinterpret_cast<const float2*>(g.stats)[(int64_t)g.nst * g.M + m];
-    for (int e = 0; e < 8; ++e) v[e] = fmaf(mr.y, fmaf(-mr.x, g.colp0[n + e], v[e]), g.colp1[n + e]);
-  }
-  uint4 o;
-  o.x = pack2e<kH>(v[0], v[1]);
-  o.y = pack2e<kH>(v[2], v[3]);
-  o.z = pack2e<kH>(v[4], v[5]);
-  o.w = pack2e<kH>(v[6], v[7]);
-  *reinterpret_cast<uint4*>(g.C + (int64_t)m * g.ldc + n) = o;
-}
-
-// ----------------------------------------------------------------------------------------------------
-// host side
-int device_cus() {                 // per-device cache of the CU count (one persistent workgroup per CU)
-  static int cache[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (cache[dev] == 0) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-    cache[dev] = n;
-  }
-  return cache[dev];
-}
-
-struct Plan {
-  int G;          // persistent workgroups
-  int S;          // K split of the tail round (1: none)
-  int n_dp;       // data-parallel tiles
-  int64_t rem;    // tail tiles
-  int64_t ws_bytes;
-};
-
-// the last partial round split in K when it is at most half full (S = 4, or 2 for K = 768)
-Plan make_plan(int64_t M, int64_t N, int64_t K, bool allow_split) {
-  Plan p;
-  const int64_t tiles = ((M + kBM - 1) / kBM) * (N / kBN);
-  const int cus = device_cus();
-  p.G = (int)(tiles < cus ? tiles : cus);
-  p.S = 1;
-  p.n_dp = (int)tiles;
-  p.rem = 0;
-  p.ws_bytes = 0;
-  const int S = K == 768 ? 2 : 4;
-  const int64_t rem = tiles % p.G;
-  if (allow_split && tiles > p.G && rem > 0 && rem * S <= p.G && rem * 2 <= p.G) {
-    p.S = S;
-    p.n_dp = (int)(tiles - rem);
-    p.rem = rem;
-    p.ws_bytes = rem * S * kBM * kBN * (int64_t)sizeof(float);
-  }
-  return p;
-}
-
-int check_shapes(const char* who, const void* A, int64_t lda, const void* W, int64_t ldw, const void* C, int64_t ldc,
-                 int64_t M, int64_t N, int64_t K, int fmt) {
-  GP_REQUIRE(fmt == GP_FMT_BF16 || fmt == GP_FMT_F16, "%s: bad fmt %d", who, fmt);
-  GP_REQUIRE(A && W && C, "%s: null pointer", who);
-  GP_REQUIRE(M > 0 && M < (int64_t)0x7fffffff && N > 0 && K > 0, "%s: bad sizes", who);
-  GP_REQUIRE(N % kBN == 0 && N <= kMaxN, "%s: N=%lld must be a multiple of %d, at most %d", who, (long long)N, kBN,
-             kMaxN);
-  GP_REQUIRE(K == 768 || K == 1536 || K == 3072, "%s: K=%lld not instantiated (768 / 1536 / 3072)", who,
-             (long long)K);
-  GP_REQUIRE(lda >= K && ldw >= K && ldc >= N && lda % 8 == 0 && ldw % 8 == 0 && ldc % 8 == 0,
-             "%s: bad leading dimensions", who);
-  GP_REQUIRE(gp_aligned(A, 16) && gp_aligned(W, 16) && gp_aligned(C, 16), "%s: misaligned operand", who);
-  GP_REQUIRE((int64_t)kBM * lda * 2 < 0x7fffffff && (int64_t)kBN * ldw * 2 < 0x7fffffff &&
-                 (int64_t)128 * ldc * 2 < 0x7fffffff,
-             "%s: leading dimension too large for 32-bit tile offsets", who);
-  return 0;
-}
-
-template <int EPI, bool kH>
-int launch(GemmArgs g, const Plan& p, hipStream_t s) {
-  g.n_dp = p.n_dp;
-  g.split = p.S > 1;
-  // Output stores: every CU finishes a tile at about the same moment, so each round of tiles writes
-  // G x 128 KiB at once (a whole XCD's L2 per round).  For wide, short-K outputs (QKV 2304 x 768, fc1
-  // 3072 x 768) non-temporal stores drain that burst faster: -14 % per launch; for N = 768 or K = 3072
-  // they are 4-10 % slower (r03_w probe).
-#ifndef GP_NT_MIN_N
-#define GP_NT_MIN_N 2048   // (lab builds probe other thresholds)
-#endif
-  const bool nt = g.N >= GP_NT_MIN_N && g.K <= 1536;
-  const dim3 grid((unsigned)p.G), block(kThreads);
-  constexpr bool kSplit = EPI != kEpiGelu;   // (the GELU plan never splits)
-  auto go = [&](auto nkc, auto ntc) {
-    constexpr int NKc = decltype(nkc)::value;
-    constexpr bool NTc = decltype(ntc)::value;
-    if (kSplit && p.S > 1) gemm_kernel<NKc, kSplit ? (NKc == 12 ? 2 : 4) : 1, EPI, kH, NTc><<<grid, block, 0, s>>>(g);
-    else gemm_kernel<NKc, 1, EPI, kH, NTc><<<grid, block, 0, s>>>(g);
-  };
-  using F_ = std::false_type;
-  using T_ = std::true_type;
-  switch (g.K) {
-    case 768:
-      if constexpr (EPI != kEpiLnFold) {
-        if (nt) { go(std::integral_constant<int, 12>(), T_()); break; }
-      }
-      go(std::integral_constant<int, 12>(), F_());
-      break;
-    case 1536:
-      if constexpr (EPI != kEpiLnFold) {
-        if (nt) { go(std::integral_constant<int, 24>(), T_()); break; }
-      }
-      go(std::integral_constant<int, 24>(), F_());
-      break;
-    default:
-      go(std::integral_constant<int, 48>(), F_());
-      break;
-  }
-  if constexpr (EPI != kEpiGelu) {
-    if (p.S > 1) gemm_reduce_kernel<EPI, kH><<<(unsigned)(p.rem * (kBM * kBN / 8 / 256)), 256, 0, s>>>(g, p.S);
-  }
-  return 0;
-}
-
-}  // namespace
+// Plain projections (gp_linear) and the split-K workspace query; kernels in gp_gemm_impl.h.
+#include "gp_gemm_impl.h"
 
 extern "C" int64_t gp_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K) {
   if (M <= 0 || N <= 0 || K <= 0 || N % kBN) return 0;
@@ -816,48 +20,7 @@ extern "C" int gp_linear(const uint16_t* A, int64_t lda, const uint16_t* W, int6
   g.lda = lda; g.ldw = ldw; g.ldc = ldc;
   g.M = (int)M; g.N = (int)N; g.K = (int)K;
   g.ws = static_cast<float*>(ws);
-  if (fmt == GP_FMT_F16) launch<kEpiLinear, true>(g, p, gp_stream(stream));
-  else launch<kEpiLinear, false>(g, p, gp_stream(stream));
+  const int lrc = fmt == GP_FMT_F16 ? launch<kEpiLinear, true, kKE | kKF>(g, p, gp_stream(stream)) : launch<kEpiLinear, false, kKE | kKF>(g, p, gp_stream(stream));
+  if (lrc != 0) return lrc;
   return gp_check_launch("gp_linear");
-}
-
-extern "C" int gp_ffn_fc1_gelu(const uint16_t* A, int64_t lda, const uint16_t* W1, int64_t ldw, const float* b1,
-                               uint16_t* h, int64_t ldh, float* stats, int64_t M, int64_t F, int64_t K, int fmt,
-                               void* stream) {
-  if (int rc = check_shapes("gp_ffn_fc1_gelu", A, lda, W1, ldw, h, ldh, M, F, K, fmt)) return rc;
-  GP_REQUIRE(stats && gp_aligned(stats, 8), "gp_ffn_fc1_gelu: null or misaligned stats");
-  GP_REQUIRE(!b1 || gp_aligned(b1, 16), "gp_ffn_fc1_gelu: misaligned bias");
-  const Plan p = make_plan(M, F, K, false);
-  GemmArgs g = {};
-  g.A = A; g.W = W1; g.colp0 = b1; g.C = h; g.stats = stats;
-  g.lda = lda; g.ldw = ldw; g.ldc = ldh;
-  g.M = (int)M; g.N = (int)F; g.K = (int)K;
-  if (fmt == GP_FMT_F16) launch<kEpiGelu, true>(g, p, gp_stream(stream));
-  else launch<kEpiGelu, false>(g, p, gp_stream(stream));
-  return gp_check_launch("gp_ffn_fc1_gelu");
-}
-
-extern "C" int gp_ffn_fc2_ln(const uint16_t* h, int64_t ldh, const uint16_t* W2g, int64_t ldw, float* stats,
-                             const float* c, const float* d, float eps, uint16_t* y, int64_t ldy, int64_t M, int64_t N,
-                             int64_t F, void* ws, int64_t ws_bytes, int fmt, void* stream) {
-  if (int rc = check_shapes("gp_ffn_fc2_ln", h, ldh, W2g, ldw, y, ldy, M, N, F, fmt)) return rc;
-  GP_REQUIRE(stats && c && d && gp_aligned(stats, 8) && gp_aligned(c, 16) && gp_aligned(d, 16),
-             "gp_ffn_fc2_ln: null or misaligned stats / c / d");
-  GP_REQUIRE(F % kBN == 0 && 2 * N <= kMaxN, "gp_ffn_fc2_ln: F=%lld must be a multiple of 256, N=%lld at most %d",
-             (long long)F, (long long)N, kMaxN / 2);
-  const Plan p = make_plan(M, N, F, ws != nullptr);
-  GP_REQUIRE(p.ws_bytes <= ws_bytes, "gp_ffn_fc2_ln: workspace of %lld bytes, %lld needed", (long long)ws_bytes,
-             (long long)p.ws_bytes);
-  GP_REQUIRE(p.ws_bytes == 0 || gp_aligned(ws, 16), "gp_ffn_fc2_ln: misaligned workspace");
-  GemmArgs g = {};
-  g.A = h; g.W = W2g; g.colp0 = c; g.colp1 = d; g.C = y; g.stats = stats;
-  g.lda = ldh; g.ldw = ldw; g.ldc = ldy;
-  g.M = (int)M; g.N = (int)N; g.K = (int)F;
-  g.nst = (int)(F / kBN);
-  g.eps = eps;
-  g.ws = static_cast<float*>(ws);
-  row_stats_kernel<<<(unsigned)((M + 255) / 256), 256, 0, gp_stream(stream)>>>(g.stats, g.M, g.nst, eps);
-  if (fmt == GP_FMT_F16) launch<kEpiLnFold, true>(g, p, gp_stream(stream));
-  else launch<kEpiLnFold, false>(g, p, gp_stream(stream));
-  return gp_check_launch("gp_ffn_fc2_ln");
 }

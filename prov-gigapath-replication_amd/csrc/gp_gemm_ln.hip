@@ -1,0 +1,48 @@
+// GEMMs with a LayerNorm folded into the epilogue (QKV after the residual, fc2); kernels in gp_gemm_impl.h.
+#include "gp_gemm_impl.h"
+
+extern "C" int gp_linear_ln(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, float* stats, int nst,
+                            const float* c, const float* d, float eps, const float* s_in, float* s_out, uint16_t* C,
+                            int64_t ldc, int64_t M, int64_t N, int64_t K, void* ws, int64_t ws_bytes, int fmt,
+                            void* stream) {
+  if (int rc = check_shapes("gp_linear_ln", A, lda, W, ldw, C, ldc, M, N, K, fmt)) return rc;
+  if (int rc = check_fold("gp_linear_ln", stats, nst, c, d, N)) return rc;
+  const Plan p = make_plan(M, N, K, ws != nullptr);
+  GP_REQUIRE(p.ws_bytes <= ws_bytes, "gp_linear_ln: workspace of %lld bytes, %lld needed", (long long)ws_bytes,
+             (long long)p.ws_bytes);
+  GP_REQUIRE(p.ws_bytes == 0 || gp_aligned(ws, 16), "gp_linear_ln: misaligned workspace");
+  GemmArgs g = {};
+  g.A = A; g.W = W; g.colp0 = c; g.colp1 = d; g.C = C; g.stats = stats;
+  g.lda = lda; g.ldw = ldw; g.ldc = ldc;
+  g.M = (int)M; g.N = (int)N; g.K = (int)K;
+  g.nst = nst;
+  g.eps = eps;
+  g.ws = static_cast<float*>(ws);
+  launch_row_stats(stats, M, nst, eps, s_in, s_out, gp_stream(stream));
+  const int lrc = fmt == GP_FMT_F16 ? launch<kEpiLnFold, true, kKE | kKF>(g, p, gp_stream(stream)) : launch<kEpiLnFold, false, kKE | kKF>(g, p, gp_stream(stream));
+  if (lrc != 0) return lrc;
+  return gp_check_launch("gp_linear_ln");
+}
+
+extern "C" int gp_ffn_fc2_ln(const uint16_t* h, int64_t ldh, const uint16_t* W2g, int64_t ldw, float* stats,
+                             const float* c, const float* d, float eps, uint16_t* y, int64_t ldy, int64_t M, int64_t N,
+                             int64_t F, void* ws, int64_t ws_bytes, int fmt, void* stream) {
+  if (int rc = check_shapes("gp_ffn_fc2_ln", h, ldh, W2g, ldw, y, ldy, M, N, F, fmt)) return rc;
+  GP_REQUIRE(F % kBN == 0, "gp_ffn_fc2_ln: F=%lld must be a multiple of 256", (long long)F);
+  if (int rc = check_fold("gp_ffn_fc2_ln", stats, F / kBN, c, d, N)) return rc;
+  const Plan p = make_plan(M, N, F, ws != nullptr);
+  GP_REQUIRE(p.ws_bytes <= ws_bytes, "gp_ffn_fc2_ln: workspace of %lld bytes, %lld needed", (long long)ws_bytes,
+             (long long)p.ws_bytes);
+  GP_REQUIRE(p.ws_bytes == 0 || gp_aligned(ws, 16), "gp_ffn_fc2_ln: misaligned workspace");
+  GemmArgs g = {};
+  g.A = h; g.W = W2g; g.colp0 = c; g.colp1 = d; g.C = y; g.stats = stats;
+  g.lda = ldh; g.ldw = ldw; g.ldc = ldy;
+  g.M = (int)M; g.N = (int)N; g.K = (int)F;
+  g.nst = (int)(F / kBN);
+  g.eps = eps;
+  g.ws = static_cast<float*>(ws);
+  launch_row_stats(g.stats, M, g.nst, eps, nullptr, nullptr, gp_stream(stream));
+  const int lrc = fmt == GP_FMT_F16 ? launch<kEpiLnFold, true, kKE | kKF>(g, p, gp_stream(stream)) : launch<kEpiLnFold, false, kKE | kKF>(g, p, gp_stream(stream));
+  if (lrc != 0) return lrc;
+  return gp_check_launch("gp_ffn_fc2_ln");
+}

@@ -1,0 +1,50 @@
+// GEMMs that update the fp32 residual stream (out-proj, fc2); kernels in gp_gemm_impl.h.
+#include "gp_gemm_impl.h"
+
+extern "C" int gp_linear_resid(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, const float* bias,
+                               float* x, int64_t ldx, const float* shift, const float* gamma, uint16_t* xb,
+                               int64_t ldxb, float* xstats, int64_t M, int64_t N, int64_t K, void* ws,
+                               int64_t ws_bytes, int fmt, void* stream) {
+  if (int rc = check_shapes("gp_linear_resid", A, lda, W, ldw, x, ldx, M, N, K, fmt)) return rc;
+  if (int rc = check_resid("gp_linear_resid", x, ldx, shift, gamma, xb, ldxb, xstats, N)) return rc;
+  GP_REQUIRE(!bias || gp_aligned(bias, 16), "gp_linear_resid: misaligned bias");
+  const Plan p = make_plan(M, N, K, ws != nullptr);
+  GP_REQUIRE(p.ws_bytes <= ws_bytes, "gp_linear_resid: workspace of %lld bytes, %lld needed", (long long)ws_bytes,
+             (long long)p.ws_bytes);
+  GP_REQUIRE(p.ws_bytes == 0 || gp_aligned(ws, 16), "gp_linear_resid: misaligned workspace");
+  GemmArgs g = {};
+  g.A = A; g.W = W; g.colp0 = bias; g.colp1 = gamma;
+  g.C = gamma ? xb : nullptr; g.ostats = xstats; g.x = x; g.shift = shift;
+  g.lda = lda; g.ldw = ldw; g.ldc = gamma ? ldxb : 8; g.ldx = ldx;
+  g.M = (int)M; g.N = (int)N; g.K = (int)K;
+  g.ws = static_cast<float*>(ws);
+  const int lrc = fmt == GP_FMT_F16 ? launch<kEpiResid, true, kKE>(g, p, gp_stream(stream)) : launch<kEpiResid, false, kKE>(g, p, gp_stream(stream));
+  if (lrc != 0) return lrc;
+  return gp_check_launch("gp_linear_resid");
+}
+
+extern "C" int gp_ffn_fc2_ln_resid(const uint16_t* h, int64_t ldh, const uint16_t* W2g, int64_t ldw, float* hstats,
+                                   const float* c, const float* d, float eps, float* x, int64_t ldx,
+                                   const float* shift, const float* gamma, uint16_t* xb, int64_t ldxb, float* xstats,
+                                   int64_t M, int64_t N, int64_t F, void* ws, int64_t ws_bytes, int fmt,
+                                   void* stream) {
+  if (int rc = check_shapes("gp_ffn_fc2_ln_resid", h, ldh, W2g, ldw, x, ldx, M, N, F, fmt)) return rc;
+  if (int rc = check_fold("gp_ffn_fc2_ln_resid", hstats, F / kBN, c, d, N)) return rc;
+  if (int rc = check_resid("gp_ffn_fc2_ln_resid", x, ldx, shift, gamma, xb, ldxb, xstats, N)) return rc;
+  const Plan p = make_plan(M, N, F, ws != nullptr);
+  GP_REQUIRE(p.ws_bytes <= ws_bytes, "gp_ffn_fc2_ln_resid: workspace of %lld bytes, %lld needed",
+             (long long)ws_bytes, (long long)p.ws_bytes);
+  GP_REQUIRE(p.ws_bytes == 0 || gp_aligned(ws, 16), "gp_ffn_fc2_ln_resid: misaligned workspace");
+  GemmArgs g = {};
+  g.A = h; g.W = W2g; g.colp0 = c; g.colp1 = d; g.colp2 = gamma;
+  g.C = gamma ? xb : nullptr; g.stats = hstats; g.ostats = xstats; g.x = x; g.shift = shift;
+  g.lda = ldh; g.ldw = ldw; g.ldc = gamma ? ldxb : 8; g.ldx = ldx;
+  g.M = (int)M; g.N = (int)N; g.K = (int)F;
+  g.nst = (int)(F / kBN);
+  g.eps = eps;
+  g.ws = static_cast<float*>(ws);
+  launch_row_stats(hstats, M, g.nst, eps, nullptr, nullptr, gp_stream(stream));
+  const int lrc = fmt == GP_FMT_F16 ? launch<kEpiLnFoldResid, true, kKF>(g, p, gp_stream(stream)) : launch<kEpiLnFoldResid, false, kKF>(g, p, gp_stream(stream));
+  if (lrc != 0) return lrc;
+  return gp_check_launch("gp_ffn_fc2_ln_resid");
+}

@@ -54,7 +54,8 @@ template <int EPL, bool kH>
 __global__ __launch_bounds__(256) void posembed_cls_ln_kernel(
     const uint16_t* __restrict__ xp, const int64_t* __restrict__ pos, const float* __restrict__ tab,
     const float* __restrict__ cls, int64_t B, int64_t N, int E, int G, const float* __restrict__ ln_w,
-    const float* __restrict__ ln_b, float eps, float* __restrict__ x_out, uint16_t* __restrict__ ln_out) {
+    const float* __restrict__ ln_b, float eps, float* __restrict__ x_out, uint16_t* __restrict__ ln_out,
+    float* __restrict__ row_mean) {
   const int lane = threadIdx.x & 63;
   const int half = E / 2;
   float wv[EPL], bv[EPL];
@@ -89,6 +90,13 @@ __global__ __launch_bounds__(256) void posembed_cls_ln_kernel(
       }
     }
     st_x4_f32<EPL>(x_out + row * E, lane, v);
+    if (row_mean != nullptr) {   // the first residual epilogue's row shift (gp_linear_resid)
+      float sm = 0.f;
+#pragma unroll
+      for (int i = 0; i < EPL; ++i) sm += v[i];
+      sm = wave_sum(sm) / (float)E;
+      if (lane == 0) row_mean[row] = sm;
+    }
     if (ln_w != nullptr) {
       wave_layernorm_regs<EPL>(v, E, wv, bv, eps);
       st_x4_e<kH, EPL>(ln_out + row * E, lane, v);
@@ -462,7 +470,8 @@ static bool epl_ok(int cols) {
 
 extern "C" int gp_posembed_cls_ln(const uint16_t* xp, const int64_t* pos, const float* tab, const float* cls,
                                   int64_t B, int64_t N, int E, int G, const float* ln_w, const float* ln_b,
-                                  float eps, float* x_out, uint16_t* ln_out, int fmt, void* stream) {
+                                  float eps, float* x_out, uint16_t* ln_out, float* row_mean, int fmt,
+                                  void* stream) {
   GP_REQUIRE(fmt == GP_FMT_BF16 || fmt == GP_FMT_F16, "gp_posembed_cls_ln: bad fmt %d", fmt);
   GP_REQUIRE(epl_ok(E), "gp_posembed_cls_ln: E=%d unsupported (64*{12,16,24})", E);
   GP_REQUIRE(B > 0 && N >= 0 && G > 0, "gp_posembed_cls_ln: bad sizes");
@@ -471,7 +480,7 @@ extern "C" int gp_posembed_cls_ln(const uint16_t* xp, const int64_t* pos, const 
   const int64_t rows = B * (N + (cls != nullptr));
   if (rows == 0) return 0;
   hipStream_t s = gp_stream(stream);
-#define GP_POSEMB(EPL, KH) posembed_cls_ln_kernel<EPL, KH><<<row_grid(rows), 256, 0, s>>>(xp, pos, tab, cls, B, N, E, G, ln_w, ln_b, eps, x_out, ln_out)
+#define GP_POSEMB(EPL, KH) posembed_cls_ln_kernel<EPL, KH><<<row_grid(rows), 256, 0, s>>>(xp, pos, tab, cls, B, N, E, G, ln_w, ln_b, eps, x_out, ln_out, row_mean)
   switch (E / 64) {
     case 12: GP_FMT_DISPATCH(fmt, GP_POSEMB(12, true), GP_POSEMB(12, false)); break;
     case 16: GP_FMT_DISPATCH(fmt, GP_POSEMB(16, true), GP_POSEMB(16, false)); break;

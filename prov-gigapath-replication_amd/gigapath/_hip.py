@@ -15,7 +15,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_lib", "libgigapath_hip.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 MAX_BRANCHES = 8
 MAX_DESTS = 8
 
@@ -37,8 +37,8 @@ SIGNATURES = {
     "gp_abi_version": [],
     "gp_last_error_string": [],
     "gp_coords_to_pos": [c_vp, c_i32, c_i64, c_i32, c_f64, c_vp, c_vp, c_vp],
-    "gp_posembed_cls_ln": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_f32, c_vp, c_vp, c_i32,
-                           c_vp],
+    "gp_posembed_cls_ln": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp,
+                           c_i32, c_vp],
     "gp_dilated_gather": [c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp],
     "gp_dilated_attn_fwd": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp,
                             c_f32, c_i32, c_i32, c_vp],
@@ -67,6 +67,14 @@ SIGNATURES = {
     "gp_ffn_fc1_gelu": [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_i32, c_vp],
     "gp_ffn_fc2_ln": [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_f32, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64,
                       c_i32, c_vp],
+    "gp_linear_resid": [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i64,
+                        c_vp, c_i64, c_i32, c_vp],
+    "gp_linear_ln": [c_vp, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64,
+                     c_i64, c_vp, c_i64, c_i32, c_vp],
+    "gp_ffn_fc1_gelu_ln": [c_vp, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp, c_i64, c_vp,
+                           c_i64, c_i64, c_i64, c_i32, c_vp],
+    "gp_ffn_fc2_ln_resid": [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_f32, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64,
+                            c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i32, c_vp],
 }
 _RESTYPES = {"gp_last_error_string": ctypes.c_char_p, "gp_varlen_plan_bytes": c_i64, "gp_gemm_workspace_bytes": c_i64}
 
@@ -168,7 +176,8 @@ def coords_to_pos(coords: torch.Tensor, grid: int, tile_size: float, pos_out: to
                                 _ptr(pos_out), _ptr(err_count), _stream()), "gp_coords_to_pos")
 
 
-def posembed_cls_ln(xp, pos, tab, cls, B, N, E, G, ln_w, ln_b, eps, x_out, ln_out):
+def posembed_cls_ln(xp, pos, tab, cls, B, N, E, G, ln_w, ln_b, eps, x_out, ln_out, row_mean=None):
+    """row_mean ([rows] fp32 or None): each x_out row's mean (the first residual epilogue's shift)."""
     lib = load_library()
     fmt = fmt_of(xp.dtype)
     _dev(xp, name="xp"); _dev(pos, torch.int64, "pos"); _dev(tab, torch.float32, "tab")
@@ -177,8 +186,13 @@ def posembed_cls_ln(xp, pos, tab, cls, B, N, E, G, ln_w, ln_b, eps, x_out, ln_ou
     _dev(x_out, torch.float32, "x_out")
     if ln_out is not None:
         _dev(ln_out, xp.dtype, "ln_out")
+    if row_mean is not None:
+        _dev(row_mean, torch.float32, "row_mean")
+        if row_mean.numel() < B * (N + (cls is not None)):
+            raise ValueError("posembed_cls_ln: row_mean holds fewer than the output rows")
     _check(lib.gp_posembed_cls_ln(_ptr(xp), _ptr(pos), _ptr(tab), _ptr(cls), B, N, E, G, _ptr(ln_w), _ptr(ln_b),
-                                  eps, _ptr(x_out), _ptr(ln_out), fmt, _stream()), "gp_posembed_cls_ln")
+                                  eps, _ptr(x_out), _ptr(ln_out), _ptr(row_mean), fmt, _stream()),
+           "gp_posembed_cls_ln")
 
 
 def dilated_gather(src, row_stride, col_off, B, L, H, D, sl, r, dst):
@@ -396,12 +410,15 @@ def branch_merge_ln_varlen(plan: VarlenPlan, ln_w, ln_b, eps, out):
 # ------------------------------------------------------------------------------------------
 # projection GEMMs (include/gigapath_hip.h "Projection GEMMs on MFMAs")
 # ------------------------------------------------------------------------------------------
-GEMM_K = (768, 1536, 3072)
+GEMM_K_E = (768, 1024, 1536)        # K = E of the three registered archs (QKV, out-proj, fc1; patch 1536)
+GEMM_K_F = (3072, 4096, 6144)       # K = F = 4E (fc2)
+GEMM_K = GEMM_K_E + GEMM_K_F
 
 
 def gemm_supported(N: int, K: int) -> bool:
-    """Shapes the MFMA GEMM kernels are instantiated for (N a multiple of 256 up to 3072)."""
-    return N % 256 == 0 and 0 < N <= 3072 and K in GEMM_K
+    """Shapes the MFMA GEMM kernels are instantiated for (N a multiple of 256, K = E or 4E of a registered arch;
+    gp_linear / gp_linear_ln cover both, the residual / fc1 epilogues K = E, the fc2 epilogues K = 4E)."""
+    return N % 256 == 0 and N > 0 and K in GEMM_K
 
 
 def gemm_workspace_bytes(M: int, N: int, K: int) -> int:
@@ -465,3 +482,97 @@ def ffn_fc2_ln(h, w2g, stats, c, d, eps, y, ws=None):
     wp, wb = _ws(ws)
     _check(lib.gp_ffn_fc2_ln(_ptr(h), h.stride(0), _ptr(w2g), w2g.stride(0), _ptr(stats), _ptr(c), _ptr(d), float(eps),
                              _ptr(y), y.stride(0), M, N, F, wp, wb, fmt, _stream()), "gp_ffn_fc2_ln")
+
+
+# ------------------------------------------------------------------------------------------
+# the residual stream inside the GEMMs (include/gigapath_hip.h, ABI 7)
+# ------------------------------------------------------------------------------------------
+def _f32_vec(t, n, name):
+    _dev(t, torch.float32, name)
+    if t.numel() < n:
+        raise ValueError("%s must hold %d floats" % (name, n))
+    return t
+
+
+def linear_resid(a, w, bias, x, shift, gamma, xb, xstats, ws=None):
+    """x += a . w^T + bias (fp32 x [M, N], in place); with gamma: xb = act(gamma * (x - shift)) [M, N] and
+    xstats [N/256 (+1), M, 2] (mean, M2) of x - shift per 256-column group.  gamma None: x only."""
+    lib = load_library()
+    fmt = fmt_of(a.dtype)
+    _rows(a, "a"); _rows(w, "w"); _rows(x, "x")
+    M, K, N = a.shape[0], a.shape[1], w.shape[0]
+    if w.dtype != a.dtype or x.dtype != torch.float32 or x.shape[0] < M or x.shape[1] < N:
+        raise TypeError("linear_resid: a / w share one 16-bit dtype; x is fp32 [M, N]")
+    if bias is not None:
+        _f32_vec(bias, N, "bias")
+    if gamma is not None:
+        _f32_vec(gamma, N, "gamma"); _f32_vec(shift, M, "shift"); _f32_vec(xstats, N // 256 * M * 2, "xstats")
+        _rows(xb, "xb")
+        if xb.dtype != a.dtype:
+            raise TypeError("linear_resid: xb must be in a's 16-bit dtype")
+    wp, wb = _ws(ws)
+    _check(lib.gp_linear_resid(_ptr(a), a.stride(0), _ptr(w), w.stride(0), _ptr(bias), _ptr(x), x.stride(0),
+                               _ptr(shift if gamma is not None else None), _ptr(gamma),
+                               _ptr(xb if gamma is not None else None), xb.stride(0) if gamma is not None else 0,
+                               _ptr(xstats if gamma is not None else None), M, N, K, wp, wb, fmt, _stream()),
+           "gp_linear_resid")
+
+
+def linear_ln(a, w, stats, nst, c, d, eps, s_in, s_out, out, ws=None):
+    """out = act(LN(x) . w^T + b) through the fold: a = xb = act(gamma * (x - s_in)), stats planes 0 .. nst-1
+    merged into plane nst (s_out = s_in + mean' when given), c = w . gamma, d = w . beta + b."""
+    lib = load_library()
+    fmt = fmt_of(a.dtype)
+    _rows(a, "a"); _rows(w, "w"); _rows(out, "out")
+    if w.dtype != a.dtype or out.dtype != a.dtype:
+        raise TypeError("linear_ln: a, w and out must share one 16-bit dtype")
+    M, K, N = a.shape[0], a.shape[1], w.shape[0]
+    _f32_vec(stats, (nst + 1) * M * 2, "stats"); _f32_vec(c, N, "c"); _f32_vec(d, N, "d")
+    for nm, t in (("s_in", s_in), ("s_out", s_out)):
+        if t is not None:
+            _f32_vec(t, M, nm)
+    wp, wb = _ws(ws)
+    _check(lib.gp_linear_ln(_ptr(a), a.stride(0), _ptr(w), w.stride(0), _ptr(stats), int(nst), _ptr(c), _ptr(d),
+                            float(eps), _ptr(s_in), _ptr(s_out), _ptr(out), out.stride(0), M, N, K, wp, wb, fmt,
+                            _stream()), "gp_linear_ln")
+
+
+def ffn_fc1_gelu_ln(a, w1, xstats, nst, c1, d1, eps, s_in, s_out, h, hstats):
+    """gp_ffn_fc1_gelu with final_layer_norm folded as in linear_ln (a = xb)."""
+    lib = load_library()
+    fmt = fmt_of(a.dtype)
+    _rows(a, "a"); _rows(w1, "w1"); _rows(h, "h")
+    if w1.dtype != a.dtype or h.dtype != a.dtype:
+        raise TypeError("ffn_fc1_gelu_ln: a, w1 and h must share one 16-bit dtype")
+    M, K, F = a.shape[0], a.shape[1], w1.shape[0]
+    _f32_vec(xstats, (nst + 1) * M * 2, "xstats"); _f32_vec(c1, F, "c1"); _f32_vec(d1, F, "d1")
+    _f32_vec(hstats, (F // 256 + 1) * M * 2, "hstats")
+    for nm, t in (("s_in", s_in), ("s_out", s_out)):
+        if t is not None:
+            _f32_vec(t, M, nm)
+    _check(lib.gp_ffn_fc1_gelu_ln(_ptr(a), a.stride(0), _ptr(w1), w1.stride(0), _ptr(xstats), int(nst), _ptr(c1),
+                                  _ptr(d1), float(eps), _ptr(s_in), _ptr(s_out), _ptr(h), h.stride(0), _ptr(hstats),
+                                  M, F, K, fmt, _stream()), "gp_ffn_fc1_gelu_ln")
+
+
+def ffn_fc2_ln_resid(h, w2g, hstats, c, d, eps, x, shift, gamma, xb, xstats, ws=None):
+    """x += fc2(ffn_layernorm(h)) through the fold; with gamma: xb / xstats as linear_resid."""
+    lib = load_library()
+    fmt = fmt_of(h.dtype)
+    _rows(h, "h"); _rows(w2g, "w2g"); _rows(x, "x")
+    M, F, N = h.shape[0], h.shape[1], w2g.shape[0]
+    if w2g.dtype != h.dtype or x.dtype != torch.float32 or x.shape[0] < M or x.shape[1] < N:
+        raise TypeError("ffn_fc2_ln_resid: h / w2g share one 16-bit dtype; x is fp32 [M, N]")
+    _f32_vec(hstats, (F // 256 + 1) * M * 2, "hstats"); _f32_vec(c, N, "c"); _f32_vec(d, N, "d")
+    if gamma is not None:
+        _f32_vec(gamma, N, "gamma"); _f32_vec(shift, M, "shift"); _f32_vec(xstats, N // 256 * M * 2, "xstats")
+        _rows(xb, "xb")
+        if xb.dtype != h.dtype:
+            raise TypeError("ffn_fc2_ln_resid: xb must be in h's 16-bit dtype")
+    wp, wb = _ws(ws)
+    _check(lib.gp_ffn_fc2_ln_resid(_ptr(h), h.stride(0), _ptr(w2g), w2g.stride(0), _ptr(hstats), _ptr(c), _ptr(d),
+                                   float(eps), _ptr(x), x.stride(0), _ptr(shift if gamma is not None else None),
+                                   _ptr(gamma), _ptr(xb if gamma is not None else None),
+                                   xb.stride(0) if gamma is not None else 0,
+                                   _ptr(xstats if gamma is not None else None), M, N, F, wp, wb, fmt, _stream()),
+           "gp_ffn_fc2_ln_resid")

@@ -2,18 +2,23 @@
 
 Per layer the engine issues 8 kernels on torch's current HIP stream (M = B*L tokens):
 
-    qkv  = a . Wqkv^T + bqkv             gp_linear (MFMA GEMM, bias epilogue) [M, 3E] bf16
+    qkv  = LN1(x) . Wqkv^T + bqkv         gp_linear_ln (MFMA GEMM, LN1 folded; layer 0: gp_linear of
+                                           the pos-embed kernel's LN1)              [M, 3E] bf16
     attn = gp_dilated_attn_fwd(qkv)        ONE launch, all dilation branches  sparse o / lse
     a    = LN_inner(merge(attn))           gp_branch_merge_ln                 [M, E] bf16
-    y    = a . Wo^T                        gp_linear                          [M, E] bf16
-    x   += y + bo ; a = LN2(x)             gp_residual_layernorm (fp32 residual stream)
-    f    = gelu(a . W1^T + b1), stats      gp_ffn_fc1_gelu (MFMA GEMM, GELU + LN statistics epilogue)
-    y    = LN_ffn(f) . W2^T + b2           gp_ffn_fc2_ln   (MFMA GEMM, LayerNorm folded into the epilogue)
-    x   += y ; a = LN1(next layer)         gp_residual_layernorm
+    x   += a . Wo^T + bo                   gp_linear_resid (fp32 residual stream updated in the epilogue,
+                                           which also writes xb = gamma2 (x - s) and LN statistics)
+    f    = gelu(LN2(x) . W1^T + b1), stats gp_ffn_fc1_gelu_ln (LN2 folded; GELU + LN statistics epilogue)
+    x   += LN_ffn(f) . W2^T + b2           gp_ffn_fc2_ln_resid (LN folded; residual + the next layer's
+                                           xb = gamma1' (x - s) and statistics in the epilogue)
 
-(plus a split-K reduce after a GEMM whose last round of tiles is split; shapes outside the GEMM
-kernels' instantiations, GIGAPATH_OWN_GEMMS=0 or GIGAPATH_FFN_FUSED=0: hipBLASLt for those GEMMs and,
-for the FFN, hipBLASLt fc1 + gp_gelu_layernorm + hipBLASLt fc2)
+(plus a split-K reduce after a GEMM whose last round of tiles is split).  The residual stream never
+makes a separate pass: each LayerNorm is folded into the GEMM that consumes it, from the 16-bit
+xb = act(gamma (x - s)) and per-256-column statistics its producer wrote (s = the row mean before the
+add; gp_gemm_impl.h).  Shapes outside the GEMM kernels' instantiations,
+GIGAPATH_RESID_FUSED=0, GIGAPATH_OWN_GEMMS=0 or GIGAPATH_FFN_FUSED=0 run the round-3 sequence instead:
+gp_linear out-proj -> gp_residual_layernorm -> gp_ffn_fc1_gelu -> gp_ffn_fc2_ln -> gp_residual_layernorm
+(hipBLASLt for uncovered GEMMs; for an uncovered FFN hipBLASLt fc1 + gp_gelu_layernorm + hipBLASLt fc2).
 
 which is EncoderLayer.forward (torchscale/architecture/encoder.py:116-162) with
 DilatedAttention.forward (component/dilated_attention.py:133-217) and the FFN
@@ -28,6 +33,7 @@ import functools
 import math
 import os
 import threading
+from collections import OrderedDict
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -247,10 +253,19 @@ class PackedLayer:
     w2g: Optional[torch.Tensor] = None      # [E, F] act: W2 * gamma_ffn (LN weight folded into fc2)
     c2: Optional[torch.Tensor] = None       # [E] fp32: row sums of w2g as rounded
     d2: Optional[torch.Tensor] = None       # [E] fp32: W2 . beta_ffn + b2
+    # the residual stream inside the GEMMs (gp_linear_ln / gp_ffn_fc1_gelu_ln fold the pre-LNs):
+    c_qkv: Optional[torch.Tensor] = None    # [3E] fp32: w_qkv . gamma1 (w_qkv as rounded)
+    d_qkv: Optional[torch.Tensor] = None    # [3E] fp32: w_qkv . beta1 + b_qkv
+    c1: Optional[torch.Tensor] = None       # [F] fp32: w1 . gamma2
+    d1: Optional[torch.Tensor] = None       # [F] fp32: w1 . beta2 + b1
 
     @property
     def ffn_fused(self) -> bool:
         return self.w2g is not None
+
+    @property
+    def resid_fused(self) -> bool:
+        return self.c1 is not None
 
     @staticmethod
     def from_module(layer, dev, act: torch.dtype = torch.bfloat16) -> "PackedLayer":
@@ -266,8 +281,8 @@ class PackedLayer:
             fln_eps=float(ffn.ffn_layernorm.eps),
             w2=_act(ffn.fc2.weight, dev, act), b2=_f32(ffn.fc2.bias, dev))
         F, E = pl.w1.shape
-        if ffn_fusable(E, F):
-            # LN(h) . W2^T + b2 = rstd (h . (W2 gamma)^T - mean c) + d  (csrc/gp_gemm.hip, "LN fold")
+        if ffn_fusable(E, F) or resid_fusable(E, F):
+            # LN(h) . W2^T + b2 = rstd (h . (W2 gamma)^T - mean c) + d  (csrc/gp_gemm_impl.h, "LN fold")
             w2 = ffn.fc2.weight.detach().to(device=dev, dtype=torch.float64)
             g = ffn.ffn_layernorm.weight.detach().to(device=dev, dtype=torch.float64)
             be = ffn.ffn_layernorm.bias.detach().to(device=dev, dtype=torch.float64)
@@ -275,10 +290,21 @@ class PackedLayer:
             pl.c2 = pl.w2g.double().sum(1).float().contiguous()
             pl.d2 = (w2 @ be + ffn.fc2.bias.detach().to(device=dev, dtype=torch.float64)).float().contiguous()
             pl.b1_f32 = _f32(ffn.fc1.bias, dev)
+        if resid_fusable(E, F):
+            # LN(x) . W^T + b = rstd (xb . W^T - mean' c) + d with xb = act(gamma (x - s)): c = W . gamma
+            # (W as the GEMM rounds it), d = W . beta + b (csrc/gp_gemm_impl.h, "the residual epilogues")
+            def fold(w_act, ln, b):
+                wd = w_act.double()
+                return ((wd @ ln.weight.detach().to(device=dev, dtype=torch.float64)).float().contiguous(),
+                        (wd @ ln.bias.detach().to(device=dev, dtype=torch.float64) + b.double()).float().contiguous())
+            pl.c_qkv, pl.d_qkv = fold(pl.attn.w_qkv, layer.self_attn_layer_norm, pl.attn.b_qkv_f32)
+            pl.c1, pl.d1 = fold(pl.w1, layer.final_layer_norm, _f32(ffn.fc1.bias, dev))
         return pl
 
 
 FFN_FUSED = os.environ.get("GIGAPATH_FFN_FUSED", "1") != "0"
+# the residual adds + pre-LNs inside the out-proj / fc2 epilogues and the QKV / fc1 folds (round 4)
+RESID_FUSED = os.environ.get("GIGAPATH_RESID_FUSED", "1") != "0"
 # the QKV / out-proj / patch projections on gp_linear (own MFMA GEMM, the default) instead of hipBLASLt.
 # With every GEMM of the forward on gp_gemm.hip kernels (persistent, data-parallel tiles, no workgroup ever
 # waits on another) concurrent HIP-graph replays on several streams run (tests/test_gpu_concurrent.py,
@@ -294,16 +320,123 @@ def linear(a: torch.Tensor, w: torch.Tensor, b_act: Optional[torch.Tensor], b_f3
     if OWN_GEMMS and a.is_cuda and _hip.gemm_supported(N, K) and (b_act is None or b_f32 is not None):
         if gemm_ws is not None and gemm_ws.numel() < _hip.gemm_workspace_bytes(a.shape[0], N, K):
             gemm_ws = None                   # (no split of the last round of tiles)
-        _hip.linear(a, w, b_f32, out, gemm_ws)
-    elif b_act is not None:
-        torch.addmm(b_act, a, w.t(), out=out)
+        # gp_linear's operand contract (row-major, 16-byte aligned rows): a strided or offset caller tensor
+        # is copied once instead of being refused
+        if not _gemm_rows_ok(a):
+            a = a.clone(memory_format=torch.contiguous_format)
+        if _gemm_rows_ok(out):
+            _hip.linear(a, w, b_f32, out, gemm_ws)
+        else:
+            tmp = torch.empty(out.shape, dtype=out.dtype, device=out.device)
+            _hip.linear(a, w, b_f32, tmp, gemm_ws)
+            out.copy_(tmp)
     else:
-        torch.mm(a, w.t(), out=out)
+        with blaslt_serialized():
+            if b_act is not None:
+                torch.addmm(b_act, a, w.t(), out=out)
+            else:
+                torch.mm(a, w.t(), out=out)
+
+
+def _gemm_rows_ok(t: torch.Tensor) -> bool:
+    """gp_linear's layout: row-major rows (unit column stride), rows a multiple of 8 elements apart,
+    a 16-byte aligned base."""
+    return t.dim() == 2 and t.stride(1) == 1 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0
+
+
+# hipBLASLt GEMMs (shapes outside the own kernels, GIGAPATH_OWN_GEMMS=0 / GIGAPATH_FFN_FUSED=0): its tuned
+# stream-K kernels spin on flags of peer workgroups, and concurrent forwards / graph replays on several
+# streams hung with them (r03_o, DESIGN §6.3).  Every such GEMM issued outside a capture is ordered after
+# the previous one on ANY stream of the device (an event chain, no host sync), and a captured graph that
+# contains one (BLASLT_ISSUED moved during its capture) replays under the same chain
+# (LongNetViT._replay): hipBLASLt never runs on two streams at once.
+BLASLT_ISSUED = [0]
+_BLASLT_LOCK = threading.RLock()
+_BLASLT_LAST: Dict[int, torch.cuda.Event] = {}
+
+
+def capture_uses_blaslt(before: int) -> bool:
+    """True when a hipBLASLt GEMM was issued since BLASLT_ISSUED[0] was `before` (a capture's contents)."""
+    return BLASLT_ISSUED[0] != before
+
+
+def replay_graph(graph) -> None:
+    """graph.replay() on the current stream; a graph holding hipBLASLt GEMMs (graph.gp_blaslt, set at
+    capture) replays in the device's hipBLASLt event chain (blaslt_serialized)."""
+    if getattr(graph, "gp_blaslt", False):
+        with blaslt_serialized():
+            graph.replay()
+    else:
+        graph.replay()
+
+
+class blaslt_serialized:
+    """Context of one hipBLASLt launch (or one graph replay containing some) on the current stream."""
+
+    def __enter__(self):
+        BLASLT_ISSUED[0] += 1
+        self._chain = torch.cuda.is_available() and not torch.cuda.is_current_stream_capturing()
+        if self._chain:
+            _BLASLT_LOCK.acquire()
+            self._stream = torch.cuda.current_stream()
+            ev = _BLASLT_LAST.get(self._stream.device.index)
+            if ev is not None:
+                self._stream.wait_event(ev)
+        return self
+
+    def __exit__(self, *exc):
+        if self._chain:
+            try:
+                ev = torch.cuda.Event()
+                ev.record(self._stream)
+                _BLASLT_LAST[self._stream.device.index] = ev
+            finally:
+                _BLASLT_LOCK.release()
+        return False
 
 
 def ffn_fusable(E: int, F: int) -> bool:
-    """The fused FFN kernels cover fc1 [F, E] and fc2 [E, F] (gp_gemm.hip instantiations)."""
-    return FFN_FUSED and _hip.gemm_supported(F, E) and _hip.gemm_supported(E, F) and 2 * E <= 3072
+    """The fused FFN kernels cover fc1 [F, E] (K = E) and fc2 [E, F] (K = F)."""
+    return (FFN_FUSED and E in _hip.GEMM_K_E and F in _hip.GEMM_K_F and _hip.gemm_supported(F, E)
+            and _hip.gemm_supported(E, F))
+
+
+def resid_fusable(E: int, F: int) -> bool:
+    """Every GEMM of the layer on the residual-epilogue / LN-fold kernels: QKV [3E, E], out-proj [E, E],
+    fc1 [F, E] with K = E and fc2 [E, F] with K = F (the three registered archs)."""
+    return (RESID_FUSED and FFN_FUSED and OWN_GEMMS and E in _hip.GEMM_K_E and F in _hip.GEMM_K_F
+            and all(_hip.gemm_supported(n, k) for n, k in ((3 * E, E), (E, E), (F, E), (E, F))))
+
+
+def resid_buffers(dev, M: int, E: int):
+    """(xstats [E/256 + 1, M, 2], shift [2, M]) of the residual epilogues (fp32)."""
+    return (torch.empty((E // 256 + 1) * M * 2, dtype=torch.float32, device=dev),
+            torch.empty(2, M, dtype=torch.float32, device=dev))
+
+
+def fused_qkv(pl: "PackedLayer", ws, qkv: torch.Tensor):
+    """QKV of a layer after the first: LN1 folded, A = ws.y (the previous fc2's xb); merges the
+    statistics (shift[1] -> shift[0])."""
+    pa = pl.attn
+    E = pa.E
+    _hip.linear_ln(ws.y, pa.w_qkv, ws.xstats, E // 256, pl.c_qkv, pl.d_qkv, pl.ln1_eps, ws.shift[1], ws.shift[0],
+                   qkv, ws.gemm_ws)
+
+
+def fused_post_attention(pl: "PackedLayer", nxt: Optional["PackedLayer"], ws):
+    """out-proj + residual, fc1 (+ folded LN2, GELU), fc2 (+ folded ffn LN, residual, the next layer's
+    xb) on ws.a (the merge output).  Shift schedule: out-proj reads shift[0] (the row mean of x before it),
+    fc1's merge writes shift[1], fc2 reads it; the next QKV maps shift[1] -> shift[0]."""
+    pa = pl.attn
+    E = pa.E
+    with TIMER.span("gemm_out"):
+        _hip.linear_resid(ws.a, pa.w_o, pa.b_o, ws.x, ws.shift[0], pl.ln2_w, ws.y, ws.xstats, ws.gemm_ws)
+    with TIMER.span("gemm_fc1"):
+        _hip.ffn_fc1_gelu_ln(ws.y, pl.w1, ws.xstats, E // 256, pl.c1, pl.d1, pl.ln2_eps, ws.shift[0], ws.shift[1],
+                             ws.f, ws.fstats)
+    with TIMER.span("gemm_fc2"):
+        _hip.ffn_fc2_ln_resid(ws.f, pl.w2g, ws.fstats, pl.c2, pl.d2, pl.fln_eps, ws.x, ws.shift[1],
+                              nxt.ln1_w if nxt is not None else None, ws.y, ws.xstats, ws.gemm_ws)
 
 
 def ffn_forward(pl: "PackedLayer", a: torch.Tensor, f: torch.Tensor, y: torch.Tensor, fstats, gemm_ws,
@@ -316,18 +449,18 @@ def ffn_forward(pl: "PackedLayer", a: torch.Tensor, f: torch.Tensor, y: torch.Te
         with TIMER.span("gemm_fc2"):
             _hip.ffn_fc2_ln(f, pl.w2g, fstats, pl.c2, pl.d2, pl.fln_eps, y, gemm_ws)
         return None
-    with TIMER.span("gemm_fc1"):
+    with TIMER.span("gemm_fc1"), blaslt_serialized():
         torch.addmm(pl.b1, a, pl.w1.t(), out=f)
     with TIMER.span("gelu_ln"):
         _hip.gelu_layernorm(f, pl.fln_w, pl.fln_b, pl.fln_eps, f, M, F)
-    with TIMER.span("gemm_fc2"):
+    with TIMER.span("gemm_fc2"), blaslt_serialized():
         torch.mm(f, pl.w2.t(), out=y)
     return pl.b2
 
 
 def ffn_buffers(dev, M: int, E: int, F: int):
-    """(stats, GEMM workspace) of the fused FFN for M rows, or (None, None) when it does not apply."""
-    if not ffn_fusable(E, F):
+    """(stats, GEMM workspace) of the fused FFN for M rows, or (None, workspace) when it does not apply."""
+    if not (ffn_fusable(E, F) or resid_fusable(E, F)):
         return None, gemm_workspace(dev, M, E, F)
     stats = torch.empty((F // 256 + 1) * M * 2, dtype=torch.float32, device=dev)
     return stats, gemm_workspace(dev, M, E, F)
@@ -406,6 +539,7 @@ class Workspace:
         self.y = torch.empty(M, E, dtype=act, device=dev)
         self.f = torch.empty(M, F, dtype=act, device=dev)
         self.fstats, self.gemm_ws = ffn_buffers(dev, M, E, F)
+        self.xstats, self.shift = resid_buffers(dev, M, E)
         self.attn = AttentionScratch(dev, B, L, H, E // H, segs, ratios, act)
 
 
@@ -425,6 +559,7 @@ class PackedWorkspace(Workspace):
         self.y = torch.empty(M, E, dtype=act, device=dev)
         self.f = torch.empty(M, F, dtype=act, device=dev)
         self.fstats, self.gemm_ws = ffn_buffers(dev, M, E, F)
+        self.xstats, self.shift = resid_buffers(dev, M, E)
         self.attn = VarlenScratch(dev, self.Ls, H, E // H, segs, ratios, self.qkv)
         self.tok_off = self.attn.plan.tok_off
         self.cls_idx = torch.tensor(self.tok_off[:-1], dtype=torch.int64, device=dev)
@@ -438,10 +573,12 @@ class EncoderEngine:
         self.layers: List[PackedLayer] = []
         self._packs: Dict[torch.dtype, tuple] = {}     # act -> (signature, packed layers)
         # activation workspaces per CALLER STREAM: two streams never share activation buffers, so
-        # forwards (and HIP graphs, which bake the workspace of the stream they were captured on)
-        # issued on different streams can run concurrently; ws / pws = the last one used
-        self._ws: Dict[int, Workspace] = {}
-        self._pws: Dict[int, PackedWorkspace] = {}
+        # forwards issued on different streams can run concurrently; ws / pws = the last one used.
+        # LRU-bounded (max_stream_workspaces): a caller using a fresh stream per request does not grow
+        # them without limit.  A HIP graph's workspace is detached from these maps after its capture
+        # (detach_workspace) and lives exactly as long as the graph (LongNetViT._graph_ws).
+        self._ws: "OrderedDict[int, Workspace]" = OrderedDict()
+        self._pws: "OrderedDict[int, PackedWorkspace]" = OrderedDict()
         self.ws: Optional[Workspace] = None
         self.pws: Optional[PackedWorkspace] = None
 
@@ -462,35 +599,70 @@ class EncoderEngine:
     def _stream_key(dev) -> int:
         return int(torch.cuda.current_stream(dev).cuda_stream) if torch.device(dev).type == "cuda" else 0
 
+    max_stream_workspaces = 4
+
+    def _cached(self, table, key, make):
+        sk = self._stream_key(self._dev_of(key))
+        ws = table.get(sk)
+        if ws is None or ws.key != key:
+            table.pop(sk, None)                # (a HIP graph that baked the old one keeps it alive)
+            while len(table) >= self.max_stream_workspaces:
+                old = next(iter(table))        # least recently used caller stream
+                table.pop(old)
+            ws = table[sk] = make()
+        table.move_to_end(sk)
+        return ws
+
+    @staticmethod
+    def _dev_of(key):
+        return torch.device(key[0])
+
     def workspace(self, dev, B, L, E, F, H, segs, ratios, act: Optional[torch.dtype] = None) -> Workspace:
         act = act or act_dtype()
         key = (str(dev), B, L, E, F, H, tuple(segs), tuple(ratios), act)
-        sk = self._stream_key(dev)
-        ws = self._ws.get(sk)
-        if ws is None or ws.key != key:
-            self._ws.pop(sk, None)             # (a HIP graph that baked the old one keeps it alive)
-            ws = self._ws[sk] = Workspace(dev, B, L, E, F, H, segs, ratios, act)
-        self.ws = ws
-        return ws
+        self.ws = self._cached(self._ws, key, lambda: Workspace(dev, B, L, E, F, H, segs, ratios, act))
+        return self.ws
 
     def workspace_packed(self, dev, Ls, E, F, H, segs, ratios, act: Optional[torch.dtype] = None) -> PackedWorkspace:
         act = act or act_dtype()
         key = (str(dev), tuple(int(x) for x in Ls), E, F, H, tuple(segs), tuple(ratios), act)
-        sk = self._stream_key(dev)
-        ws = self._pws.get(sk)
-        if ws is None or ws.key != key:
-            self._pws.pop(sk, None)
-            ws = self._pws[sk] = PackedWorkspace(dev, Ls, E, F, H, segs, ratios, act)
-        self.pws = ws
-        return ws
+        self.pws = self._cached(self._pws, key, lambda: PackedWorkspace(dev, Ls, E, F, H, segs, ratios, act))
+        return self.pws
 
-    def run_layers(self, ws: Workspace, B: int, L: int, layer_hook=None):
+    def detach_workspace(self, ws) -> None:
+        """Forget `ws` (a HIP graph's baked workspace): the next eager call on its stream allocates a new
+        one, and the graph cache alone decides how long `ws` lives."""
+        for table in (self._ws, self._pws):
+            for k in [k for k, v in table.items() if v is ws]:
+                table.pop(k)
+        if self.ws is ws:
+            self.ws = None
+        if self.pws is ws:
+            self.pws = None
+
+    def run_layers(self, ws: Workspace, B: int, L: int, layer_hook=None, shift_ready: bool = False):
         """ws.x holds the fp32 embedding and ws.a = LN1_0(ws.x) (16-bit).  Runs every layer in
-        place; layer_hook(i) is called after layer i-1 finishes (i = 1..depth)."""
+        place; layer_hook(i) is called after layer i-1 finishes (i = 1..depth).  shift_ready: ws.shift[0]
+        already holds the row means of ws.x (gp_posembed_cls_ln's row_mean); otherwise they are computed."""
         M = B * L
         E = ws.x.shape[1]
         F = ws.f.shape[1]
         nl = len(self.layers)
+        if self.layers and all(pl.resid_fused for pl in self.layers) and ws.fstats is not None:
+            if not shift_ready:
+                torch.mean(ws.x, 1, out=ws.shift[0])
+            for li, pl in enumerate(self.layers):
+                pa = pl.attn
+                with TIMER.span("gemm_qkv"):
+                    if li == 0:
+                        linear(ws.a, pa.w_qkv, pa.b_qkv, pa.b_qkv_f32, ws.qkv, ws.gemm_ws)
+                    else:
+                        fused_qkv(pl, ws, ws.qkv)
+                dilated_attention_core(pa, ws.qkv, B, L, ws.attn, ws.a)
+                fused_post_attention(pl, self.layers[li + 1] if li + 1 < nl else None, ws)
+                if layer_hook is not None:
+                    layer_hook(li + 1)
+            return
         for li, pl in enumerate(self.layers):
             pa = pl.attn
             with TIMER.span("gemm_qkv"):

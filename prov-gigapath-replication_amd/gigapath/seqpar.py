@@ -359,12 +359,16 @@ class ExchangeMonitor:
         self._pending = []                   # RCCL (layer, phase, e0, e1) until resolve()
         self._armed: Optional[Tuple[float, str]] = None
         self._lock = threading.Lock()
+        self._stop = threading.Event()
         self._thread = threading.Thread(target=self._watch, name="sp-exchange-watchdog", daemon=True)
         self._thread.start()
 
+    def close(self):
+        """Stop the watchdog thread (SeqParallelContext.set_monitor does it when the monitor is replaced)."""
+        self._stop.set()
+
     def _watch(self):
-        while True:
-            time.sleep(0.25)
+        while not self._stop.wait(0.25):
             with self._lock:
                 armed = self._armed
             if armed is not None and time.monotonic() - armed[0] > self.bound_s:
@@ -418,6 +422,7 @@ class ShardWorkspace:
         self.y = torch.empty(self.n, E, dtype=act, device=dev)
         self.f = torch.empty(self.n, F, dtype=act, device=dev)
         self.fstats, self.gemm_ws = runtime.ffn_buffers(dev, self.n, E, F)
+        self.xstats, self.shift = runtime.resid_buffers(dev, self.n, E)
         # per branch: K/V receive buffer = the need range in token order; send buffer packed by peer
         self.kvs, self.kv_base, self.send, self.send_off = [], [], [], []
         for b in range(len(plan.geo)):
@@ -536,8 +541,8 @@ class SeqParallelEngine:
         Exchange.wait(handles)
         e1.record()
         mon.arm(self._label(li, ph, branches))
-        while not e1.query():
-            time.sleep(2e-5)
+        while not e1.query():       # (sleeping releases the GIL; 0.2 ms against a ~ms exchange)
+            time.sleep(2e-4)
         mon.disarm()
         mon._pending.append((li, ph, e0, e1))
 
@@ -572,17 +577,21 @@ class SeqParallelEngine:
         if g is None:
             fn()                                    # this call's work (and allocator warm-up)
             g = torch.cuda.CUDAGraph()
+            n_blaslt = runtime.BLASLT_ISSUED[0]
             with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 fn()                                # captured, not executed
+            g.gp_blaslt = runtime.capture_uses_blaslt(n_blaslt)
             self.graphs[key] = g
             return
-        g.replay()
+        runtime.replay_graph(g)
 
     def run_layers(self, layers, ws: ShardWorkspace, layer_hook=None, weights_sig=None):
-        """ws.x holds this shard's fp32 embedding and ws.a = LN1_0(ws.x).  Runs every layer in place.
+        """ws.x holds this shard's fp32 embedding, ws.a = LN1_0(ws.x) and ws.shift[0] its row means
+        (gp_posembed_cls_ln).  Runs every layer in place.
         Per layer: [QKV GEMM + sparsify] -> all-to-alls (phase A, phase B) -> wait A -> attention A
-        -> wait B -> [attention B + merge + out-proj + residual/LN + FFN + residual/LN]; with
-        use_graphs the two bracketed segments are HIP-graph replays (collectives stay eager)."""
+        -> wait B -> [attention B + merge + out-proj + residual + FFN + residual (runtime's residual
+        epilogues; the round-3 residual/LN passes where they do not apply)]; with use_graphs the two
+        bracketed segments are HIP-graph replays (collectives stay eager)."""
         plan = self.plan
         E, H, D = plan.E, plan.H, plan.D
         a, e = plan.bounds[self.rank]
@@ -597,13 +606,17 @@ class SeqParallelEngine:
         if wsig != self._graph_sig:          # new weights: captures of the old ones never replay
             self.graphs.clear()
             self._graph_sig = wsig
+        fused = bool(layers) and all(pl.resid_fused for pl in layers) and ws.fstats is not None
         for li, pl in enumerate(layers):
             pa = pl.attn
             nxt = layers[li + 1] if li + 1 < nl else None
 
-            def head(pa=pa):
+            def head(pa=pa, pl=pl, li=li):
                 with runtime.TIMER.span("gemm_qkv"):
-                    runtime.linear(ws.a, pa.w_qkv, pa.b_qkv, pa.b_qkv_f32, ws.qkv, ws.gemm_ws)
+                    if fused and li > 0:
+                        runtime.fused_qkv(pl, ws, ws.qkv)
+                    else:
+                        runtime.linear(ws.a, pa.w_qkv, pa.b_qkv, pa.b_qkv_f32, ws.qkv, ws.gemm_ws)
                 self.sparsify(ws)
 
             def tail(pa=pa, pl=pl, nxt=nxt):
@@ -611,6 +624,9 @@ class SeqParallelEngine:
                 with runtime.TIMER.span("merge"):
                     _hip.branch_merge_ln_window(ws.attn.outs, ws.attn.lses, plan.segs, plan.ratios, 1, plan.L, a, M,
                                                 H, D, pa.ln_w, pa.ln_b, pa.ln_eps, ws.a)
+                if fused:
+                    runtime.fused_post_attention(pl, nxt, ws)
+                    return
                 with runtime.TIMER.span("gemm_out"):
                     runtime.linear(ws.a, pa.w_o, None, None, ws.y, ws.gemm_ws)
                 with runtime.TIMER.span("resid_ln"):
@@ -654,7 +670,10 @@ class SeqParallelContext:
         self.monitor: Optional[ExchangeMonitor] = None
 
     def set_monitor(self, monitor: Optional[ExchangeMonitor]):
-        """Attach (or, with None, detach) an ExchangeMonitor to this and every later engine."""
+        """Attach (or, with None, detach) an ExchangeMonitor to this and every later engine.  A monitor
+        that is replaced (not merely detached) has its watchdog thread stopped."""
+        if self.monitor is not None and monitor is not None and monitor is not self.monitor:
+            self.monitor.close()
         self.monitor = monitor
         if self.engine is not None:
             self.engine.monitor = monitor

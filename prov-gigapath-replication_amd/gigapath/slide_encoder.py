@@ -100,7 +100,8 @@ class LongNetViT(nn.Module):
         self._graph_ws = {}
         self._graph_bytes = {}
         self._graph_seen = {}
-        self._capture_streams = {}
+        self._capture_streams = OrderedDict()
+        self.max_capture_streams = 8
         self.initialize_vit_weights()
 
     # ---------------------------------------------------------------- sequence parallel
@@ -223,7 +224,7 @@ class LongNetViT(nn.Module):
         graph, sx, sc, outs = ent
         sx.copy_(x)
         sc.copy_(c)
-        graph.replay()
+        runtime.replay_graph(graph)
         return [o.clone() for o in outs]
 
     def check_positions(self, coords_list):
@@ -247,7 +248,12 @@ class LongNetViT(nn.Module):
         dev = self.cls_token.device
         key = (str(dev), int(torch.cuda.current_stream(dev).cuda_stream))
         if key not in self._capture_streams:
+            # LRU-bounded: a captured graph replays on whatever stream calls it, so an evicted capture
+            # stream costs only a new stream object at the next capture from that caller stream
+            while len(self._capture_streams) >= self.max_capture_streams:
+                self._capture_streams.pop(next(iter(self._capture_streams)))
             self._capture_streams[key] = torch.cuda.Stream(device=dev)
+        self._capture_streams.move_to_end(key)
         return self._capture_streams[key]
 
     def graph_entry(self, x, c, all_layer_embed):
@@ -328,12 +334,17 @@ class LongNetViT(nn.Module):
         with torch.cuda.stream(stream):
             run(sx, sc)
         graph = torch.cuda.CUDAGraph()
+        n_blaslt = runtime.BLASLT_ISSUED[0]
         with torch.cuda.graph(graph, stream=stream, capture_error_mode="thread_local"):
             outs = run(sx, sc)
+        # a graph with hipBLASLt GEMMs in it replays in the device's hipBLASLt event chain (runtime.replay_graph)
+        graph.gp_blaslt = runtime.capture_uses_blaslt(n_blaslt)
         cur.wait_stream(stream)
-        # the graph bakes this shape's workspace: keep it alive with the graph; evict least recently
-        # used graphs beyond the entry and byte budgets
+        # the graph bakes this shape's workspace: keep it alive with the graph (and ONLY with it: the
+        # engine forgets it, so evicting the graph frees it); evict least recently used graphs beyond
+        # the entry and byte budgets
         ws = workspace()
+        self.encoder.engine.detach_workspace(ws)
         nbytes = self._tensor_bytes(ws) + sx.untyped_storage().nbytes() + sc.untyped_storage().nbytes()
         while self._graphs and (len(self._graphs) >= self.max_hip_graphs or
                                 sum(self._graph_bytes.values()) + nbytes > self.hip_graph_max_bytes):
@@ -398,7 +409,7 @@ class LongNetViT(nn.Module):
                 graph, sx, sc, res = ent
                 sx.copy_(x_cat)
                 sc.copy_(c_cat)
-                graph.replay()
+                runtime.replay_graph(graph)
                 res = res.clone()
         else:
             res = self._forward_packed_device(x_cat, c_cat, Ns, all_layer_embed)
@@ -428,7 +439,7 @@ class LongNetViT(nn.Module):
                 t0 = ws.tok_off[i]
                 _hip.posembed_cls_ln(xp[n0:n0 + n], ws.pos[n0:n0 + n], top["tab"], top["cls"], 1, n, E,
                                      self.slide_ngrids, top["ln1_w"], top["ln1_b"], top["ln1_eps"],
-                                     ws.x[t0:t0 + n + 1], ws.a[t0:t0 + n + 1])
+                                     ws.x[t0:t0 + n + 1], ws.a[t0:t0 + n + 1], ws.shift[0, t0:t0 + n + 1])
                 n0 += n
         n_out = (1 + len(layers)) if all_layer_embed else 1
         res = torch.empty(n_out, S, E, dtype=torch.float32, device=dev)
@@ -445,7 +456,7 @@ class LongNetViT(nn.Module):
 
         if all_layer_embed:
             readout(0)
-        eng.run_layers(ws, 1, T, readout if all_layer_embed else None)
+        eng.run_layers(ws, 1, T, readout if all_layer_embed else None, shift_ready=True)
         if not all_layer_embed:
             if self.global_pool:
                 _hip.layernorm_f32(ws.x, E, top["enc_w"], top["enc_b"], top["enc_eps"], ws.x, T, E)
@@ -481,7 +492,7 @@ class LongNetViT(nn.Module):
                              (self.slide_ngrids ** 2 + 1, int(ws.err.item())))
         with runtime.TIMER.span("posembed"):
             _hip.posembed_cls_ln(xp, ws.pos, top["tab"], top["cls"], B, N, E, self.slide_ngrids, top["ln1_w"],
-                                 top["ln1_b"], top["ln1_eps"], ws.x, ws.a)
+                                 top["ln1_b"], top["ln1_eps"], ws.x, ws.a, ws.shift[0])
 
         n_out = (1 + len(layers)) if all_layer_embed else 1
         res = torch.empty(n_out, B, E, dtype=torch.float32, device=dev)
@@ -496,7 +507,7 @@ class LongNetViT(nn.Module):
 
         if all_layer_embed:
             readout(0)
-        eng.run_layers(ws, B, L, readout if all_layer_embed else None)
+        eng.run_layers(ws, B, L, readout if all_layer_embed else None, shift_ready=True)
         if not all_layer_embed:
             if self.global_pool:
                 _hip.layernorm_f32(ws.x, E, top["enc_w"], top["enc_b"], top["enc_eps"], ws.x, M, E)
@@ -546,7 +557,7 @@ class LongNetViT(nn.Module):
                                  (self.slide_ngrids ** 2 + 1, int(err.item())))
         with runtime.TIMER.span("posembed"):
             _hip.posembed_cls_ln(xp, ws.pos, top["tab"], top["cls"] if a == 0 else None, 1, nt, E, self.slide_ngrids,
-                                 top["ln1_w"], top["ln1_b"], top["ln1_eps"], ws.x, ws.a)
+                                 top["ln1_w"], top["ln1_b"], top["ln1_eps"], ws.x, ws.a, ws.shift[0])
         n_out = (1 + len(layers)) if all_layer_embed else 1
         res = torch.zeros(n_out, 1, E, dtype=torch.float32, device=dev)
         pool = torch.empty(1, E, dtype=torch.float32, device=dev)

@@ -31,7 +31,7 @@ def coords_to_pos(coords, grid, tile_size, pos_out, err_count):
         err_count += int(((pos < -nrows) | (pos >= nrows)).sum())
 
 
-def posembed_cls_ln(xp, pos, tab, cls, B, N, E, G, ln_w, ln_b, eps, x_out, ln_out):
+def posembed_cls_ln(xp, pos, tab, cls, B, N, E, G, ln_w, ln_b, eps, x_out, ln_out, row_mean=None):
     has = cls is not None
     rows = B * (N + has)
     assert x_out.shape[0] >= rows and (ln_out is None or ln_out.shape[0] >= rows)
@@ -41,6 +41,9 @@ def posembed_cls_ln(xp, pos, tab, cls, B, N, E, G, ln_w, ln_b, eps, x_out, ln_ou
     v = xp[:B * N].float() + pe
     out = torch.cat([cls.view(1, E).float(), v], 0) if has else v
     x_out[:rows] = out
+    if row_mean is not None:
+        assert row_mean.numel() >= rows
+        row_mean.view(-1)[:rows] = out.mean(1)
     if ln_w is not None:
         ln_out[:rows] = _ln(out, ln_w, ln_b, eps).to(ln_out.dtype)
 
@@ -96,6 +99,70 @@ def ffn_fc2_ln(h, w2g, stats, c, d, eps, y, ws=None):
     rstd = torch.rsqrt(m2 / F + eps)
     acc = h.float() @ w2g.float().t()
     y[:M] = (rstd[:, None] * (acc - mean[:, None] * c.float()[None]) + d.float()[None]).to(y.dtype)
+
+
+def _merge_stats(stats, nst, M, eps, s_in, s_out):
+    """row_stats_kernel: Chan-merge planes 0 .. nst-1 into plane nst; s_out = s_in + mean."""
+    st = stats.view(-1)[:(nst + 1) * M * 2].view(nst + 1, M, 2)
+    mg = st[:nst, :, 0]
+    mean = mg.mean(0)
+    m2 = st[:nst, :, 1].sum(0) + 256.0 * ((mg - mean) ** 2).sum(0)
+    rstd = torch.rsqrt(m2 / (256 * nst) + eps)
+    st[nst, :, 0] = mean
+    st[nst, :, 1] = rstd
+    if s_out is not None:
+        s_out.view(-1)[:M] = (s_in.view(-1)[:M] if s_in is not None else 0) + mean
+    return mean, rstd
+
+
+def _resid_out(x, v, shift, gamma, xb, xstats):
+    """The residual epilogue: x = v; xb = act(gamma (x - shift)); xstats[g][m] = (mean, M2) of x - shift."""
+    M, N = v.shape
+    x[:M, :N] = v
+    if gamma is None:
+        return
+    assert shift.numel() >= M and xb.shape[0] >= M and xb.shape[1] >= N and xstats.numel() >= N // 256 * M * 2
+    dlt = v - shift.view(-1)[:M, None]
+    xb[:M, :N] = (dlt * gamma.float()[None]).to(xb.dtype)
+    dg = dlt.view(M, N // 256, 256)
+    mean = dg.mean(-1)
+    st = xstats.view(-1)[:(N // 256) * M * 2].view(N // 256, M, 2)
+    st[..., 0] = mean.t()
+    st[..., 1] = ((dg - mean[..., None]) ** 2).sum(-1).t()
+
+
+def linear_resid(a, w, bias, x, shift, gamma, xb, xstats, ws=None):
+    M, N = a.shape[0], w.shape[0]
+    y = a.float() @ w.float().t() + (bias.float() if bias is not None else 0)
+    _resid_out(x, x[:M, :N] + y, shift, gamma, xb, xstats)
+
+
+def linear_ln(a, w, stats, nst, c, d, eps, s_in, s_out, out, ws=None):
+    M = a.shape[0]
+    mean, rstd = _merge_stats(stats, nst, M, eps, s_in, s_out)
+    acc = a.float() @ w.float().t()
+    out[:M] = (rstd[:, None] * (acc - mean[:, None] * c.float()[None]) + d.float()[None]).to(out.dtype)
+
+
+def ffn_fc1_gelu_ln(a, w1, xstats, nst, c1, d1, eps, s_in, s_out, h, hstats):
+    M, F = a.shape[0], w1.shape[0]
+    mean, rstd = _merge_stats(xstats, nst, M, eps, s_in, s_out)
+    v = (rstd[:, None] * (a.float() @ w1.float().t() - mean[:, None] * c1.float()[None]) + d1.float()[None])
+    g = torch.nn.functional.gelu(v.to(h.dtype).float()).to(h.dtype)
+    h[:M] = g
+    gf = g.float().view(M, F // 256, 256)
+    gm = gf.mean(-1)
+    st = hstats.view(-1)[:(F // 256) * M * 2].view(F // 256, M, 2)
+    st[..., 0] = gm.t()
+    st[..., 1] = ((gf - gm[..., None]) ** 2).sum(-1).t()
+
+
+def ffn_fc2_ln_resid(h, w2g, hstats, c, d, eps, x, shift, gamma, xb, xstats, ws=None):
+    M, F = h.shape
+    N = w2g.shape[0]
+    mean, rstd = _merge_stats(hstats, F // 256, M, eps, None, None)
+    y = rstd[:, None] * (h.float() @ w2g.float().t() - mean[:, None] * c.float()[None]) + d.float()[None]
+    _resid_out(x, x[:M, :N] + y, shift, gamma, xb, xstats)
 
 
 def dilated_sparsify(src, src_row_stride, k_col, v_col, tok_lo, n_tok, L, H, D, segs, ratios, dsts, dst_bases=None):
@@ -221,7 +288,8 @@ def install():
     """Replace the _hip entry points in this process (call in a test subprocess only)."""
     from gigapath import _hip
     for name in ("coords_to_pos", "posembed_cls_ln", "layernorm_f32", "mean_tokens", "residual_layernorm",
-                 "gelu_layernorm", "ffn_fc1_gelu", "ffn_fc2_ln", "dilated_sparsify", "dilated_sparsify_dests", "attn_branch", "dilated_attn_fwd_ex",
+                 "gelu_layernorm", "ffn_fc1_gelu", "ffn_fc2_ln", "linear_resid", "linear_ln", "ffn_fc1_gelu_ln",
+                 "ffn_fc2_ln_resid", "dilated_sparsify", "dilated_sparsify_dests", "attn_branch", "dilated_attn_fwd_ex",
                  "branch_merge_ln_window"):
         setattr(_hip, name, globals()[name])
     _written.clear()

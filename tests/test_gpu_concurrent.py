@@ -17,14 +17,25 @@ import oracle as orc
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.timeout(300)
-def test_four_stream_concurrent_graph_replays_equal_eager():
+ARCH_SIZES = {"gigapath_slide_enc12l768d": [24000, 17000, 30000, 24000],
+              # (round 4: every GEMM of the 1024-d arch on the own kernels -- K = 1024 / 4096, N = 3072 / 4096 --
+              # so its graphs hold no hipBLASLt stream-K kernel either; verdict r03 item 7)
+              "gigapath_slide_enc24l1024d": [12000, 9000, 15000, 12000]}
+
+
+def _model(arch):
     from gigapath import slide_encoder
-    cfg = orc.arch_config("gigapath_slide_enc12l768d")
-    model = slide_encoder.create_model("", "gigapath_slide_enc12l768d", 1536)
+    cfg = orc.arch_config(arch)
+    model = slide_encoder.create_model("", arch, 1536)
     model.load_state_dict({k: torch.from_numpy(v) for k, v in orc.make_weights(cfg, seed=0).items()}, strict=True)
-    model = model.cuda().eval()
-    sizes = [24000, 17000, 30000, 24000]          # two equal shapes: must not share activation buffers
+    return model.cuda().eval()
+
+
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("arch", sorted(ARCH_SIZES))
+def test_four_stream_concurrent_graph_replays_equal_eager(arch):
+    model = _model(arch)
+    sizes = ARCH_SIZES[arch]                      # two equal shapes: must not share activation buffers
     slides = []
     for i, n in enumerate(sizes):
         x, c = orc.synthetic_slide(n, seed_x=70 + i, seed_c=80 + i)
@@ -43,6 +54,7 @@ def test_four_stream_concurrent_graph_replays_equal_eager():
                     model(x, c, all_layer_embed=True)
             torch.cuda.synchronize()
             assert len(model._graphs) == 4
+            assert not any(g[0].gp_blaslt for g in model._graphs.values())   # no hipBLASLt in the forward
             for _ in range(3):                            # concurrent replays
                 outs = []
                 for s, (x, c) in zip(streams, slides):
@@ -55,5 +67,88 @@ def test_four_stream_concurrent_graph_replays_equal_eager():
     finally:
         model.use_hip_graphs, model.graph_min_uses = False, 2
         model.validate_positions = True
+        for k in list(model._graphs):
+            model._drop_graph(k)
+
+
+@pytest.mark.timeout(300)
+def test_graph_eviction_frees_its_workspace():
+    """A graph's baked activation workspace lives exactly as long as the graph: the engine
+    forgets it after the capture, so dropping the graph returns its memory; a caller using a fresh stream
+    per call does not grow the engine's per-stream workspaces past their LRU bound."""
+    import gc
+    model = _model("gigapath_slide_enc12l768d")
+    x, c = orc.synthetic_slide(20000, seed_x=5, seed_c=6)
+    x, c = torch.from_numpy(x).cuda(), torch.from_numpy(c).cuda()
+    eng = model.encoder.engine
+    model.use_hip_graphs, model.graph_min_uses = True, 1
+    try:
+        with torch.no_grad():
+            model(x, c)
+            torch.cuda.synchronize()
+            gc.collect()
+            held = torch.cuda.memory_allocated()
+            assert len(model._graphs) == 1
+            (key,) = list(model._graphs)
+            ws = model._graph_ws[key]
+            assert all(v is not ws for v in eng._ws.values())
+            nbytes = model._graph_bytes[key]
+            model._drop_graph(key)
+            del ws
+            gc.collect()
+            torch.cuda.synchronize()
+            freed = held - torch.cuda.memory_allocated()
+            assert freed >= 0.5 * nbytes, (freed, nbytes)
+        model.use_hip_graphs = False
+        with torch.no_grad():
+            for _ in range(eng.max_stream_workspaces + 3):
+                s = torch.cuda.Stream()
+                s.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s):
+                    model(x[:, :2000], c[:, :2000])
+                torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        assert len(eng._ws) <= eng.max_stream_workspaces
+    finally:
+        model.use_hip_graphs, model.graph_min_uses = False, 2
+        for k in list(model._graphs):
+            model._drop_graph(k)
+
+
+@pytest.mark.timeout(300)
+def test_hipblaslt_graphs_replay_serialised(monkeypatch):
+    """With the own GEMMs switched off (GIGAPATH_OWN_GEMMS=0: the forward's projections on hipBLASLt,
+    whose stream-K kernels hung concurrent replays in r03_o), a captured graph is flagged and its
+    replays on several streams are ordered by the device's hipBLASLt event chain: results equal eager."""
+    from gigapath import runtime
+    monkeypatch.setattr(runtime, "OWN_GEMMS", False)
+    monkeypatch.setattr(runtime, "RESID_FUSED", False)
+    model = _model("gigapath_slide_enc12l768d")
+    slides = []
+    for i, n in enumerate([9000, 7000]):
+        x, c = orc.synthetic_slide(n, seed_x=30 + i, seed_c=40 + i)
+        slides.append((torch.from_numpy(x).cuda(), torch.from_numpy(c).cuda()))
+    with torch.no_grad():
+        ref = [torch.stack(model(x, c, all_layer_embed=True)) for x, c in slides]
+    streams = [torch.cuda.Stream() for _ in slides]
+    model.use_hip_graphs, model.graph_min_uses, model.validate_positions = True, 1, False
+    try:
+        with torch.no_grad():
+            for s, (x, c) in zip(streams, slides):
+                s.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s):
+                    model(x, c, all_layer_embed=True)
+            torch.cuda.synchronize()
+            assert all(g[0].gp_blaslt for g in model._graphs.values())
+            for _ in range(2):
+                outs = []
+                for s, (x, c) in zip(streams, slides):
+                    with torch.cuda.stream(s):
+                        outs.append(torch.stack(model(x, c, all_layer_embed=True)))
+                torch.cuda.synchronize()
+                for got, want in zip(outs, ref):
+                    assert torch.equal(got, want)
+    finally:
+        model.use_hip_graphs, model.graph_min_uses, model.validate_positions = False, 2, True
         for k in list(model._graphs):
             model._drop_graph(k)

@@ -210,3 +210,224 @@ def test_ffn_fc2_layernorm_fold(act, M):
     cos = torch.nn.functional.cosine_similarity(y.float().flatten(), ref.flatten(), dim=0).item()
     assert cos >= 0.99995, cos
     assert runtime.ffn_fusable(E, F)
+
+
+# ---------------------------------------------------------------------------------------------------
+# The residual stream inside the GEMMs (ABI 7): gp_linear_resid / gp_ffn_fc2_ln_resid (producers: x += y,
+# xb = act(gamma (x - s)), per-256-column statistics of x - s) and gp_linear_ln / gp_ffn_fc1_gelu_ln
+# (consumers: the LayerNorm folded, statistics merged, shift carried).  Reference: encoder.py:141,147,159
+# (residual adds), :126 / :147 (pre-LNs) -- restated in torch fp32/fp64 on the same 16-bit operands.
+def _resid_inputs(g, M, N, shift_noise=0.05):
+    x = _rand((M, N), g) + 0.7                       # a residual stream with a non-zero row mean
+    s = x.mean(1) + _rand((M,), g, shift_noise)      # the shift: a stale row mean (the mean before the add)
+    return x, s
+
+
+def _stats_ref(v, s, N):
+    dlt = (v.double() - s.double()[:, None]).view(v.shape[0], N // 256, 256)
+    mean = dlt.mean(-1)
+    return mean, ((dlt - mean[..., None]) ** 2).sum(-1)
+
+
+def _check_resid(act, x_new, xb, xst, ref_x, s, gamma, N, M):
+    # x: fp32 sum of the old stream and the GEMM output (accumulation-order differences only)
+    err = (x_new.double() - ref_x.double()).abs().max().item()
+    assert err <= 2e-4 * ref_x.abs().max().item(), err
+    # xb = act(gamma (x - s)) of the kernel's own x, one 16-bit rounding
+    want = ((x_new.double() - s.double()[:, None]) * gamma.double()[None]).to(act)
+    assert (xb.float() - want.float()).abs().max().item() <= 1e-2 * want.float().abs().max().item()
+    assert (xb == want).float().mean().item() >= 0.98
+    mean, m2 = _stats_ref(x_new, s, N)
+    st = xst.view(N // 256, M, 2).double()
+    assert torch.allclose(st[..., 0], mean.t(), rtol=1e-4, atol=1e-5)
+    assert torch.allclose(st[..., 1], m2.t(), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("act", ACTS)
+@pytest.mark.parametrize("M", [1, 17, 4097, 70001])
+def test_linear_resid(act, M):
+    """out-proj + residual (gp_linear_resid): x += a . w^T + b, xb, statistics; rows past M untouched; the
+    split tail (70001 rows: 822 tiles) and the data-parallel plan; gamma = None updates x only."""
+    h = _hip()
+    N = K = 768
+    g = torch.Generator(device=DEV).manual_seed(M + 7)
+    a = _rand((M, K), g).to(act)
+    w = _rand((N, K), g, K ** -0.5).to(act)
+    b = _rand((N,), g, 0.1)
+    gamma = 1.0 + _rand((N,), g, 0.3)
+    x0, s = _resid_inputs(g, M, N)
+    ref_x = x0 + (a.float() @ w.float().t() + b)
+    nb = h.gemm_workspace_bytes(M, N, K)
+    ws = torch.empty(max(nb, 16), dtype=torch.uint8, device=DEV)
+    for use_ws in (True, False):
+        xbuf = torch.full((M + 8, N), 7.0, device=DEV)
+        xbuf[:M] = x0
+        xb = torch.full((M + 8, N), float("nan"), dtype=act, device=DEV)
+        xst = torch.full((N // 256 + 1, M, 2), float("nan"), device=DEV)
+        h.linear_resid(a, w, b, xbuf, s, gamma, xb, xst, ws if use_ws else None)
+        torch.cuda.synchronize()
+        assert (xbuf[M:] == 7.0).all() and torch.isnan(xb[M:].float()).all()   # nothing past row M
+        _check_resid(act, xbuf[:M], xb[:M], xst[:N // 256], ref_x, s, gamma, N, M)
+    xbuf = x0.clone()
+    h.linear_resid(a, w, b, xbuf, None, None, None, None, ws)
+    torch.cuda.synchronize()
+    assert (xbuf.double() - ref_x.double()).abs().max().item() <= 2e-4 * ref_x.abs().max().item()
+
+
+def _fold_setup(g, act, M, E, Nout):
+    """x, shift, LN affine and the producer's xb / statistics planes (merged plane left to the consumer)."""
+    x, s = _resid_inputs(g, M, E)
+    gam = 1.0 + _rand((E,), g, 0.3)
+    bet = _rand((E,), g, 0.1)
+    xb = ((x.double() - s.double()[:, None]) * gam.double()[None]).to(act)
+    mean, m2 = _stats_ref(x, s, E)
+    st = torch.empty(E // 256 + 1, M, 2, device=DEV)
+    st[:E // 256, :, 0] = mean.t().float()
+    st[:E // 256, :, 1] = m2.t().float()
+    return x, s, gam, bet, xb, st
+
+
+@pytest.mark.parametrize("act", ACTS)
+@pytest.mark.parametrize("M", [1, 300, 70001])
+def test_linear_ln_fold(act, M):
+    """QKV with the pre-LN folded (gp_linear_ln): against the reference order LN(x) in fp32 rounded to act,
+    then x . W^T + b; the merged statistics plane and the carried shift s_out = s_in + mean'."""
+    h = _hip()
+    E, N = 768, 2304
+    g = torch.Generator(device=DEV).manual_seed(M + 11)
+    x, s, gam, bet, xb, st = _fold_setup(g, act, M, E, N)
+    w = _rand((N, E), g, E ** -0.5).to(act)
+    b = _rand((N,), g, 0.1)
+    c = (w.double() @ gam.double()).float()
+    d = (w.double() @ bet.double() + b.double()).float()
+    s_out = torch.full((M,), float("nan"), device=DEV)
+    nb = h.gemm_workspace_bytes(M, N, E)
+    ws = torch.empty(max(nb, 16), dtype=torch.uint8, device=DEV)
+    out = torch.full((M, N), float("nan"), dtype=act, device=DEV)
+    h.linear_ln(xb, w, st, E // 256, c, d, 1e-5, s, s_out, out, ws)
+    torch.cuda.synchronize()
+    ln = torch.nn.functional.layer_norm(x, (E,), gam, bet, 1e-5)
+    assert torch.allclose(s_out.double(), x.double().mean(1), rtol=1e-5, atol=1e-5)
+    assert torch.allclose(st[E // 256, :, 1].double(), 1.0 / torch.sqrt(x.double().var(1, unbiased=False) + 1e-5),
+                          rtol=1e-4)
+    ref = ln.to(act).float() @ w.float().t() + b
+    rel = _rel(out, ref)
+    assert rel <= 1e-2, rel
+    cos = torch.nn.functional.cosine_similarity(out.float().flatten(), ref.flatten(), dim=0).item()
+    assert cos >= 0.99995, cos
+
+
+@pytest.mark.parametrize("act", ACTS)
+@pytest.mark.parametrize("M", [1, 300, 70001])
+def test_ffn_fc1_gelu_ln_fold(act, M):
+    """fc1 + GELU with final_layer_norm folded (gp_ffn_fc1_gelu_ln) against LN(x) -> act -> fc1 -> act ->
+    gelu -> act; its statistics against the kernel's own h."""
+    h = _hip()
+    E, F = 768, 3072
+    g = torch.Generator(device=DEV).manual_seed(M + 13)
+    x, s, gam, bet, xb, st = _fold_setup(g, act, M, E, F)
+    w1 = _rand((F, E), g, E ** -0.5 * 1.5).to(act)
+    b1 = _rand((F,), g, 0.2)
+    c1 = (w1.double() @ gam.double()).float()
+    d1 = (w1.double() @ bet.double() + b1.double()).float()
+    hh = torch.full((M, F), float("nan"), dtype=act, device=DEV)
+    hst = torch.full((F // 256 + 1, M, 2), float("nan"), device=DEV)
+    s_out = torch.empty(M, device=DEV)
+    h.ffn_fc1_gelu_ln(xb, w1, st, E // 256, c1, d1, 1e-5, s, s_out, hh, hst)
+    torch.cuda.synchronize()
+    ln = torch.nn.functional.layer_norm(x, (E,), gam, bet, 1e-5).to(act).float()
+    pre = (ln @ w1.float().t() + b1).to(act).float()
+    ref = torch.nn.functional.gelu(pre)
+    rel = _rel(hh, ref)
+    assert rel <= 1e-2, rel
+    hf = hh.float().view(M, F // 256, 256).double()
+    mean = hf.mean(-1)
+    assert torch.allclose(hst[:F // 256, :, 0].double(), mean.t(), rtol=1e-5, atol=1e-6)
+    assert torch.allclose(hst[:F // 256, :, 1].double(), ((hf - mean[..., None]) ** 2).sum(-1).t(), rtol=1e-4,
+                          atol=1e-4)
+
+
+@pytest.mark.parametrize("act", ACTS)
+@pytest.mark.parametrize("M", [1, 300, 70001])
+def test_ffn_fc2_ln_resid(act, M):
+    """fc2 with ffn_layernorm folded + residual (gp_ffn_fc2_ln_resid): x += LN(h) . W2^T + b2 in the
+    reference order (LN in fp32 rounded to act, fp32 GEMM), the next layer's xb / statistics; gamma =
+    None (the last layer) updates x only."""
+    h = _hip()
+    E, F = 768, 3072
+    g = torch.Generator(device=DEV).manual_seed(M + 17)
+    hh = torch.nn.functional.gelu(_rand((M, F), g)).to(act)
+    hst = torch.empty(F // 256 + 1, M, 2, device=DEV)
+    hf = hh.float().view(M, F // 256, 256).double()
+    mean = hf.mean(-1)
+    hst[:F // 256, :, 0] = mean.t().float()
+    hst[:F // 256, :, 1] = ((hf - mean[..., None]) ** 2).sum(-1).t().float()
+    gf = 1.0 + _rand((F,), g, 0.3)
+    bf = _rand((F,), g, 0.1)
+    w2 = _rand((E, F), g, F ** -0.5).to(act)
+    b2 = _rand((E,), g, 0.1)
+    w2g = (w2.double() * gf.double()[None]).to(act)
+    c = w2g.double().sum(1).float()
+    d = (w2.double() @ bf.double() + b2.double()).float()
+    gam_next = 1.0 + _rand((E,), g, 0.3)
+    x0, s = _resid_inputs(g, M, E)
+    ln = torch.nn.functional.layer_norm(hh.float(), (F,), gf, bf, 1e-5).to(act).float()
+    y_ref = ln @ w2.float().t() + b2
+    nb = h.gemm_workspace_bytes(M, E, F)
+    ws = torch.empty(max(nb, 16), dtype=torch.uint8, device=DEV)
+    xbuf = x0.clone()
+    xb = torch.full((M, E), float("nan"), dtype=act, device=DEV)
+    xst = torch.full((E // 256 + 1, M, 2), float("nan"), device=DEV)
+    h.ffn_fc2_ln_resid(hh, w2g, hst, c, d, 1e-5, xbuf, s, gam_next, xb, xst, ws)
+    torch.cuda.synchronize()
+    y = xbuf.double() - x0.double()
+    assert (y - y_ref.double()).abs().max().item() <= 1e-2 * y_ref.abs().max().item()
+    _check_resid(act, xbuf, xb, xst[:E // 256], xbuf, s, gam_next, E, M)
+    x2 = x0.clone()
+    h.ffn_fc2_ln_resid(hh, w2g, hst, c, d, 1e-5, x2, None, None, None, None, ws)
+    torch.cuda.synchronize()
+    assert torch.equal(x2, xbuf)        # the same x whether or not the next LN's operands are written
+
+
+def test_resid_epilogue_errors():
+    """The C ABI's checks of the residual entry points (no launch)."""
+    h = _hip()
+    g = torch.Generator(device=DEV).manual_seed(5)
+    a = _rand((64, 768), g).bfloat16()
+    w = _rand((768, 768), g).bfloat16()
+    x = torch.zeros(64, 768, device=DEV)
+    with pytest.raises(RuntimeError, match="K=3072"):   # the residual out-proj epilogue: K = E only
+        h.linear_resid(_rand((64, 3072), g).bfloat16(), _rand((768, 3072), g).bfloat16(), None, x, None, None,
+                       None, None)
+    with pytest.raises(RuntimeError, match="xb"):
+        lib = h.load_library()
+        rc = lib.gp_linear_resid(a.data_ptr(), 768, w.data_ptr(), 768, None, x.data_ptr(), 768,
+                                 x.data_ptr(), x.data_ptr(), None, 768, x.data_ptr(), 64, 768, 768, None, 0, 0,
+                                 h._stream())
+        h._check(rc, "gp_linear_resid")
+
+
+def test_runtime_linear_takes_strided_and_offset_operands():
+    """runtime.linear (the engine's nn.Linear) accepts what torch.addmm accepts: an operand whose storage
+    offset breaks gp_linear's 16-byte row alignment, a transposed-strided one, and a strided output are
+    staged instead of refused; results equal the aligned call."""
+    from gigapath import runtime
+    _hip()
+    g = torch.Generator(device=DEV).manual_seed(21)
+    M, K, N = 333, 768, 768
+    w = _rand((N, K), g, K ** -0.5).bfloat16()
+    b = _rand((N,), g, 0.1)
+    a = _rand((M, K), g).bfloat16()
+    ref = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    runtime.linear(a, w, b.bfloat16(), b, ref)
+    flat = torch.zeros(M * K + 4, dtype=torch.bfloat16, device=DEV)
+    a_off = flat[4:].view(M, K)
+    a_off.copy_(a)                                    # storage offset 4 elements = 8 bytes
+    a_t = a.t().contiguous().t()                      # column-major view
+    for aa in (a_off, a_t):
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        runtime.linear(aa, w, b.bfloat16(), b, out)
+        assert torch.equal(out, ref)
+    big = torch.zeros(M, N + 4, dtype=torch.bfloat16, device=DEV)
+    runtime.linear(a, w, b.bfloat16(), b, big[:, 4:])  # output rows 8 bytes off alignment
+    assert torch.equal(big[:, 4:], ref)
