@@ -654,9 +654,10 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
               rc_, (__attribute__((address_space(3))) void*)(g_colt[slot] + (w - 1) * kBN), 16, lane * 16, 0, 0, 0);
         }
       }
-      // residual: the row shift s of the tile's 256 rows (wave 7)
+      // residual: the row shift s of the tile's 256 rows (wave 7; none without a next LN: no xb, no
+      // statistics, and the shift may be null)
       if constexpr (kRes) {
-        if (w == 7) {
+        if (w == 7 && g.shift != nullptr) {
           const int64_t nb = (int64_t)(g.M - m0) * 4;
           const __amdgpu_buffer_rsrc_t rh_ = __builtin_amdgcn_make_buffer_rsrc(
               (void*)(g.shift + m0), (short)0, (int)(nb < 1024 ? nb : 1024), 0x00020000);
