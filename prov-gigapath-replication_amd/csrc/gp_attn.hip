@@ -494,6 +494,19 @@ static_assert(kNWFast == 4 || kNWFast == 8 || kNWFast == 16, "GP_ATTN_NW must be
 #endif
 // Measured lab variants of this kernel (the 16x16x32 P.V GP_ATTN_PV16, the 3-slot ring GP_ATTN_RING3) live
 // in tools/attn_lab/gp_attn_r3_lab.hip.
+// GP_ATTN_VASM (round-4 A/B): the V^T fragment reads of the 2-slot kernel as inline asm with explicit lgkmcnt
+// waits -- the ds_read_tr builtin carries no alias information, so hipcc puts a vmcnt(0) (a wait for this
+// wave's in-flight LDS-DMA of the NEXT tile, which targets the other buffer) before the first V read of
+// every tile; with asm reads the only DMA wait left is the one before the tile's barrier.
+#ifndef GP_ATTN_VASM
+#define GP_ATTN_VASM 0
+#endif
+template <int OFF>
+GP_DEV s16x4 ds_read_tr_asm(uint32_t addr) {
+  s16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
+  return r;
+}
 
 template <int D, bool kPre, int MODE, bool kTab, int NW, bool kH>
 __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_idx) {
@@ -531,6 +544,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   };
   using IB0 = std::integral_constant<int, 0>;
 
+  constexpr bool kVA = GP_ATTN_VASM != 0 && MODE == kModeFast && !kH;
   // ---- work item (32-bit index math: items < 2^31, checked on the host)
   WorkItem wi;
   AttnBranch te;                             // kTab: this item's table entry
@@ -705,6 +719,15 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   // prefetch -- before the first MFMA of every tile
   __builtin_amdgcn_s_waitcnt(0x0f70);
 
+  // kVA: the lane part of the V^T fragment addresses (row & 3, the swizzle, the 8-byte column), LDS bytes
+  uint32_t vlane[2] = {0u, 0u};
+  if constexpr (kVA) {
+    const int row_l = 4 * (lane >> 5) + ((lane >> 2) & 3);
+    const uint32_t sb = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const char*)smem);
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+      vlane[mt] = sb + (uint32_t)(row_l * VROWB + 32 * ((2 * mt + ((lane >> 4) & 1)) ^ (row_l & 3)) + 8 * (lane & 3));
+  }
   if constexpr (GP_ATTN_PRIO != 0 && NW >= 8) {
     if (__builtin_amdgcn_readfirstlane((int)threadIdx.x) >= NT / 2) __builtin_amdgcn_s_setprio(1);
   }
@@ -860,6 +883,27 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
       }
 
       // ---- O^T += V^T . P^T  (2 sub-tiles x 2 k-steps x 2 d-tiles)
+      if constexpr (kVA) {
+        // per sub-tile u: its 8 V^T reads (asm, immediate offsets of this tile's buffer), then one lgkmcnt(0)
+        // tied to their registers, then its 4 MFMAs
+        auto sub = [&](auto uc) {
+          constexpr int u = decltype(uc)::value;
+          constexpr int VB = SET * BUF + KTILE;
+          constexpr int R0 = VB + 32 * u * VROWB, R1 = VB + (32 * u + 16) * VROWB, H8 = 8 * VROWB;
+          s16x4 v00l = ds_read_tr_asm<R0>(vlane[0]), v00h = ds_read_tr_asm<R0 + H8>(vlane[0]);
+          s16x4 v01l = ds_read_tr_asm<R0>(vlane[1]), v01h = ds_read_tr_asm<R0 + H8>(vlane[1]);
+          s16x4 v10l = ds_read_tr_asm<R1>(vlane[0]), v10h = ds_read_tr_asm<R1 + H8>(vlane[0]);
+          s16x4 v11l = ds_read_tr_asm<R1>(vlane[1]), v11h = ds_read_tr_asm<R1 + H8>(vlane[1]);
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v00l), "+v"(v00h), "+v"(v01l), "+v"(v01h), "+v"(v10l),
+                       "+v"(v10h), "+v"(v11l), "+v"(v11h));
+          oacc[0] = mfma_32x32x16<kH>(__builtin_bit_cast(bf16x8, __builtin_shufflevector(v00l, v00h, 0, 1, 2, 3, 4, 5, 6, 7)), pf[u][0], oacc[0]);
+          oacc[1] = mfma_32x32x16<kH>(__builtin_bit_cast(bf16x8, __builtin_shufflevector(v01l, v01h, 0, 1, 2, 3, 4, 5, 6, 7)), pf[u][0], oacc[1]);
+          oacc[0] = mfma_32x32x16<kH>(__builtin_bit_cast(bf16x8, __builtin_shufflevector(v10l, v10h, 0, 1, 2, 3, 4, 5, 6, 7)), pf[u][1], oacc[0]);
+          oacc[1] = mfma_32x32x16<kH>(__builtin_bit_cast(bf16x8, __builtin_shufflevector(v11l, v11h, 0, 1, 2, 3, 4, 5, 6, 7)), pf[u][1], oacc[1]);
+        };
+        sub(std::integral_constant<int, 0>());
+        sub(std::integral_constant<int, 1>());
+      } else
   #pragma unroll
       for (int u = 0; u < 2; ++u)
   #pragma unroll

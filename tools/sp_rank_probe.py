@@ -1,6 +1,6 @@
 """Per-rank compute of the sequence-parallel forward at W ranks, measured on ONE GPU (the pool's boxes
 have one): for each rank r of the W-rank shard plan of the C4 slide, that rank's 12 encoder layers
-(QKV GEMM + sparsify, windowed attention over all branches, merge, out-proj, residual/LN, FFN) run with
+(QKV GEMM + sparsify, windowed attention over all branches, merge, out-proj + residual, FFN + residual) run with
 the K/V exchange replaced by nothing (the receive buffers hold random rows), as HIP-graph replays, timed
 with HIP events.  max over ranks = the compute floor of the W-GPU forward's encoder; the plan's
 received bytes per rank say what the RCCL exchange has to hide.  W = 1 is the same engine on the whole
@@ -69,6 +69,7 @@ def main():
             ws = seqpar.ShardWorkspace(plan, r, dev, F, torch.bfloat16)
             ws.x.normal_(generator=g)
             ws.a.copy_(ws.x)
+            ws.shift[0].copy_(ws.x.mean(1))        # (gp_posembed_cls_ln's row means, for the residual epilogues)
             for kv in ws.kvs:
                 kv.normal_(generator=g)
             if ws.hq:
@@ -83,6 +84,7 @@ def main():
                 for _ in range(args.reps):
                     ws.x.copy_(x0)
                     ws.a.copy_(x0)
+                    ws.shift[0].copy_(x0.mean(1))
                     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     s.record()
                     eng.run_layers(layers, ws)
@@ -92,6 +94,7 @@ def main():
                 # per-kernel-kind breakdown of one eager run (HIP events around each launch)
                 ws.x.copy_(x0)
                 ws.a.copy_(x0)
+                ws.shift[0].copy_(x0.mean(1))
                 runtime.TIMER.reset()
                 runtime.TIMER.enabled = True
                 eng.run_layers(layers, ws)
