@@ -501,6 +501,13 @@ static_assert(kNWFast == 4 || kNWFast == 8 || kNWFast == 16, "GP_ATTN_NW must be
 #ifndef GP_ATTN_VASM
 #define GP_ATTN_VASM 0
 #endif
+// GP_ATTN_VPLANE (round-4 A/B): the V image of the LDS-DMA kernels as planes instead of 128-B swizzled rows --
+// d 0-31 in 64-B rows (4 KiB), d 32-47 in 32-B rows (2 KiB), and a static plane of identical "ones" rows
+// (2 KiB, written once) that the lanes reading d 48-63 address instead: 13 DMA pieces per 64-key tile
+// instead of 15 (no lanes switched off), every ds_read_b64_tr lane group still on 64 distinct banks.
+#ifndef GP_ATTN_VPLANE
+#define GP_ATTN_VPLANE 0
+#endif
 template <int OFF>
 GP_DEV s16x4 ds_read_tr_asm(uint32_t addr) {
   s16x4 r;
@@ -545,6 +552,8 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   using IB0 = std::integral_constant<int, 0>;
 
   constexpr bool kVA = GP_ATTN_VASM != 0 && MODE == kModeFast && !kH;
+  constexpr bool kVP = GP_ATTN_VPLANE != 0 && MODE != kModeGen && D == 48;
+  constexpr int kVPB = 4096, kVPO = 6144;    // kVP: plane of d 32-47, the ones plane (bytes into the V image)
   // ---- work item (32-bit index math: items < 2^31, checked on the host)
   WorkItem wi;
   AttnBranch te;                             // kTab: this item's table entry
@@ -599,7 +608,8 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
       constexpr uint32_t one2 = kH ? 0x3C003C00u : 0x3F803F80u;
       const uint4 ones = make_uint4(one2, one2, one2, one2);
 #endif
-      *reinterpret_cast<uint4*>(bb + KTILE + row * VROWB + 32 * (3 ^ (row & 3)) + 16 * half) = ones;
+      if constexpr (kVP) *reinterpret_cast<uint4*>(bb + KTILE + kVPO + row * 32 + 16 * half) = ones;
+      else *reinterpret_cast<uint4*>(bb + KTILE + row * VROWB + 32 * (3 ^ (row & 3)) + 16 * half) = ones;
     }
   }
 
@@ -624,7 +634,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   // kDMA: piece p of the 15 (7 K + 8 V) goes to wave p % NW; lane-linear 16-B units.  K image:
   // 112-B rows = 6 chunks + 1 pad unit (pad lanes off); V image: 128-B rows, swizzled 32-B blocks
   // (the lanes of the bf16-ones block are off: the prologue wrote it)
-  constexpr int kPieces = (KT * KROWB + KT * VROWB) / 1024;
+  constexpr int kPieces = (KT * KROWB + (kVP ? KT * 96 : KT * VROWB)) / 1024;
   constexpr int PPW = (kPieces + NW - 1) / NW;   // pieces per wave
   int dvo[PPW];
   unsigned dmask = 0;
@@ -638,6 +648,12 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
         const int unit = pc * 64 + lane, row = unit / 7, ch = unit % 7;
         dvo[sl] = (int)((int64_t)row * kvstride * 2 + (ch < 6 ? ch : 0) * 16);
         if (ch < 6) dmask |= 1u << sl;
+      } else if constexpr (kVP) {   // pieces 0-3: d 0-31 (4 x 16 B per key row), 4-5: d 32-47 (2 x 16 B)
+        const int vp = pc - KTILE / 1024;
+        const int unit = (vp < 4 ? vp : vp - 4) * 64 + lane;
+        const int row = vp < 4 ? unit / 4 : unit / 2, ch = vp < 4 ? unit % 4 : 4 + unit % 2;
+        dvo[sl] = (int)(kv_dv + (int64_t)row * kvstride * 2 + ch * 16);
+        dmask |= 1u << sl;
       } else {
         const int unit = (pc - KTILE / 1024) * 64 + lane, row = unit / 8, slot = unit % 8;
         const int b = (slot >> 1) ^ (row & 3);
@@ -727,6 +743,15 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
       vlane[mt] = sb + (uint32_t)(row_l * VROWB + 32 * ((2 * mt + ((lane >> 4) & 1)) ^ (row_l & 3)) + 8 * (lane & 3));
+  }
+  // kVP: the V^T fragment address of (u, s, mt) = vpl[mt] + (32u + 16s) * row bytes of the plane (+ 8 rows
+  // for the high half): d 0-31 -> plane A (64-B rows), d 32-47 -> plane B, d 48-63 -> the ones plane at the
+  // complementary 128-B bank half of the lane's 32-lane group
+  int vpl[2] = {0, 0};
+  if constexpr (kVP) {
+    const int hq = lane >> 5, j = (lane >> 2) & 3, cq = lane & 3, bb = (lane >> 4) & 1;
+    vpl[0] = KTILE + (4 * hq + j) * 64 + 32 * bb + 8 * cq;
+    vpl[1] = bb ? KTILE + kVPO + 128 * (1 - hq) + 32 * j + 8 * cq : KTILE + kVPB + (4 * hq + j) * 32 + 8 * cq;
   }
   if constexpr (GP_ATTN_PRIO != 0 && NW >= 8) {
     if (__builtin_amdgcn_readfirstlane((int)threadIdx.x) >= NT / 2) __builtin_amdgcn_s_setprio(1);
@@ -888,12 +913,17 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
         // tied to their registers, then its 4 MFMAs
         auto sub = [&](auto uc) {
           constexpr int u = decltype(uc)::value;
-          constexpr int VB = SET * BUF + KTILE;
-          constexpr int R0 = VB + 32 * u * VROWB, R1 = VB + (32 * u + 16) * VROWB, H8 = 8 * VROWB;
-          s16x4 v00l = ds_read_tr_asm<R0>(vlane[0]), v00h = ds_read_tr_asm<R0 + H8>(vlane[0]);
-          s16x4 v01l = ds_read_tr_asm<R0>(vlane[1]), v01h = ds_read_tr_asm<R0 + H8>(vlane[1]);
-          s16x4 v10l = ds_read_tr_asm<R1>(vlane[0]), v10h = ds_read_tr_asm<R1 + H8>(vlane[0]);
-          s16x4 v11l = ds_read_tr_asm<R1>(vlane[1]), v11h = ds_read_tr_asm<R1 + H8>(vlane[1]);
+          // immediate offsets of (u, s, mt): the old layout's lane bases exclude KTILE, kVP's include it
+          constexpr int VB = SET * BUF + (kVP ? 0 : KTILE);
+          constexpr int RA = kVP ? 64 : VROWB, RBB = kVP ? 32 : VROWB;   // row bytes for mt = 0 / 1
+          constexpr int A0 = VB + 32 * u * RA, A1 = VB + (32 * u + 16) * RA;
+          constexpr int B0 = VB + 32 * u * RBB, B1 = VB + (32 * u + 16) * RBB;
+          const uint32_t l0 = kVP ? (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const char*)smem) + vpl[0] : vlane[0];
+          const uint32_t l1 = kVP ? (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const char*)smem) + vpl[1] : vlane[1];
+          s16x4 v00l = ds_read_tr_asm<A0>(l0), v00h = ds_read_tr_asm<A0 + 8 * RA>(l0);
+          s16x4 v01l = ds_read_tr_asm<B0>(l1), v01h = ds_read_tr_asm<B0 + 8 * RBB>(l1);
+          s16x4 v10l = ds_read_tr_asm<A1>(l0), v10h = ds_read_tr_asm<A1 + 8 * RA>(l0);
+          s16x4 v11l = ds_read_tr_asm<B1>(l1), v11h = ds_read_tr_asm<B1 + 8 * RBB>(l1);
           asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v00l), "+v"(v00h), "+v"(v01l), "+v"(v01h), "+v"(v10l),
                        "+v"(v10h), "+v"(v11l), "+v"(v11h));
           oacc[0] = mfma_32x32x16<kH>(__builtin_bit_cast(bf16x8, __builtin_shufflevector(v00l, v00h, 0, 1, 2, 3, 4, 5, 6, 7)), pf[u][0], oacc[0]);
@@ -914,6 +944,11 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
             const int blk = 2 * mt + ((lane >> 4) & 1);
             const char* p0 = Vb + row * VROWB + 32 * (blk ^ (row & 3)) + 8 * (lane & 3);
             const char* p1 = p0 + 8 * VROWB;   // rows + 8 keep (row & 3)
+            if constexpr (kVP) {
+              const int rb = mt == 0 ? 64 : 32;   // plane A rows / plane B and ones rows
+              p0 = Kb + vpl[mt] + (32 * u + 16 * s) * rb;
+              p1 = p0 + 8 * rb;
+            }
             const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
             const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p1);
             const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
