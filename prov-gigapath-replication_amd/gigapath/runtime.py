@@ -409,9 +409,11 @@ def resid_fusable(E: int, F: int) -> bool:
 
 
 def resid_buffers(dev, M: int, E: int):
-    """(xstats [E/256 + 1, M, 2], shift [2, M]) of the residual epilogues (fp32)."""
+    """(xstats [E/256 + 1, M, 2], shift [2, M]) of the residual epilogues (fp32).  The two shift rows are
+    each padded to a multiple of 4 floats, so both start 16-byte aligned (the GEMMs LDS-DMA them)."""
+    mp = (M + 3) // 4 * 4
     return (torch.empty((E // 256 + 1) * M * 2, dtype=torch.float32, device=dev),
-            torch.empty(2, M, dtype=torch.float32, device=dev))
+            torch.empty(2, mp, dtype=torch.float32, device=dev)[:, :M])
 
 
 def fused_qkv(pl: "PackedLayer", ws, qkv: torch.Tensor):
