@@ -240,6 +240,15 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
   const int n_my = sid < n_dp ? (n_dp - 1 - sid) / G + 1 : 0;
   const bool tail = S > 1 && g.split && sid < (ntiles - n_dp) * S;
   if (n_my == 0 && !tail) return;
+#if GP_GEMM_STAGGER
+  // lab (round 4): half of each XCD's workgroups start ~GP_GEMM_STAGGER x NK / 12 x 4 us late, so the residual
+  // epilogues' HBM phases (x read + write: 10 B per output element) of one half fall into the other half's
+  // MFMA phases instead of every CU bursting at once
+  if constexpr (epi_res<EPI>) {
+    if ((blockIdx.x >> 3) & 1)
+      for (int z = 0; z < (GP_GEMM_STAGGER * NK) / 12; ++z) __builtin_amdgcn_s_sleep(127);
+  }
+#endif
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const int wm = w >> 2, wn = w & 3;
@@ -614,6 +623,10 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
   // (resid: 32 x stores + 16 xb stores, the x loads interleaved with them already consumed; a count below the
   // true one only makes the next tile's first wait stricter)
   constexpr int kEpiVmem = kRes ? 48 : 16;
+  // VMEM instructions EVERY wave issues in init_tile (the per-tile parameters' LDS-DMA pieces, padded with
+  // stores through an empty descriptor): one compile-time count, so K-tile 0's counted wait can leave them
+  // and the previous epilogue's stores in flight (uncounted, they made that wait drain the first stores)
+  constexpr int kInitVmem = 2;
   // accumulators start at zero (the epilogue applies the bias / the LN fold)
   auto zero_acc = [&]() {
 #pragma unroll
@@ -628,6 +641,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
       zero_acc();
       const int m0 = (T / tiles_n) * kBM, n0 = (T % tiles_n) * kBN;
       const int slot = i_tile & 1;
+      int issued = 0;   // (wave-uniform)
       // LN fold: (mean, rstd) of the tile's 256 rows -> g_rowst[slot]: 2 KiB, two 1-KiB LDS-DMA pieces of
       // wave 0 (lane l: rows 2l, 2l+1 of the piece); rows past M read as zero
       if constexpr (kFold) {
@@ -641,6 +655,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
             __builtin_amdgcn_raw_ptr_buffer_load_lds(
                 rs_, (__attribute__((address_space(3))) void*)((char*)g_rowst[slot] + j * 1024), 16, lane * 16,
                 j * 1024, 0, 0);
+          issued = 2;
         }
       }
       // column vector v (the tile's 256 columns, 1 KiB) by wave 1 + v; a null vector (no bias, no next LN)
@@ -652,6 +667,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
                                                                               0x00020000);
           __builtin_amdgcn_raw_ptr_buffer_load_lds(
               rc_, (__attribute__((address_space(3))) void*)(g_colt[slot] + (w - 1) * kBN), 16, lane * 16, 0, 0, 0);
+          issued = 1;
         }
       }
       // residual: the row shift s of the tile's 256 rows (wave 7; none without a next LN: no xb, no
@@ -663,8 +679,13 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
               (void*)(g.shift + m0), (short)0, (int)(nb < 1024 ? nb : 1024), 0x00020000);
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rh_, (__attribute__((address_space(3))) void*)(g_shift[slot]), 16,
                                                    lane * 16, 0, 0, 0);
+          issued = 1;
         }
       }
+      const __amdgpu_buffer_rsrc_t none_ = __builtin_amdgcn_make_buffer_rsrc(g.ws, (short)0, 0, 0x00020000);
+#pragma unroll
+      for (int j = 0; j < kInitVmem; ++j)
+        if (j >= issued) __builtin_amdgcn_raw_buffer_store_b32(0, none_, 0, 0, 0);
     }
   };
 
@@ -729,7 +750,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
       stage(I1(), I1(), bc, v + 2);
       // retire K-tile v+1 (the weights of v+2 stay in flight); at v = 0 K-tile 1's A halves are older
       // than the previous tile's epilogue stores (or the prologue's stand-ins), which may stay in flight
-      if (pre) wait_vmcnt<4 + kEpiVmem>();
+      if (pre) wait_vmcnt<4 + kEpiVmem + kInitVmem>();
       else wait_vmcnt<4>();
       sync();
       quadrant(I1(), I0());

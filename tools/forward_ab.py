@@ -3,6 +3,10 @@ library builds of the same ABI: per round every build runs one forward (after on
 reports the median forward time and the median per-kernel spans (runtime.TIMER) of each build.
 
     python tools/forward_ab.py --libs prod,tools/attn_lab/liblab_x.so [--tiles 70000] [--rounds 5]
+
+A library entry may carry host-path options after a colon: "prod:noresid" runs the product library with
+runtime.RESID_FUSED off (the round-3 out-proj -> residual_layernorm -> FFN -> residual_layernorm sequence),
+repacking the weights for it -- the in-process A/B of the residual epilogues.
 """
 import argparse
 import contextlib
@@ -28,7 +32,10 @@ def main():
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     prod = _hip.load_library()
-    libs = [(p, prod if p == "prod" else _hip.load_library(os.path.join(ROOT, p))) for p in args.libs.split(",")]
+    libs = []
+    for spec in args.libs.split(","):
+        p = spec.split(":")[0]
+        libs.append((spec, prod if p == "prod" else _hip.load_library(os.path.join(ROOT, p))))
     dev = torch.device("cuda")
     with contextlib.redirect_stdout(sys.stderr):
         model = slide_encoder.create_model("", "gigapath_slide_enc12l768d", 1536).to(dev).eval()
@@ -42,6 +49,11 @@ def main():
         for rnd in range(args.rounds + 1):
             for p, lib in libs:
                 _hip._lib = lib
+                want = ":noresid" not in p
+                if runtime.RESID_FUSED != want:        # (re)pack the weights for this host path
+                    runtime.RESID_FUSED = want
+                    model.encoder.engine._packs.clear()
+                    model.encoder.engine._ws.clear()
                 runtime.TIMER.reset()
                 runtime.TIMER.enabled = rnd > 0
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -15,5 +15,5 @@ timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $OUT
 rc=$?; echo "bench70k rc=$rc"; cat $OUT/bench_70k.json; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python bench.py --no-cpu-baseline > $OUT/prof.log 2>&1
 rc=$?; echo "rocprof rc=$rc"; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python tools/attn_ab.py --libs prod,tools/attn_lab/liblab_vasm.so,tools/attn_lab/liblab_vplane.so,tools/attn_lab/liblab_vpva.so --rounds 7 --out $OUT/ab_vasm.json > $OUT/ab_vasm.log 2>&1
-rc=$?; echo "ab vasm rc=$rc"; tail -6 $OUT/ab_vasm.log
+timeout -k 10 400 python tools/forward_ab.py --libs prod,prod:noresid,tools/attn_lab/liblab_st2.so,tools/attn_lab/liblab_st4.so --rounds 5 --out $OUT/forward_ab.json > $OUT/forward_ab.log 2>&1
+rc=$?; echo "forward ab rc=$rc"; cat $OUT/forward_ab.log | grep forward_ms | cut -c1-300
