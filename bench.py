@@ -54,20 +54,40 @@ def make_slide(n_tiles, seed=1, in_chans=1536, tile=256):
     return x, coords
 
 
-def host_cores():
-    """(threads used for the CPU baseline, usable cores = this process's affinity mask, os.cpu_count()).
-    The GPU box shows the whole machine in os.cpu_count(); the affinity mask is what this job may use,
-    and the CPU baseline runs on all of it (the reference CPU path on the box's host cores)."""
+def cgroup_cpu_quota():
+    """CPUs granted by this job's cgroup CPU bandwidth limit (cgroup v2 cpu.max / v1 cfs quota), None if
+    unlimited.  The GPU box's job shows 256 CPUs in its affinity mask under a 16-CPU quota
+    ("1600000 100000", profiles/r04_f_cpu_facts.txt)."""
     try:
-        usable = len(os.sched_getaffinity(0))
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        return None if q == "max" else float(q) / float(p)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = float(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            p = float(f.read())
+        return None if q <= 0 else q / p
+    except (OSError, ValueError):
+        return None
+
+
+def host_cores():
+    """(threads used for the CPU baseline, usable cores, os.cpu_count(), how usable was derived).
+    Usable = the affinity mask, capped by the cgroup CPU quota: the GPU box's affinity mask lists the whole
+    256-CPU machine while the job's cgroup grants 16 CPUs of bandwidth, and torch on 256 threads under that
+    quota is throttled, not faster (r04_f: no output for 180 s, killed).  The CPU baseline runs on every
+    usable core (the reference CPU path on the box's host cores)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
-        usable = os.cpu_count() or 1
-    return usable, usable, os.cpu_count() or usable
-
-
-# the second, labelled CPU figure: the same sample on this many threads (the OMP_NUM_THREADS share the GPU
-# box grants one GPU's job; BENCH_r01-r03 were measured this way)
-CPU_SECOND_THREADS = 16
+        aff = os.cpu_count() or 1
+    quota = cgroup_cpu_quota()
+    usable = max(1, min(aff, math.ceil(quota))) if quota else aff
+    how = {"affinity": aff, "cgroup_cpu_quota": quota}
+    return usable, usable, os.cpu_count() or usable, how
 
 
 def cpu_baseline(n_tiles, threads, sample_tiles=70000, total_tflops=None):
@@ -92,9 +112,9 @@ def cpu_baseline(n_tiles, threads, sample_tiles=70000, total_tflops=None):
         oracle.encoder_layer(h, W, "encoder.layers.0", cfg["segment_length"], cfg["dilated_ratio"], 16)
         t2 = time.perf_counter()
     full = (t1 - t0) + cfg["depth"] * (t2 - t1)
-    _, usable, ncpu = host_cores()
+    _, usable, ncpu, how = host_cores()
     res = {"value": round(ns / full, 2), "unit": "tiles/s", "cores": threads, "usable_cores": usable,
-           "cpu_count": ncpu, "kind": "port",
+           "usable_from": how, "cpu_count": ncpu, "kind": "port",
            "sample": "EXTRAPOLATED: oracle fp32 torch-CPU, embed + 1 of 12 layers of the %d-tile slide (%.1f s), "
                      "x12 layers (%.1f s per forward)" % (ns, t2 - t0, full)}
     if total_tflops is not None and ns != n_tiles:
@@ -410,15 +430,12 @@ def main():
             r["exchange_exposed"]["ms_per_layer"] for r in reps)
         result["sp_transport"] = "rccl" if backend == "nccl" else backend + " (host-staged rehearsal)"
     if rank == 0 and not args.no_cpu_baseline:
-        threads, usable, ncpu = host_cores()
+        threads, usable, ncpu, _ = host_cores()
         threads = args.cpu_threads or threads
+        print("bench: CPU baseline on %d threads ..." % threads, file=sys.stderr, flush=True)
         result["cpu_baseline"] = cpu_baseline(args.tiles, threads, total_tflops=total_tf)
-        if threads != CPU_SECOND_THREADS and not args.cpu_threads:
-            second = cpu_baseline(args.tiles, min(CPU_SECOND_THREADS, usable), total_tflops=total_tf)
-            second["label"] = ("second figure: the same sample on %d threads (the per-GPU CPU share; "
-                               "not the baseline)" % second["cores"])
-            result["cpu_baseline_16_threads"] = second
         if world == 1 and not mixed and not args.no_cpu_full:
+            print("bench: CPU full forwards (C1, C2) ...", file=sys.stderr, flush=True)
             result["cpu_full_forwards"] = cpu_full_forwards([("C1", 1024), ("C2", 16384)], threads)
     if rank == 0:
         print(json.dumps(result), flush=True)
