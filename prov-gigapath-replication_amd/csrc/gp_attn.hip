@@ -494,26 +494,6 @@ static_assert(kNWFast == 4 || kNWFast == 8 || kNWFast == 16, "GP_ATTN_NW must be
 #endif
 // Measured lab variants of this kernel (the 16x16x32 P.V GP_ATTN_PV16, the 3-slot ring GP_ATTN_RING3) live
 // in tools/attn_lab/gp_attn_r3_lab.hip.
-// GP_ATTN_VASM (round-4 A/B): the V^T fragment reads of the 2-slot kernel as inline asm with explicit lgkmcnt
-// waits -- the ds_read_tr builtin carries no alias information, so hipcc puts a vmcnt(0) (a wait for this
-// wave's in-flight LDS-DMA of the NEXT tile, which targets the other buffer) before the first V read of
-// every tile; with asm reads the only DMA wait left is the one before the tile's barrier.
-#ifndef GP_ATTN_VASM
-#define GP_ATTN_VASM 0
-#endif
-// GP_ATTN_VPLANE (round-4 A/B): the V image of the LDS-DMA kernels as planes instead of 128-B swizzled rows --
-// d 0-31 in 64-B rows (4 KiB), d 32-47 in 32-B rows (2 KiB), and a static plane of identical "ones" rows
-// (2 KiB, written once) that the lanes reading d 48-63 address instead: 13 DMA pieces per 64-key tile
-// instead of 15 (no lanes switched off), every ds_read_b64_tr lane group still on 64 distinct banks.
-#ifndef GP_ATTN_VPLANE
-#define GP_ATTN_VPLANE 0
-#endif
-template <int OFF>
-GP_DEV s16x4 ds_read_tr_asm(uint32_t addr) {
-  s16x4 r;
-  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
-  return r;
-}
 
 template <int D, bool kPre, int MODE, bool kTab, int NW, bool kH>
 __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_idx) {
@@ -551,9 +531,6 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   };
   using IB0 = std::integral_constant<int, 0>;
 
-  constexpr bool kVA = GP_ATTN_VASM != 0 && MODE == kModeFast && !kH;
-  constexpr bool kVP = GP_ATTN_VPLANE != 0 && MODE != kModeGen && D == 48;
-  constexpr int kVPB = 4096, kVPO = 6144;    // kVP: plane of d 32-47, the ones plane (bytes into the V image)
   // ---- work item (32-bit index math: items < 2^31, checked on the host)
   WorkItem wi;
   AttnBranch te;                             // kTab: this item's table entry
@@ -608,8 +585,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
       constexpr uint32_t one2 = kH ? 0x3C003C00u : 0x3F803F80u;
       const uint4 ones = make_uint4(one2, one2, one2, one2);
 #endif
-      if constexpr (kVP) *reinterpret_cast<uint4*>(bb + KTILE + kVPO + row * 32 + 16 * half) = ones;
-      else *reinterpret_cast<uint4*>(bb + KTILE + row * VROWB + 32 * (3 ^ (row & 3)) + 16 * half) = ones;
+      *reinterpret_cast<uint4*>(bb + KTILE + row * VROWB + 32 * (3 ^ (row & 3)) + 16 * half) = ones;
     }
   }
 
@@ -634,7 +610,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   // kDMA: piece p of the 15 (7 K + 8 V) goes to wave p % NW; lane-linear 16-B units.  K image:
   // 112-B rows = 6 chunks + 1 pad unit (pad lanes off); V image: 128-B rows, swizzled 32-B blocks
   // (the lanes of the bf16-ones block are off: the prologue wrote it)
-  constexpr int kPieces = (KT * KROWB + (kVP ? KT * 96 : KT * VROWB)) / 1024;
+  constexpr int kPieces = (KT * KROWB + KT * VROWB) / 1024;
   constexpr int PPW = (kPieces + NW - 1) / NW;   // pieces per wave
   int dvo[PPW];
   unsigned dmask = 0;
@@ -648,12 +624,6 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
         const int unit = pc * 64 + lane, row = unit / 7, ch = unit % 7;
         dvo[sl] = (int)((int64_t)row * kvstride * 2 + (ch < 6 ? ch : 0) * 16);
         if (ch < 6) dmask |= 1u << sl;
-      } else if constexpr (kVP) {   // pieces 0-3: d 0-31 (4 x 16 B per key row), 4-5: d 32-47 (2 x 16 B)
-        const int vp = pc - KTILE / 1024;
-        const int unit = (vp < 4 ? vp : vp - 4) * 64 + lane;
-        const int row = vp < 4 ? unit / 4 : unit / 2, ch = vp < 4 ? unit % 4 : 4 + unit % 2;
-        dvo[sl] = (int)(kv_dv + (int64_t)row * kvstride * 2 + ch * 16);
-        dmask |= 1u << sl;
       } else {
         const int unit = (pc - KTILE / 1024) * 64 + lane, row = unit / 8, slot = unit % 8;
         const int b = (slot >> 1) ^ (row & 3);
@@ -735,24 +705,6 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   // prefetch -- before the first MFMA of every tile
   __builtin_amdgcn_s_waitcnt(0x0f70);
 
-  // kVA: the lane part of the V^T fragment addresses (row & 3, the swizzle, the 8-byte column), LDS bytes
-  uint32_t vlane[2] = {0u, 0u};
-  if constexpr (kVA) {
-    const int row_l = 4 * (lane >> 5) + ((lane >> 2) & 3);
-    const uint32_t sb = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const char*)smem);
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-      vlane[mt] = sb + (uint32_t)(row_l * VROWB + 32 * ((2 * mt + ((lane >> 4) & 1)) ^ (row_l & 3)) + 8 * (lane & 3));
-  }
-  // kVP: the V^T fragment address of (u, s, mt) = vpl[mt] + (32u + 16s) * row bytes of the plane (+ 8 rows
-  // for the high half): d 0-31 -> plane A (64-B rows), d 32-47 -> plane B, d 48-63 -> the ones plane at the
-  // complementary 128-B bank half of the lane's 32-lane group
-  int vpl[2] = {0, 0};
-  if constexpr (kVP) {
-    const int hq = lane >> 5, j = (lane >> 2) & 3, cq = lane & 3, bb = (lane >> 4) & 1;
-    vpl[0] = KTILE + (4 * hq + j) * 64 + 32 * bb + 8 * cq;
-    vpl[1] = bb ? KTILE + kVPO + 128 * (1 - hq) + 32 * j + 8 * cq : KTILE + kVPB + (4 * hq + j) * 32 + 8 * cq;
-  }
   if constexpr (GP_ATTN_PRIO != 0 && NW >= 8) {
     if (__builtin_amdgcn_readfirstlane((int)threadIdx.x) >= NT / 2) __builtin_amdgcn_s_setprio(1);
   }
@@ -908,32 +860,6 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
       }
 
       // ---- O^T += V^T . P^T  (2 sub-tiles x 2 k-steps x 2 d-tiles)
-      if constexpr (kVA) {
-        // per sub-tile u: its 8 V^T reads (asm, immediate offsets of this tile's buffer), then one lgkmcnt(0)
-        // tied to their registers, then its 4 MFMAs
-        auto sub = [&](auto uc) {
-          constexpr int u = decltype(uc)::value;
-          // immediate offsets of (u, s, mt): the old layout's lane bases exclude KTILE, kVP's include it
-          constexpr int VB = SET * BUF + (kVP ? 0 : KTILE);
-          constexpr int RA = kVP ? 64 : VROWB, RBB = kVP ? 32 : VROWB;   // row bytes for mt = 0 / 1
-          constexpr int A0 = VB + 32 * u * RA, A1 = VB + (32 * u + 16) * RA;
-          constexpr int B0 = VB + 32 * u * RBB, B1 = VB + (32 * u + 16) * RBB;
-          const uint32_t l0 = kVP ? (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const char*)smem) + vpl[0] : vlane[0];
-          const uint32_t l1 = kVP ? (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const char*)smem) + vpl[1] : vlane[1];
-          s16x4 v00l = ds_read_tr_asm<A0>(l0), v00h = ds_read_tr_asm<A0 + 8 * RA>(l0);
-          s16x4 v01l = ds_read_tr_asm<B0>(l1), v01h = ds_read_tr_asm<B0 + 8 * RBB>(l1);
-          s16x4 v10l = ds_read_tr_asm<A1>(l0), v10h = ds_read_tr_asm<A1 + 8 * RA>(l0);
-          s16x4 v11l = ds_read_tr_asm<B1>(l1), v11h = ds_read_tr_asm<B1 + 8 * RBB>(l1);
-          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v00l), "+v"(v00h), "+v"(v01l), "+v"(v01h), "+v"(v10l),
-                       "+v"(v10h), "+v"(v11l), "+v"(v11h));
-          oacc[0] = mfma_32x32x16<kH>(__builtin_bit_cast(bf16x8, __builtin_shufflevector(v00l, v00h, 0, 1, 2, 3, 4, 5, 6, 7)), pf[u][0], oacc[0]);
-          oacc[1] = mfma_32x32x16<kH>(__builtin_bit_cast(bf16x8, __builtin_shufflevector(v01l, v01h, 0, 1, 2, 3, 4, 5, 6, 7)), pf[u][0], oacc[1]);
-          oacc[0] = mfma_32x32x16<kH>(__builtin_bit_cast(bf16x8, __builtin_shufflevector(v10l, v10h, 0, 1, 2, 3, 4, 5, 6, 7)), pf[u][1], oacc[0]);
-          oacc[1] = mfma_32x32x16<kH>(__builtin_bit_cast(bf16x8, __builtin_shufflevector(v11l, v11h, 0, 1, 2, 3, 4, 5, 6, 7)), pf[u][1], oacc[1]);
-        };
-        sub(std::integral_constant<int, 0>());
-        sub(std::integral_constant<int, 1>());
-      } else
   #pragma unroll
       for (int u = 0; u < 2; ++u)
   #pragma unroll
@@ -944,11 +870,6 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
             const int blk = 2 * mt + ((lane >> 4) & 1);
             const char* p0 = Vb + row * VROWB + 32 * (blk ^ (row & 3)) + 8 * (lane & 3);
             const char* p1 = p0 + 8 * VROWB;   // rows + 8 keep (row & 3)
-            if constexpr (kVP) {
-              const int rb = mt == 0 ? 64 : 32;   // plane A rows / plane B and ones rows
-              p0 = Kb + vpl[mt] + (32 * u + 16 * s) * rb;
-              p1 = p0 + 8 * rb;
-            }
             const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
             const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p1);
             const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));

@@ -62,13 +62,6 @@ constexpr int kHalf = 128 * kRowB;            // one operand half-tile: 16 KiB
 // written as xb = act(gamma_next * (x - s)) with per-256-column statistics of x - s (s = a per-row shift,
 // the row mean before the add, so the 16-bit rounding sees a nearly centred row); the next GEMM folds that
 // LayerNorm (kEpiLnFold = QKV, kEpiLnFoldGelu = fc1).  The residual_layernorm pass disappears.
-// cache policy of the residual epilogue's x loads / stores (lab A/B: 2 = nt)
-#ifndef GP_GEMM_XLOAD_AUX
-#define GP_GEMM_XLOAD_AUX 0
-#endif
-#ifndef GP_GEMM_XSTORE_AUX
-#define GP_GEMM_XSTORE_AUX 0
-#endif
 enum { kEpiLinear = 0, kEpiGelu = 1, kEpiLnFold = 2, kEpiResid = 3, kEpiLnFoldResid = 4, kEpiLnFoldGelu = 5 };
 template <int EPI>
 constexpr bool epi_fold = EPI == kEpiLnFold || EPI == kEpiLnFoldResid || EPI == kEpiLnFoldGelu;
@@ -247,15 +240,6 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
   const int n_my = sid < n_dp ? (n_dp - 1 - sid) / G + 1 : 0;
   const bool tail = S > 1 && g.split && sid < (ntiles - n_dp) * S;
   if (n_my == 0 && !tail) return;
-#if GP_GEMM_STAGGER
-  // lab (round 4): half of each XCD's workgroups start ~GP_GEMM_STAGGER x NK / 12 x 4 us late, so the residual
-  // epilogues' HBM phases (x read + write: 10 B per output element) of one half fall into the other half's
-  // MFMA phases instead of every CU bursting at once
-  if constexpr (epi_res<EPI>) {
-    if ((blockIdx.x >> 3) & 1)
-      for (int z = 0; z < (GP_GEMM_STAGGER * NK) / 12; ++z) __builtin_amdgcn_s_sleep(127);
-  }
-#endif
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const int wm = w >> 2, wn = w & 3;
@@ -478,8 +462,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
       auto load_x = [&](int mi) {
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni)
-          xv[mi & 1][ni] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rx, x_lane, mi * x_mi + ni * 64,
-                                                                                              GP_GEMM_XLOAD_AUX));
+          xv[mi & 1][ni] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rx, x_lane, mi * x_mi + ni * 64, 0));
       };
       load_x(0);
       load_x(1);
@@ -497,8 +480,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
           }
           const f32x4v v = xv[mi & 1][ni] + yv;   // the reference's order: x + (y + b), y kept in fp32
           typedef int i32x4 __attribute__((ext_vector_type(4)));
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), rx, x_lane, mi * x_mi + ni * 64,
-                                                 GP_GEMM_XSTORE_AUX);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), rx, x_lane, mi * x_mi + ni * 64, 0);
           __builtin_amdgcn_sched_barrier(0);
           asm volatile("s_nop 1");   // the store-data hazard (see the C stores below)
           __builtin_amdgcn_sched_barrier(0);
