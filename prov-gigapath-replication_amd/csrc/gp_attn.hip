@@ -495,24 +495,8 @@ static_assert(kNWFast == 4 || kNWFast == 8 || kNWFast == 16, "GP_ATTN_NW must be
 // Measured lab variants of this kernel (the 16x16x32 P.V GP_ATTN_PV16, the 3-slot ring GP_ATTN_RING3) live
 // in tools/attn_lab/gp_attn_r3_lab.hip.
 
-// GP_ATTN_PERSIST: the LDS-DMA fast / exact launches run min(items, 2 x CUs) workgroups that walk the
-// work items (virtual blocks b, b + G, ...: the same XCD-grouped item order, every virtual block of a
-// workgroup on its XCD); after an item's last tile the NEXT item's K/V tile 0 and Q fragments are issued
-// before this item's epilogue, so their latency runs under it, and no workgroup launch separates two items.
-#ifndef GP_ATTN_PERSIST
-#define GP_ATTN_PERSIST 0
-#endif
-// what one item hands the next (GP_ATTN_PERSIST): pre = the next item's tile 0 is being staged in K/V buffer
-// 0 (the next prologue's wait + barrier publish it) and its Q fragments are loading into qn
-template <int D>
-struct ItemCarry {
-  bool pre = false;
-  bf16x8 qn[D / 16];
-};
-
 template <int D, bool kPre, int MODE, bool kTab, int NW, bool kH>
-__device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_idx, ItemCarry<D>& cy,
-                                            const int next_item, const bool first) {
+__device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_idx) {
   static_assert(!kH || D == 48 || MODE == kModeGen, "fp16 LDS-DMA modes: D = 48");
   static_assert(D == 48 || D == 64, "v2 kernel covers D = 48 and 64");
   static_assert(MODE == kModeGen || (D == 48 && kPre), "LDS-DMA modes need D = 48 and a pre-scaled q");
@@ -523,7 +507,6 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   constexpr int KS = D / 16;                 // k-steps of Q.K^T
   constexpr bool kOnes = (D % 32) != 0;      // spare d rows carry the row-sum ones
   constexpr bool kDMA = MODE != kModeGen;
-  constexpr bool kPersist = GP_ATTN_PERSIST != 0 && (MODE == kModeFast || MODE == kModeExact);
   constexpr bool kZM = MODE == kModeFast && !kH;   // no max, no offset
   // fp16 fast mode: p = 2^(s - m0) with m0 the row max of tile 0 only (fp16's range ends at 2^16, so
   // bf16's offset-free p = 2^s cannot be used); a later key more than 16 log2 units above m0
@@ -558,10 +541,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   const int hh = wi.hh, c = wi.c, bn = wi.bn;
   const int rows_needed = wi.i_hi;
   const int q0 = wi.i_lo + wi.qb * QB;
-  if (q0 >= rows_needed) {                   // (workgroup-uniform) nothing of this item is needed
-    cy.pre = false;
-    return;
-  }
+  if (q0 >= rows_needed) return;
   // rows >= c are zero-padded queries (their q is 0): load nothing for them
   const int qvalid = c < rows_needed ? c : rows_needed;
   if constexpr (MODE == kModeFix) {          // only blocks the fast kernel flagged are recomputed
@@ -594,7 +574,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
 
   // V images: the d-columns >= D of every row (block 3 for D = 48) hold bf16 1.0
   // (GP_ATTN_ONES_SPARSE: only d = 48 and 52, the two rows the epilogue reads; the rest 0)
-  if (kOnes && first) {   // (the DMA never writes these blocks: once per workgroup)
+  if constexpr (kOnes) {
     for (int idx = threadIdx.x; idx < NBUF * KT * 2; idx += NT) {   // NBUF bufs x KT rows x 2 chunks
       const int buf = idx / (2 * KT), rem = idx % (2 * KT), row = rem >> 1, half = rem & 1;
       char* const bb = smem + buf * BUF;
@@ -610,21 +590,15 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   }
 
   // Q fragments (B operand): lane holds Q[q = l32][d = 16ks + 8h .. +7]
-  auto load_q = [&](const uint16_t* qb, int64_t qs, int qq0, int qv, bf16x8 (&dst)[KS]) {
-    const int i = qq0 + w * 32 + l32;
+  bf16x8 qf[KS];
+  {
+    const int i = q0 + w * 32 + l32;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       bf16x8 z = {};
-      if (i < qv) z = *reinterpret_cast<const bf16x8*>(qb + (int64_t)i * qs + 16 * ks + 8 * h);
-      dst[ks] = z;
+      if (i < qvalid) z = *reinterpret_cast<const bf16x8*>(qbase + (int64_t)i * qstride + 16 * ks + 8 * h);
+      qf[ks] = z;
     }
-  };
-  bf16x8 qf[KS];
-  if (kPersist && cy.pre) {
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) qf[ks] = cy.qn[ks];
-  } else {
-    load_q(qbase, qstride, q0, qvalid, qf);
   }
 
   // ---- K/V staging
@@ -638,29 +612,25 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   // (the lanes of the bf16-ones block are off: the prologue wrote it)
   constexpr int kPieces = (KT * KROWB + KT * VROWB) / 1024;
   constexpr int PPW = (kPieces + NW - 1) / NW;   // pieces per wave
-  auto make_dvo = [&](int64_t kvs, int64_t kvdv, int (&dv)[PPW], unsigned& dm) {
-    dm = 0;
-#pragma unroll
-    for (int sl = 0; sl < PPW; ++sl) {
-      const int pc = w + NW * sl;
-      dv[sl] = 0;
-      if (pc >= kPieces) continue;
-      if (pc < KTILE / 1024) {
-        const int unit = pc * 64 + lane, row = unit / 7, ch = unit % 7;
-        dv[sl] = (int)((int64_t)row * kvs * 2 + (ch < 6 ? ch : 0) * 16);
-        if (ch < 6) dm |= 1u << sl;
-      } else {
-        const int unit = (pc - KTILE / 1024) * 64 + lane, row = unit / 8, slot = unit % 8;
-        const int b = (slot >> 1) ^ (row & 3);
-        dv[sl] = (int)(kvdv + (int64_t)row * kvs * 2 + (2 * (b < 3 ? b : 0) + (slot & 1)) * 16);
-        if (b < 3) dm |= 1u << sl;
-      }
-    }
-  };
   int dvo[PPW];
   unsigned dmask = 0;
   if constexpr (kDMA) {
-    make_dvo(kvstride, kv_dv, dvo, dmask);
+#pragma unroll
+    for (int sl = 0; sl < PPW; ++sl) {
+      const int pc = w + NW * sl;
+      dvo[sl] = 0;
+      if (pc >= kPieces) continue;
+      if (pc < KTILE / 1024) {
+        const int unit = pc * 64 + lane, row = unit / 7, ch = unit % 7;
+        dvo[sl] = (int)((int64_t)row * kvstride * 2 + (ch < 6 ? ch : 0) * 16);
+        if (ch < 6) dmask |= 1u << sl;
+      } else {
+        const int unit = (pc - KTILE / 1024) * 64 + lane, row = unit / 8, slot = unit % 8;
+        const int b = (slot >> 1) ^ (row & 3);
+        dvo[sl] = (int)(kv_dv + (int64_t)row * kvstride * 2 + (2 * (b < 3 ? b : 0) + (slot & 1)) * 16);
+        if (b < 3) dmask |= 1u << sl;
+      }
+    }
   } else {
 #pragma unroll
     for (int u = 0; u < LPT; ++u) {
@@ -674,24 +644,21 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
     }
   }
   // kDMA: tile kv0 / KT goes to buffer (kv0 / KT) % 2 = the compile-time bc
-  auto issue_dma = [&](const uint16_t* kb, int64_t kvs, int64_t kvdv, int cc, const int (&dv)[PPW], unsigned dm,
-                       int kv0, char* bufp) {
-    const int64_t tb = (int64_t)kv0 * kvs * 2;
-    const int64_t nrec = (int64_t)(cc - kv0 - 1) * kvs * 2 + kvdv + 2 * D;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)((const char*)kb + tb), (short)0, (int)(nrec < 0x7fffffff ? nrec : 0x7fffffff), 0x00020000);
-#pragma unroll
-    for (int sl = 0; sl < PPW; ++sl) {
-      const int pc = w + NW * sl;
-      if (pc < kPieces && ((dm >> sl) & 1u))
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rs, (__attribute__((address_space(3))) void*)(bufp + (pc < KTILE / 1024 ? pc * 1024 : KTILE + (pc - KTILE / 1024) * 1024)),
-            16, dv[sl], 0, 0, 0);
-    }
-  };
   auto load_tile = [&](int kv0, auto bc) {
     if constexpr (kDMA) {
-      issue_dma(kbase, kvstride, kv_dv, c, dvo, dmask, kv0, bufc(bc));
+      const int64_t tb = (int64_t)kv0 * kvstride * 2;
+      const int64_t nrec = (int64_t)(c - kv0 - 1) * kvstride * 2 + kv_dv + 2 * D;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)((const char*)kbase + tb), (short)0, (int)(nrec < 0x7fffffff ? nrec : 0x7fffffff), 0x00020000);
+      char* bufp = bufc(bc);
+#pragma unroll
+      for (int sl = 0; sl < PPW; ++sl) {
+        const int pc = w + NW * sl;
+        if (pc < kPieces && ((dmask >> sl) & 1u))
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(
+              rs, (__attribute__((address_space(3))) void*)(bufp + (pc < KTILE / 1024 ? pc * 1024 : KTILE + (pc - KTILE / 1024) * 1024)),
+              16, dvo[sl], 0, 0, 0);
+      }
     } else {
       const int64_t toff = (int64_t)kv0 * kvstride;      // wave-uniform
       if (kv0 + KT <= c) {                                // full tile: no per-key bound checks
@@ -727,40 +694,10 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
     for (int r = 0; r < 16; ++r) oacc[mt][r] = 0.f;
 
   const int ntiles = (c + KT - 1) / KT;
-  if (ntiles > 0 && !(kPersist && cy.pre)) {
+  if (ntiles > 0) {
     load_tile(0, IB0());
     store_tile(0);
   }
-  cy.pre = false;
-  // (kPersist) the next item's tile 0 into K/V buffer b and its Q fragments into cy.qn; nothing for a next
-  // item with no needed row (it returns at once and the one after loads its own)
-  auto prefetch_next = [&](int b) {
-    WorkItem wn;
-    AttnBranch ten;
-    if constexpr (kTab) decode_item_tab(a, next_item, wn, ten);
-    else decode_item(a, next_item, wn);
-    const AttnBranch& bq = kTab ? ten : a.br[wn.bi];
-    const GpBranch gn = bq.g;
-    const int q0n = wn.i_lo + wn.qb * QB;
-    if (q0n >= wn.i_hi) return;
-    const int cn = wn.c;
-    const int64_t tokn = (int64_t)wn.bidx * a.L + (int64_t)wn.n * gn.s + wn.j;
-    const int64_t kvsn = (int64_t)gn.r * bq.kv_stride;
-    const int kcn = bq.kv_sparse ? (wn.hh % gn.hpg) * D : wn.hh * D;
-    const uint16_t* qbn = kTab ? bq.q + tokn * a.q_stride + wn.hh * D
-                               : a.q + (tokn - a.q_tok_base) * a.q_stride + wn.hh * D;
-    const uint16_t* kbn = bq.k + (tokn - bq.kv_tok_base) * bq.kv_stride + kcn;
-    const uint16_t* vbn = bq.v + (tokn - bq.kv_tok_base) * bq.kv_stride + kcn;
-    if (cn > 0) {
-      const int64_t kvdvn = (int64_t)((const char*)vbn - (const char*)kbn);
-      int dvn[PPW];
-      unsigned dmn;
-      make_dvo(kvsn, kvdvn, dvn, dmn);
-      issue_dma(kbn, kvsn, kvdvn, cn, dvn, dmn, 0, smem + b * BUF);
-    }
-    load_q(qbn, (int64_t)gn.r * a.q_stride, q0n, cn < wn.i_hi ? cn : wn.i_hi, cy.qn);
-    cy.pre = true;
-  };
   __syncthreads();
   // every vector load so far (Q fragments, tile 0) is complete here; saying so with a real
   // s_waitcnt (vmcnt 0) lets the compiler's wait insertion drop its "Q may still be in flight"
@@ -950,11 +887,6 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
       tile_step(t, std::integral_constant<int, 0>());
       if (t + 1 < ntiles) tile_step(t + 1, std::integral_constant<int, 1>());
     }
-    // (kPersist) both K/V buffers are free after the last tile's barrier: stage the next item's tile 0 into
-    // buffer 0 and its Q fragments now, so their latency runs under this item's epilogue
-    if constexpr (kPersist) {
-      if (next_item >= 0) prefetch_next(0);
-    }
   } else {
     for (int t = 0; t < ntiles; ++t) tile_step(t, std::integral_constant<int, 0>());
   }
@@ -1038,9 +970,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
 // once (independent loads per lane), exits unless one holds the kLseRedo marker, and recomputes the
 // flagged items in turn; kFixItems = 1 (lab builds) is one item per block in item order.
 template <int D, bool kPre, int MODE, bool kTab = false, int NW = 4, bool kH = false>
-// (GP_ATTN_PERSIST: >= 4 waves per SIMD, i.e. <= 128 VGPRs, so two workgroups stay resident per CU)
-__global__ __launch_bounds__(NW * 64, (GP_ATTN_PERSIST != 0 && (MODE == kModeFast || MODE == kModeExact)) ? 4 : 2)
-void dilated_attn32_kernel(const AttnArgs a) {
+__global__ __launch_bounds__(NW * 64, 2) void dilated_attn32_kernel(const AttnArgs a) {
   if constexpr (MODE == kModeFix && kFixItems == 1) {
     attn32_item<D, kPre, MODE, kTab, NW, kH>(a, (int)blockIdx.x);   // its own flagged-row check first
   } else if constexpr (MODE == kModeFix) {
@@ -1076,22 +1006,9 @@ void dilated_attn32_kernel(const AttnArgs a) {
 #pragma unroll
     for (int n = 0; n < NV; ++n) flagged |= use[n] && vals[n] == kLseRedo;
     if (!__syncthreads_or(flagged)) return;
-    ItemCarry<D> cy;
-    for (int k = 0; k < kFixItems && it0 + k < a.total_items; ++k)
-      attn32_item<D, kPre, MODE, kTab, NW, kH>(a, it0 + k, cy, -1, true);
-  } else if constexpr (GP_ATTN_PERSIST != 0 && (MODE == kModeFast || MODE == kModeExact)) {
-    // persistent: virtual blocks b, b + G, ... (G a multiple of 8: the same XCD as b)
-    ItemCarry<D> cy;
-    const int64_t n = a.total_items, G = gridDim.x;
-    bool first = true;
-    for (int64_t vb = blockIdx.x; vb < n; vb += G) {
-      const int nit = vb + G < n ? (int)xcd_group(vb + G, n) : -1;
-      attn32_item<D, kPre, MODE, kTab, NW, kH>(a, (int)xcd_group(vb, n), cy, nit, first);
-      first = false;
-    }
+    for (int k = 0; k < kFixItems && it0 + k < a.total_items; ++k) attn32_item<D, kPre, MODE, kTab, NW, kH>(a, it0 + k);
   } else {
-    ItemCarry<D> cy;
-    attn32_item<D, kPre, MODE, kTab, NW, kH>(a, (int)xcd_group(blockIdx.x, gridDim.x), cy, -1, true);
+    attn32_item<D, kPre, MODE, kTab, NW, kH>(a, (int)xcd_group(blockIdx.x, gridDim.x));
   }
 }
 // ---------------------------------------------------------------------------------------
@@ -1302,25 +1219,6 @@ extern "C" int gp_dilated_gather(const uint16_t* src, int64_t row_stride, int64_
 }
 
 // kh: fp16 operands (the register-staged exact kernels); bf16 otherwise
-// grid of the LDS-DMA fast / exact launches: one workgroup per item, or (GP_ATTN_PERSIST) at most two
-// resident workgroups per CU walking the items (a multiple of 8, so a workgroup's items stay on its XCD)
-static unsigned fast_grid(int64_t items, hipStream_t s) {
-  if constexpr (GP_ATTN_PERSIST == 0) return (unsigned)items;
-  static int cache[64] = {0};
-  hipDevice_t dev = 0;
-  int cus = 256;
-  if (hipStreamGetDevice(s, &dev) == hipSuccess && dev >= 0 && dev < 64) {
-    if (cache[dev] == 0) {
-      int n = 0;
-      if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-      cache[dev] = n;
-    }
-    cus = cache[dev];
-  }
-  const int64_t cap = (2 * (int64_t)cus) & ~(int64_t)7;
-  return (unsigned)(items < cap || cap < 8 ? items : cap);
-}
-
 static int attn_fwd_impl(const uint16_t* q, int64_t q_row_stride, int64_t q_tok_base, int64_t B, int64_t L, int H,
                          int D, int64_t win_lo, int64_t win_hi, const GpAttnBranch* branches, int nbranch,
                          float softmax_scale, int q_log2_prescaled, bool kh, void* stream) {
@@ -1425,9 +1323,9 @@ static int attn_fwd_impl(const uint16_t* q, int64_t q_row_stride, int64_t q_tok_
   if (kh) {
     if (fast) {        // fp16: the exact running-max kernel (GP_ATTN_FP16_EXACT above)
       if constexpr (GP_ATTN_FP16_EXACT != 0) {
-        dilated_attn32_kernel<48, true, kModeExact, false, kNWFast, true><<<fast_grid(items, s), 64 * kNWFast, 0, s>>>(a);
+        dilated_attn32_kernel<48, true, kModeExact, false, kNWFast, true><<<(unsigned)items, 64 * kNWFast, 0, s>>>(a);
       } else {
-        dilated_attn32_kernel<48, true, kModeFast, false, kNWFast, true><<<fast_grid(items, s), 64 * kNWFast, 0, s>>>(a);
+        dilated_attn32_kernel<48, true, kModeFast, false, kNWFast, true><<<(unsigned)items, 64 * kNWFast, 0, s>>>(a);
         if constexpr (GP_ATTN_NOFIX == 0)
           dilated_attn32_kernel<48, true, kModeFix, false, kNWFast, true>
               <<<(unsigned)((items + kFixItems - 1) / kFixItems), 64 * kNWFast, 0, s>>>(a);
@@ -1441,7 +1339,7 @@ static int attn_fwd_impl(const uint16_t* q, int64_t q_row_stride, int64_t q_tok_
     dilated_attn_kernel<96><<<(unsigned)items, 256, 0, s>>>(a);
   } else if (fast) {
     // the product launch: no-max kernel, then the fixup pass (exits at once unless a row was flagged)
-    dilated_attn32_kernel<48, true, kModeFast, false, kNWFast><<<fast_grid(items, s), 64 * kNWFast, 0, s>>>(a);
+    dilated_attn32_kernel<48, true, kModeFast, false, kNWFast><<<(unsigned)items, 64 * kNWFast, 0, s>>>(a);
     if constexpr (GP_ATTN_NOFIX == 0)
       dilated_attn32_kernel<48, true, kModeFix, false, kNWFast>
           <<<(unsigned)((items + kFixItems - 1) / kFixItems), 64 * kNWFast, 0, s>>>(a);
@@ -1729,17 +1627,16 @@ extern "C" int gp_dilated_attn_fwd_varlen(const void* plan_host, const void* pla
   if (fmt == GP_FMT_F16) {
     if constexpr (GP_ATTN_FP16_EXACT != 0) {
       dilated_attn32_kernel<48, true, kModeExact, true, kNWFast, true>
-          <<<fast_grid(h.total_items, gp_stream(stream)), 64 * kNWFast, 0, gp_stream(stream)>>>(a);
+          <<<(unsigned)h.total_items, 64 * kNWFast, 0, gp_stream(stream)>>>(a);
     } else {
       dilated_attn32_kernel<48, true, kModeFast, true, kNWFast, true>
-          <<<fast_grid(h.total_items, gp_stream(stream)), 64 * kNWFast, 0, gp_stream(stream)>>>(a);
+          <<<(unsigned)h.total_items, 64 * kNWFast, 0, gp_stream(stream)>>>(a);
       dilated_attn32_kernel<48, true, kModeFix, true, kNWFast, true>
           <<<(unsigned)((h.total_items + kFixItems - 1) / kFixItems), 64 * kNWFast, 0, gp_stream(stream)>>>(a);
     }
     return gp_check_launch("gp_dilated_attn_fwd_varlen");
   }
-  dilated_attn32_kernel<48, true, kModeFast, true, kNWFast>
-      <<<fast_grid(h.total_items, gp_stream(stream)), 64 * kNWFast, 0, gp_stream(stream)>>>(a);
+  dilated_attn32_kernel<48, true, kModeFast, true, kNWFast><<<(unsigned)h.total_items, 64 * kNWFast, 0, gp_stream(stream)>>>(a);
   dilated_attn32_kernel<48, true, kModeFix, true, kNWFast>
       <<<(unsigned)((h.total_items + kFixItems - 1) / kFixItems), 64 * kNWFast, 0, gp_stream(stream)>>>(a);
   return gp_check_launch("gp_dilated_attn_fwd_varlen");
