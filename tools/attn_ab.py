@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--branches", default="all")
     ap.add_argument("--out", default=None)
     ap.add_argument("--merge", action="store_true")
+    ap.add_argument("--fp16", action="store_true", help="fp16 operands (the pipeline's autocast caller: the exact kernel)")
     args = ap.parse_args()
     if args.merge:
         args.branches = "all"
@@ -48,12 +49,13 @@ def main():
     g = torch.Generator(device="cuda").manual_seed(0)
     qkv = torch.randn(L, 3 * E, device="cuda", generator=g)
     qkv[:, :E] *= 0.35
-    qkv = qkv.to(torch.bfloat16)
+    act = torch.float16 if args.fp16 else torch.bfloat16
+    qkv = qkv.to(act)
     sets = []
     for b in args.branches.split(","):
         sel = list(range(5)) if b == "all" else [int(b)]
         sets.append((b, [SEGS[i] for i in sel], [RATIOS[i] for i in sel]))
-    scratch = {name: runtime.AttentionScratch(torch.device("cuda"), 1, L, H, D, s, r) for name, s, r in sets}
+    scratch = {name: runtime.AttentionScratch(torch.device("cuda"), 1, L, H, D, s, r, act) for name, s, r in sets}
     flops = {name: runtime.attention_valid_flops(L, s, r, H, D) for name, s, r in sets}
     if args.merge:     # report GB/s of the merge's algorithmic bytes instead
         flops = {name: 1e-3 * L * ((2 * E + 4 * H) * sum(1.0 / x for x in r) + 2 * E) for name, _, r in sets}
