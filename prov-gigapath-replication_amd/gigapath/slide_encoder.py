@@ -225,6 +225,17 @@ class LongNetViT(nn.Module):
         sx.copy_(x)
         sc.copy_(c)
         runtime.replay_graph(graph)
+        return self._clone_outputs(outs)
+
+    @staticmethod
+    def _clone_outputs(outs):
+        """Copies of the graph's static outputs.  The readouts are views of one [n_out, B, E] table: one
+        copy of the table (one copy launch instead of 13 for all_layer_embed) and the same views into it."""
+        base = outs[0]._base if outs else None
+        if base is not None and base.is_contiguous() and all(o._base is base for o in outs):
+            nb = base.clone()
+            off = base.storage_offset()
+            return [nb.as_strided(o.size(), o.stride(), o.storage_offset() - off) for o in outs]
         return [o.clone() for o in outs]
 
     def check_positions(self, coords_list):

@@ -234,3 +234,20 @@ def test_activation_format_selection():
     assert (_hip.fmt_of(torch.bfloat16), _hip.fmt_of(torch.float16)) == (_hip.FMT_BF16, _hip.FMT_F16)
     with pytest.raises(TypeError):
         _hip.fmt_of(torch.float32)
+
+
+def test_graph_outputs_cloned_with_one_copy():
+    """The graph replay's readouts (views of one [n_out, B, E] table) come back as views of ONE fresh copy
+    (one copy launch instead of one per readout); independent outputs are cloned one by one."""
+    from gigapath.slide_encoder import LongNetViT
+    res = torch.randn(13, 2, 768)
+    outs = [res[i] for i in range(13)]
+    got = LongNetViT._clone_outputs(outs)
+    assert all(torch.equal(a, b) for a, b in zip(got, outs))
+    assert got[0].untyped_storage().data_ptr() == got[12].untyped_storage().data_ptr()
+    assert got[0].untyped_storage().data_ptr() != res.untyped_storage().data_ptr()
+    got[3].zero_()                      # the copies are disjoint views: the rest is untouched
+    assert torch.equal(got[4], outs[4]) and not torch.equal(got[3], outs[3])
+    loose = [torch.randn(2, 768) for _ in range(3)]
+    got2 = LongNetViT._clone_outputs(loose)
+    assert all(torch.equal(a, b) and a.data_ptr() != b.data_ptr() for a, b in zip(got2, loose))
