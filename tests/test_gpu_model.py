@@ -423,3 +423,20 @@ def test_classification_head_logits(model):
     assert torch.allclose(logits.detach(), want, atol=1e-5)
     logits.sum().backward()                          # the classifier trains on frozen features
     assert head.classifier[0].weight.grad is not None
+
+
+@pytest.mark.parametrize("N,B", [(1, 1), (2, 1), (31, 1), (255, 1), (257, 1), (1023, 1), (5, 3)])
+def test_tiny_and_ragged_slides_vs_oracle(model, N, B):
+    """Edge cases of the token count L = N + 1 (the CLS row included) against the fp32 oracle: one-tile
+    slides (every GEMM a single partial 256-row tile, attention segments of 2 tokens), lengths one short of /
+    one past a 256-row tile, one short of the 1,024-token segment, and a batch of three 5-tile slides --
+    eager and through the HIP-graph replay (each shape captured on first reuse)."""
+    Wt = {k: torch.from_numpy(v) for k, v in orc.make_weights(CFG, seed=0).items()}   # the fixture's weights
+    x, coords = orc.synthetic_slide(N, B=B)
+    ref = torch.stack(orc.slide_encoder_forward(Wt, x, coords, CFG, all_layer_embed=True)).numpy()
+    xt, ct = torch.from_numpy(x).to(DEV), torch.from_numpy(coords).to(DEV)
+    with torch.no_grad():
+        outs = [torch.stack(model(xt, ct, all_layer_embed=True)).cpu().numpy() for _ in range(3)]
+    for k, got in enumerate(outs):
+        check_vectors("tiny/ragged N=%d B=%d run %d" % (N, B, k), "all_layer", got, ref)
+    assert np.array_equal(outs[1], outs[2])     # graph replays agree with each other bit for bit
