@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 4: the default bench command (70k, CPU baseline on every usable core + the 16-thread figure) timed end
+# Round 4: the default bench command (70k, CPU baseline on every usable core) timed end
 # to end, with the box's CPU facts recorded.
 set -o pipefail
 TAG=${1:-r04_f}
