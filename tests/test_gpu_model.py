@@ -440,3 +440,17 @@ def test_tiny_and_ragged_slides_vs_oracle(model, N, B):
     for k, got in enumerate(outs):
         check_vectors("tiny/ragged N=%d B=%d run %d" % (N, B, k), "all_layer", got, ref)
     assert np.array_equal(outs[1], outs[2])     # graph replays agree with each other bit for bit
+
+
+@pytest.mark.parametrize("N,B", [(1, 1), (257, 1), (5, 3)])
+def test_tiny_and_ragged_slides_fp16_caller_vs_oracle(model, N, B):
+    """The same edge cases under the reference pipeline's fp16 autocast (fp16 GEMMs and GELU, the exact
+    fp16 attention kernel) against the fp32 oracle."""
+    Wt = {k: torch.from_numpy(v) for k, v in orc.make_weights(CFG, seed=0).items()}
+    x, coords = orc.synthetic_slide(N, B=B)
+    ref = torch.stack(orc.slide_encoder_forward(Wt, x, coords, CFG, all_layer_embed=True)).numpy()
+    xt, ct = torch.from_numpy(x).to(DEV).half(), torch.from_numpy(coords).to(DEV)
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.float16):
+        outs = [torch.stack(model(xt, ct, all_layer_embed=True)).float().cpu().numpy() for _ in range(2)]
+    for k, got in enumerate(outs):
+        check_vectors("tiny/ragged fp16 N=%d B=%d run %d" % (N, B, k), "all_layer", got, ref)
