@@ -232,6 +232,8 @@ def main():
     ap.add_argument("--mixed-slides", type=int, default=32, help="--mode mixed: slides in the batch")
     ap.add_argument("--no-graphs", action="store_true", help="eager launches instead of HIP graph replay")
     ap.add_argument("--no-cpu-full", action="store_true", help="skip the full C1/C2 CPU forwards")
+    ap.add_argument("--no-c4-ref", action="store_true",
+                    help="N = 1: skip the 256k-slide line (the workload the N > 1 runs shard)")
     ap.add_argument("--dry-run", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
@@ -429,6 +431,27 @@ def main():
         result["sp_exchange_exposed_ms_per_layer_max"] = max(
             r["exchange_exposed"]["ms_per_layer"] for r in reps)
         result["sp_transport"] = "rccl" if backend == "nccl" else backend + " (host-staged rehearsal)"
+    if world == 1 and plain and args.tiles == 70000 and not args.no_c4_ref:
+        # the C4 256k slide on this one GPU, same process: the N > 1 lines shard THIS workload, so their
+        # speedup over this line (not over the 70k `value`) is the sequence-parallel scaling
+        x4, c4 = make_slide(256000, seed=1)
+        x4t, c4t = torch.from_numpy(x4).to(dev), torch.from_numpy(c4).to(dev)
+        del x4, c4
+        print("bench: C4 256k reference line on this GPU ...", file=sys.stderr, flush=True)
+        with torch.no_grad():
+            for _ in range(2):
+                model(x4t, c4t, all_layer_embed=True)
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for _ in range(3):
+                model(x4t, c4t, all_layer_embed=True)
+            torch.cuda.synchronize(dev)
+            e4 = time.perf_counter() - t0
+        result["c4_256k_same_gpu"] = {
+            "workload": "C4 slide (256,000 tiles) forward on this one GPU, all_layer_embed=True, HIP-graph replay",
+            "tiles_per_s": round(256000 * 3 / e4, 2), "ms_per_step": round(e4 / 3 * 1e3, 3), "steps": 3,
+            "note": "the N > 1 lines shard this workload: their speedup over this line is the C4 scaling"}
+        del x4t, c4t
     if rank == 0 and not args.no_cpu_baseline:
         threads, usable, ncpu, _ = host_cores()
         threads = args.cpu_threads or threads
