@@ -900,9 +900,15 @@ Plan make_plan(int64_t M, int64_t N, int64_t K, bool allow_split) {
   p.n_dp = (int)tiles;
   p.rem = 0;
   p.ws_bytes = 0;
-  const int S = K == 768 ? 2 : 4;
+#ifndef GP_GEMM_SPLIT_SHORT
+#define GP_GEMM_SPLIT_SHORT 2
+#endif
+#ifndef GP_GEMM_SPLIT_LONG
+#define GP_GEMM_SPLIT_LONG 4
+#endif
+  const int S = K == 768 ? GP_GEMM_SPLIT_SHORT : (K == 3072 ? GP_GEMM_SPLIT_LONG : 4);
   const int64_t rem = tiles % p.G;
-  if (allow_split && tiles > p.G && rem > 0 && rem * S <= p.G && rem * 2 <= p.G) {
+  if (allow_split && S > 1 && tiles > p.G && rem > 0 && rem * S <= p.G && rem * 2 <= p.G) {
     p.S = S;
     p.n_dp = (int)(tiles - rem);
     p.rem = rem;
@@ -956,7 +962,8 @@ int launch(GemmArgs g, const Plan& p, hipStream_t s) {
   auto go = [&](auto nkc, auto ntc) {
     constexpr int NKc = decltype(nkc)::value;
     constexpr bool NTc = decltype(ntc)::value && kNtOk;
-    if (kSplit && p.S > 1) gemm_kernel<NKc, kSplit ? (NKc == 12 ? 2 : 4) : 1, EPI, kH, NTc><<<grid, block, 0, s>>>(g);
+    constexpr int Sc = NKc == 12 ? GP_GEMM_SPLIT_SHORT : (NKc == 48 ? GP_GEMM_SPLIT_LONG : 4);
+    if (kSplit && Sc > 1 && p.S > 1) gemm_kernel<NKc, (kSplit && Sc > 1) ? Sc : 1, EPI, kH, NTc><<<grid, block, 0, s>>>(g);
     else gemm_kernel<NKc, 1, EPI, kH, NTc><<<grid, block, 0, s>>>(g);
   };
   auto go_nt = [&](auto nkc) {
