@@ -19,11 +19,11 @@ timeout -k 10 300 python bench.py --tiles 256000 --steps 5 --warmup 2 --no-cpu-b
 rc=$?; echo "bench256k rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python bench.py --mode mixed --steps 3 --warmup 2 --no-cpu-baseline > $OUT/bench_c5.json 2> $OUT/bench_c5.err
 rc=$?; echo "benchC5 rc=$rc"; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python bench.py --no-cpu-baseline > $OUT/prof.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python bench.py --no-cpu-baseline --no-c4-ref > $OUT/prof.log 2>&1
 rc=$?; echo "rocprof rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python tools/fp16_caller_bench.py > $OUT/fp16_caller.log 2>&1
 rc=$?; echo "fp16 caller rc=$rc"; tail -4 $OUT/fp16_caller.log; [ $rc -eq 0 ] || exit $rc
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc/fetch -o run -- python bench.py --no-cpu-baseline --steps 1 --warmup 1 > $OUT/pmc_fetch.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc/fetch -o run -- python bench.py --no-cpu-baseline --no-c4-ref --steps 1 --warmup 1 > $OUT/pmc_fetch.log 2>&1
 rc=$?; echo "pmc fetch rc=$rc"; [ $rc -eq 0 ] || exit $rc
-timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc/write -o run -- python bench.py --no-cpu-baseline --steps 1 --warmup 1 > $OUT/pmc_write.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc/write -o run -- python bench.py --no-cpu-baseline --no-c4-ref --steps 1 --warmup 1 > $OUT/pmc_write.log 2>&1
 rc=$?; echo "pmc write rc=$rc"; exit $rc
