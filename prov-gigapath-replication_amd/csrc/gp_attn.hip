@@ -492,8 +492,8 @@ static_assert(kNWFast == 4 || kNWFast == 8 || kNWFast == 16, "GP_ATTN_NW must be
 #ifndef GP_ATTN_FP16_EXACT
 #define GP_ATTN_FP16_EXACT 1
 #endif
-// Measured lab variants of this kernel (the 16x16x32 P.V GP_ATTN_PV16, the 3-slot ring GP_ATTN_RING3) live
-// in tools/attn_lab/gp_attn_r3_lab.hip.
+// Measured lab variants of this kernel (the 16x16x32 P.V GP_ATTN_PV16, the 3-slot ring GP_ATTN_RING3) build
+// from round 3's source in git (make -C tools/attn_lab r3lab).
 
 template <int D, bool kPre, int MODE, bool kTab, int NW, bool kH>
 __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_idx) {

@@ -51,6 +51,12 @@
 
 namespace {
 
+// GP_LAB_EPI (lab builds only, tools/attn_lab `make full`; 0 in the product): timing-only ablations of the
+// epilogues, results deliberately wrong -- 1: no residual x loads (x = 0), 2: no x stores, 4: no 16-bit
+// output stores (xb / h / C), 8: no GELU evaluation (h = the packed pre-activation)
+#ifndef GP_LAB_EPI
+#define GP_LAB_EPI 0
+#endif
 constexpr int kBM = 256, kBN = 256, kBK = 64;
 constexpr int kThreads = 512;
 constexpr int kRowB = kBK * 2;                // 128-byte LDS rows
@@ -409,6 +415,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
       // gives the other case.  (NT: non-temporal stores for wide, short-K outputs, see launch().)
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
+        if constexpr ((GP_LAB_EPI & 4) != 0) continue;
         __builtin_amdgcn_raw_buffer_store_b128(hh ? Y : X, rc, c_lane, mi * c_mi + hh * c_hi, NT ? 2 : 0);
         __builtin_amdgcn_sched_barrier(0);
         asm volatile("s_nop 1");
@@ -461,8 +468,10 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
       f32x4v xv[2][4];
       auto load_x = [&](int mi) {
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni)
-          xv[mi & 1][ni] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rx, x_lane, mi * x_mi + ni * 64, 0));
+        for (int ni = 0; ni < 4; ++ni) {
+          if constexpr ((GP_LAB_EPI & 1) != 0) xv[mi & 1][ni] = f32x4v{0.f, 0.f, 0.f, 0.f};
+          else xv[mi & 1][ni] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rx, x_lane, mi * x_mi + ni * 64, 0));
+        }
       };
       load_x(0);
       load_x(1);
@@ -480,10 +489,12 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
           }
           const f32x4v v = xv[mi & 1][ni] + yv;   // the reference's order: x + (y + b), y kept in fp32
           typedef int i32x4 __attribute__((ext_vector_type(4)));
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), rx, x_lane, mi * x_mi + ni * 64, 0);
-          __builtin_amdgcn_sched_barrier(0);
-          asm volatile("s_nop 1");   // the store-data hazard (see the C stores below)
-          __builtin_amdgcn_sched_barrier(0);
+          if constexpr ((GP_LAB_EPI & 2) == 0) {
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), rx, x_lane, mi * x_mi + ni * 64, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_nop 1");   // the store-data hazard (see the C stores below)
+            __builtin_amdgcn_sched_barrier(0);
+          }
           const f32x4v dv = v - sh;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
@@ -537,7 +548,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
               xp[ni][e] = pack2e<false>(acc[mi][ni][2 * e], acc[mi][ni][2 * e + 1]);
-              hp[mi][ni][e] = gelu_lut_pair(xp[ni][e], bad);
+              if constexpr ((GP_LAB_EPI & 8) != 0) hp[mi][ni][e] = xp[ni][e];
+              else hp[mi][ni][e] = gelu_lut_pair(xp[ni][e], bad);
             }
           if (__builtin_amdgcn_ballot_w64(bad) != 0) {   // a |x| < 2^-16 or > 5.53 in this m-frag (rare)
 #pragma unroll
@@ -890,6 +902,17 @@ struct Plan {
   int64_t ws_bytes;
 };
 
+#ifndef GP_GEMM_SPLIT_SHORT
+#define GP_GEMM_SPLIT_SHORT 2
+#endif
+#ifndef GP_GEMM_SPLIT_LONG
+#define GP_GEMM_SPLIT_LONG 4
+#endif
+// K-split factor of the tail round for a K loop of nk K-tiles: ONE definition, used by make_plan and by
+// launch's kernel choice (round 4 had two, and a plan whose split the launched kernel did not share left
+// its tail tiles uncomputed: DESIGN §10, "r04_y")
+constexpr int split_for_nk(int nk) { return nk == 12 ? GP_GEMM_SPLIT_SHORT : (nk == 48 ? GP_GEMM_SPLIT_LONG : 4); }
+
 // the last partial round split in K when it is at most half full (S = 4, or 2 for K = 768)
 Plan make_plan(int64_t M, int64_t N, int64_t K, bool allow_split) {
   Plan p;
@@ -900,13 +923,7 @@ Plan make_plan(int64_t M, int64_t N, int64_t K, bool allow_split) {
   p.n_dp = (int)tiles;
   p.rem = 0;
   p.ws_bytes = 0;
-#ifndef GP_GEMM_SPLIT_SHORT
-#define GP_GEMM_SPLIT_SHORT 2
-#endif
-#ifndef GP_GEMM_SPLIT_LONG
-#define GP_GEMM_SPLIT_LONG 4
-#endif
-  const int S = K == 768 ? GP_GEMM_SPLIT_SHORT : (K == 3072 ? GP_GEMM_SPLIT_LONG : 4);
+  const int S = split_for_nk((int)(K / kBK));
   const int64_t rem = tiles % p.G;
   if (allow_split && S > 1 && tiles > p.G && rem > 0 && rem * S <= p.G && rem * 2 <= p.G) {
     p.S = S;
@@ -959,12 +976,26 @@ int launch(GemmArgs g, const Plan& p, hipStream_t s) {
   constexpr bool kSplit = !epi_gelu<EPI>;   // (the GELU plan never splits)
   // nt only for the epilogues whose output is a plain wide activation (QKV / fc1 / their LN-fold forms)
   constexpr bool kNtOk = !epi_res<EPI> && EPI != kEpiLnFoldResid;
+  // The plan must be one the launched kernel computes completely: unsplit (every tile data-parallel), or
+  // split by exactly the factor the kernel instantiation carries for this K -- a tail outside the
+  // data-parallel range with no matching split kernel would be skipped silently (round 4's r04_y failure).
+  const int64_t ntiles = ((int64_t)(g.M + kBM - 1) / kBM) * (g.N / kBN);
+  GP_REQUIRE(p.S == 1 ? (p.rem == 0 && p.n_dp == ntiles)
+                      : (kSplit && g.K % kBK == 0 && p.S == split_for_nk(g.K / kBK) && p.rem > 0 &&
+                         p.n_dp + p.rem == ntiles && p.rem * p.S <= p.G && p.n_dp % p.G == 0),
+             "GEMM epilogue %d: inconsistent tile plan (S=%d, n_dp=%d, rem=%lld, tiles=%lld, K=%d)", EPI, p.S, p.n_dp,
+             (long long)p.rem, (long long)ntiles, g.K);
   auto go = [&](auto nkc, auto ntc) {
     constexpr int NKc = decltype(nkc)::value;
     constexpr bool NTc = decltype(ntc)::value && kNtOk;
-    constexpr int Sc = NKc == 12 ? GP_GEMM_SPLIT_SHORT : (NKc == 48 ? GP_GEMM_SPLIT_LONG : 4);
-    if (kSplit && Sc > 1 && p.S > 1) gemm_kernel<NKc, (kSplit && Sc > 1) ? Sc : 1, EPI, kH, NTc><<<grid, block, 0, s>>>(g);
-    else gemm_kernel<NKc, 1, EPI, kH, NTc><<<grid, block, 0, s>>>(g);
+    constexpr int Sc = split_for_nk(NKc);
+    if constexpr (kSplit && Sc > 1) {
+      if (p.S > 1) {   // (== Sc: checked above)
+        gemm_kernel<NKc, Sc, EPI, kH, NTc><<<grid, block, 0, s>>>(g);
+        return;
+      }
+    }
+    gemm_kernel<NKc, 1, EPI, kH, NTc><<<grid, block, 0, s>>>(g);
   };
   auto go_nt = [&](auto nkc) {
     if (nt) go(nkc, std::true_type());

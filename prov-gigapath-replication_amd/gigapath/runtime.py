@@ -601,7 +601,10 @@ class EncoderEngine:
     def _stream_key(dev) -> int:
         return int(torch.cuda.current_stream(dev).cuda_stream) if torch.device(dev).type == "cuda" else 0
 
-    max_stream_workspaces = 4
+    # (8 = LongNetViT.max_capture_streams: the documented 4-stream concurrent pattern plus the default stream
+    # and the capture side streams stay cached; beyond it an eager call on yet another stream evicts the least
+    # recently used workspace and reallocates its own -- correct, but hundreds of MB per call at 20-70k tiles)
+    max_stream_workspaces = 8
 
     def _cached(self, table, key, make):
         sk = self._stream_key(self._dev_of(key))
@@ -630,6 +633,12 @@ class EncoderEngine:
         key = (str(dev), tuple(int(x) for x in Ls), E, F, H, tuple(segs), tuple(ratios), act)
         self.pws = self._cached(self._pws, key, lambda: PackedWorkspace(dev, Ls, E, F, H, segs, ratios, act))
         return self.pws
+
+    def stream_workspace(self, stream, packed: bool = False):
+        """The workspace the engine keeps for `stream` (the one a forward issued on that stream used),
+        or None."""
+        table = self._pws if packed else self._ws
+        return table.get(int(stream.cuda_stream)) if stream is not None else None
 
     def detach_workspace(self, ws) -> None:
         """Forget `ws` (a HIP graph's baked workspace): the next eager call on its stream allocates a new

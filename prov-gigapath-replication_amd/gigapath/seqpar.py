@@ -585,9 +585,10 @@ class SeqParallelEngine:
             return
         runtime.replay_graph(g)
 
-    def run_layers(self, layers, ws: ShardWorkspace, layer_hook=None, weights_sig=None):
-        """ws.x holds this shard's fp32 embedding, ws.a = LN1_0(ws.x) and ws.shift[0] its row means
-        (gp_posembed_cls_ln).  Runs every layer in place.
+    def run_layers(self, layers, ws: ShardWorkspace, layer_hook=None, weights_sig=None, shift_ready: bool = False):
+        """ws.x holds this shard's fp32 embedding and ws.a = LN1_0(ws.x); shift_ready: ws.shift[0] already
+        holds the row means of ws.x (gp_posembed_cls_ln's row_mean), otherwise they are computed here (as
+        runtime.EncoderEngine.run_layers does).  Runs every layer in place.
         Per layer: [QKV GEMM + sparsify] -> all-to-alls (phase A, phase B) -> wait A -> attention A
         -> wait B -> [attention B + merge + out-proj + residual + FFN + residual (runtime's residual
         epilogues; the round-3 residual/LN passes where they do not apply)]; with use_graphs the two
@@ -607,6 +608,8 @@ class SeqParallelEngine:
             self.graphs.clear()
             self._graph_sig = wsig
         fused = bool(layers) and all(pl.resid_fused for pl in layers) and ws.fstats is not None
+        if fused and not shift_ready:
+            torch.mean(ws.x, 1, out=ws.shift[0])
         for li, pl in enumerate(layers):
             pa = pl.attn
             nxt = layers[li + 1] if li + 1 < nl else None

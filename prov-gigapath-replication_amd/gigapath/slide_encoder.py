@@ -280,7 +280,7 @@ class LongNetViT(nn.Module):
         ent = self._graph_lookup(key)
         if ent is None and self._graph_wanted(key):
             ent = self._capture(key, x, c, lambda sx, sc: self._forward_device(sx, sc, all_layer_embed, False),
-                                lambda: self.encoder.engine.ws)
+                                lambda st: self.encoder.engine.stream_workspace(st, packed=False))
         return ent
 
     def _graph_lookup(self, key):
@@ -318,6 +318,22 @@ class LongNetViT(nn.Module):
         return tot
 
     @staticmethod
+    def _tensors_of(obj, seen=None):
+        """Every CUDA tensor reachable from a workspace object / list / tuple (once each)."""
+        seen = set() if seen is None else seen
+        if isinstance(obj, torch.Tensor):
+            if obj.is_cuda and id(obj) not in seen:
+                seen.add(id(obj))
+                yield obj
+            return
+        if obj is None or isinstance(obj, (int, float, str, bool)) or id(obj) in seen:
+            return
+        seen.add(id(obj))
+        items = obj if isinstance(obj, (list, tuple)) else (obj.__dict__.values() if hasattr(obj, "__dict__") else ())
+        for v in items:
+            yield from LongNetViT._tensors_of(v, seen)
+
+    @staticmethod
     def _weights_sig(key):
         """(top weights signature, encoder (device, param_signature)) of a graph key, whose last two
         entries are self._top_sig and EncoderEngine._sig = (device, param_signature, act)."""
@@ -327,7 +343,8 @@ class LongNetViT(nn.Module):
     def _capture(self, key, x, c, run, workspace):
         """Capture run(static_x, static_coords) -> outputs on the side stream (after one eager
         warm-up run there: allocations, TunableOp lookups) and cache it under `key`, keeping the
-        workspace the graph bakes in (workspace() after the warm-up) alive with it."""
+        workspace the graph bakes in (workspace(capture stream): the one the captured run itself used,
+        not whichever the engine used last) alive with it."""
         # superseded weights never replay: drop graphs whose (top, encoder) WEIGHT signatures differ.
         # The encoder signature's activation format is left out of that comparison (it stays in the
         # lookup key): a bf16 and an fp16 caller each keep their graphs, as pack() keeps one packing
@@ -354,8 +371,17 @@ class LongNetViT(nn.Module):
         # the graph bakes this shape's workspace: keep it alive with the graph (and ONLY with it: the
         # engine forgets it, so evicting the graph frees it); evict least recently used graphs beyond
         # the entry and byte budgets
-        ws = workspace()
+        ws = workspace(stream)
+        if ws is None:
+            raise RuntimeError("HIP graph capture: no engine workspace recorded for the capture stream")
         self.encoder.engine.detach_workspace(ws)
+        # The workspace was allocated on the capture stream, but the graph replays on the caller stream
+        # `cur` (part of the key).  The caching allocator orders a freed block's reuse only against its
+        # allocation stream, so without this, dropping the graph (LRU eviction, new weights) while a replay
+        # is still queued on `cur` could hand its memory to another allocation.  record_stream
+        # makes each block's free wait for the work queued on `cur` at that moment.
+        for t in self._tensors_of((ws, sx, sc, outs)):
+            t.record_stream(cur)
         nbytes = self._tensor_bytes(ws) + sx.untyped_storage().nbytes() + sc.untyped_storage().nbytes()
         while self._graphs and (len(self._graphs) >= self.max_hip_graphs or
                                 sum(self._graph_bytes.values()) + nbytes > self.hip_graph_max_bytes):
@@ -413,7 +439,7 @@ class LongNetViT(nn.Module):
             if ent is None and self._graph_wanted(key):
                 ent = self._capture(key, x_cat, c_cat,
                                     lambda sx, sc: self._forward_packed_device(sx, sc, Ns, all_layer_embed),
-                                    lambda: self.encoder.engine.pws)
+                                    lambda st: self.encoder.engine.stream_workspace(st, packed=True))
             if ent is None:
                 res = self._forward_packed_device(x_cat, c_cat, Ns, all_layer_embed)
             else:
@@ -593,7 +619,7 @@ class LongNetViT(nn.Module):
 
         if all_layer_embed:
             readout(0)
-        spe.run_layers(layers, ws, readout if all_layer_embed else None, weights_sig=eng._sig)
+        spe.run_layers(layers, ws, readout if all_layer_embed else None, weights_sig=eng._sig, shift_ready=True)
         if not all_layer_embed:
             if self.global_pool:
                 _hip.layernorm_f32(ws.x, E, top["enc_w"], top["enc_b"], top["enc_eps"], ws.x, ws.n, E)

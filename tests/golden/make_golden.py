@@ -239,8 +239,54 @@ def add_e2e(N, B=1):
     print("e2e", N, B, "done %.1fs" % (time.time() - t0))
 
 
+TINY_CASES = ((1, 1), (2, 1), (31, 1), (255, 1), (257, 1), (1023, 1), (5, 3))
+
+
+def add_tiny():
+    """The tiny / ragged slides of tests/test_gpu_model.py::test_tiny_and_ragged_slides_* as reference
+    fixtures: python tests/golden/make_golden.py --tiny  (seconds).
+
+    Weights = the tests' model fixture (oracle.make_weights(cfg, seed=0), no perturbation).  Per case the
+    reference's fp32 all_layer_embed output AND the same reference model run in bf16 (weights and input
+    cast, as for the N = 1024 case above), so the tests can bound the build's bf16 deviation by the
+    reference's OWN bf16 deviation at that size instead of a flat tolerance.  The deviation is recorded
+    per output vector, as tests/test_gpu_model.py::check_vectors measures it (max|d| / max|ref| of each
+    [E] vector), worst over the vectors."""
+    t0 = time.time()
+    se, _, _ = ref_harness.load_reference()
+    arch = "gigapath_slide_enc12l768d"
+    cfg = orc.arch_config(arch)
+    with open(os.path.join(HERE, "golden_meta.json")) as f:
+        meta = json.load(f)
+    W = orc.make_weights(cfg, seed=0)
+    model = se.create_model("", arch, 1536).eval()
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()}, strict=True)
+    mb = copy.deepcopy(model).to(torch.bfloat16)
+    arrs, ents = {}, []
+    for N, B in TINY_CASES:
+        x, coords = orc.synthetic_slide(N, B=B)
+        xt, ct = torch.from_numpy(x), torch.from_numpy(coords)
+        with torch.no_grad():
+            allv = torch.stack(model(xt, ct, all_layer_embed=True), 0).numpy()
+            bfv = torch.stack(mb(xt.bfloat16(), ct, all_layer_embed=True), 0).float().numpy()
+        vec = [float(np.abs(bfv[i] - allv[i]).max() / np.abs(allv[i]).max()) for i in np.ndindex(*allv.shape[:-1])]
+        arrs["N%d_B%d_fp32" % (N, B)] = allv
+        arrs["N%d_B%d_bf16" % (N, B)] = bfv
+        ents.append({"N": N, "B": B, "x_sha256": sha(x), "coords_sha256": sha(coords),
+                     "ref_bf16_rel_vec_max": max(vec),
+                     "ref_bf16_rel_inf": float(np.abs(bfv - allv).max() / np.abs(allv).max())})
+        print("tiny", N, B, "ref bf16 worst-vector rel %.3e" % max(vec))
+    save("tiny_slides.npz", **arrs)
+    meta["tiny"] = {"weights_sha256": orc.weights_sha256(W), "cases": ents}
+    with open(os.path.join(HERE, "golden_meta.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+    print("tiny done %.1fs" % (time.time() - t0))
+
+
 if __name__ == "__main__":
-    if len(sys.argv) == 3 and sys.argv[1] == "--e2e":
+    if len(sys.argv) == 2 and sys.argv[1] == "--tiny":
+        add_tiny()
+    elif len(sys.argv) == 3 and sys.argv[1] == "--e2e":
         add_e2e(int(sys.argv[2]))
     else:
         main()

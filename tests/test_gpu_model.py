@@ -4,6 +4,8 @@ Tolerance: the build runs in bf16 and is compared with the referen
 the reference's OWN bf16-vs-fp32 deviation at N=1024 is 1.0-1.4e-2 (max|d|/max|ref|), so the
 acceptance is max|d|/max|ref| <= max(2e-2, 1.5 x that) and cosine >= 0.9995 per output.
 """
+import hashlib
+
 import numpy as np
 import pytest
 import torch
@@ -425,32 +427,75 @@ def test_classification_head_logits(model):
     assert head.classifier[0].weight.grad is not None
 
 
-@pytest.mark.parametrize("N,B", [(1, 1), (2, 1), (31, 1), (255, 1), (257, 1), (1023, 1), (5, 3)])
-def test_tiny_and_ragged_slides_vs_oracle(model, N, B):
-    """Edge cases of the token count L = N + 1 (the CLS row included) against the fp32 oracle: one-tile
-    slides (every GEMM a single partial 256-row tile, attention segments of 2 tokens), lengths one short of /
-    one past a 256-row tile, one short of the 1,024-token segment, and a batch of three 5-tile slides --
-    eager and through the HIP-graph replay (each shape captured on first reuse)."""
-    Wt = {k: torch.from_numpy(v) for k, v in orc.make_weights(CFG, seed=0).items()}   # the fixture's weights
+def _tiny_case(golden_meta, N, B):
+    """(fp32 reference output, the reference's own worst per-vector bf16 deviation) of a tiny / ragged slide
+    (tests/golden/make_golden.py --tiny: the reference itself, the model fixture's weights)."""
+    ent = [e for e in golden_meta["tiny"]["cases"] if e["N"] == N and e["B"] == B][0]
     x, coords = orc.synthetic_slide(N, B=B)
-    ref = torch.stack(orc.slide_encoder_forward(Wt, x, coords, CFG, all_layer_embed=True)).numpy()
+    sha = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()   # noqa: E731
+    assert sha(x) == ent["x_sha256"] and sha(coords) == ent["coords_sha256"]
+    g = load_golden("tiny_slides.npz")
+    return x, coords, g["N%d_B%d_fp32" % (N, B)], ent["ref_bf16_rel_vec_max"]
+
+
+def check_tiny(test, got, ref, ref_dev):
+    """Every [E] output vector within max(north-star 1e-2, 1.5 x the REFERENCE's own bf16-vs-fp32
+    deviation at this size, worst vector) of the fp32 reference, cosine >= 0.9995 (verdict r04 item 5:
+    the bound is pinned by the reference's own noise, not a flat 2e-2)."""
+    tol = max(NORTH_STAR_REL, 1.5 * ref_dev)
+    worst_rel, worst_cos = 0.0, 1.0
+    for idx in np.ndindex(*got.shape[:-1]):
+        g, r = np.asarray(got[idx], np.float64), np.asarray(ref[idx], np.float64)
+        rel = np.abs(g - r).max() / np.abs(r).max()
+        cos = (g * r).sum() / np.sqrt((g * g).sum() * (r * r).sum())
+        assert rel <= tol and cos >= 0.9995, (test, idx, rel, cos, tol)
+        worst_rel, worst_cos = max(worst_rel, rel), min(worst_cos, cos)
+    record_parity(test + " (ref's own bf16 dev %.2e)" % ref_dev, "all_layer", worst_rel, worst_cos, tol, 0.9995,
+                  int(np.prod(got.shape[:-1])))
+
+
+@pytest.mark.parametrize("N,B", [(1, 1), (2, 1), (31, 1), (255, 1), (257, 1), (1023, 1), (5, 3)])
+def test_tiny_and_ragged_slides_vs_reference(model, golden_meta, N, B):
+    """Edge cases of the token count L = N + 1 (the CLS row included) against the reference's fp32 output
+    (tests/golden/tiny_slides.npz): one-tile slides (every GEMM a single partial 256-row tile, attention
+    segments of 2 tokens), lengths one short of / one past a 256-row tile, one short of the 1,024-token
+    segment, and a batch of three 5-tile slides -- eager and through the HIP-graph replay (each shape
+    captured on first reuse).  Bound: check_tiny (the reference's own bf16 deviation here is 1.4-2.0e-2)."""
+    x, coords, ref, ref_dev = _tiny_case(golden_meta, N, B)
     xt, ct = torch.from_numpy(x).to(DEV), torch.from_numpy(coords).to(DEV)
     with torch.no_grad():
         outs = [torch.stack(model(xt, ct, all_layer_embed=True)).cpu().numpy() for _ in range(3)]
     for k, got in enumerate(outs):
-        check_vectors("tiny/ragged N=%d B=%d run %d" % (N, B, k), "all_layer", got, ref)
+        check_tiny("tiny/ragged N=%d B=%d run %d" % (N, B, k), got, ref, ref_dev)
     assert np.array_equal(outs[1], outs[2])     # graph replays agree with each other bit for bit
 
 
 @pytest.mark.parametrize("N,B", [(1, 1), (257, 1), (5, 3)])
-def test_tiny_and_ragged_slides_fp16_caller_vs_oracle(model, N, B):
-    """The same edge cases under the reference pipeline's fp16 autocast (fp16 GEMMs and GELU, the exact
-    fp16 attention kernel) against the fp32 oracle."""
-    Wt = {k: torch.from_numpy(v) for k, v in orc.make_weights(CFG, seed=0).items()}
-    x, coords = orc.synthetic_slide(N, B=B)
-    ref = torch.stack(orc.slide_encoder_forward(Wt, x, coords, CFG, all_layer_embed=True)).numpy()
+def test_tiny_and_ragged_slides_fp16_caller_vs_reference(model, golden_meta, N, B):
+    """The same edge cases under the reference pipeline's fp16 autocast (fp16 GEMMs and GELU, the fp16
+    attention) against the reference's fp32 output, same bound."""
+    x, coords, ref, ref_dev = _tiny_case(golden_meta, N, B)
     xt, ct = torch.from_numpy(x).to(DEV).half(), torch.from_numpy(coords).to(DEV)
     with torch.no_grad(), torch.autocast("cuda", dtype=torch.float16):
         outs = [torch.stack(model(xt, ct, all_layer_embed=True)).float().cpu().numpy() for _ in range(2)]
     for k, got in enumerate(outs):
-        check_vectors("tiny/ragged fp16 N=%d B=%d run %d" % (N, B, k), "all_layer", got, ref)
+        check_tiny("tiny/ragged fp16 N=%d B=%d run %d" % (N, B, k), got, ref, ref_dev)
+
+
+@pytest.mark.parametrize("bad", [float("nan"), float("inf")])
+def test_nonfinite_tile_propagates_like_reference(model, bad):
+    """One non-finite feature in one tile: the reference's torch ops turn every layer output after the
+    embedding into NaN (the tile's k / v row poisons every segment that holds it, then the CLS row), while
+    the layer-0 readout (the CLS token before any layer) stays finite.  The kernels are built with
+    -fno-honor-nans (csrc/Makefile: v_max without NaN canonicalisation); this pins that the NaN still
+    propagates exactly as in the oracle instead of being absorbed by a max ("NaN inputs")."""
+    Wt = {k: torch.from_numpy(v) for k, v in orc.make_weights(CFG, seed=0).items()}
+    x, coords = orc.synthetic_slide(300)
+    x[0, 7, 5] = bad
+    ref = torch.stack(orc.slide_encoder_forward(Wt, x, coords, CFG, all_layer_embed=True)).numpy()
+    xt, ct = torch.from_numpy(x).to(DEV), torch.from_numpy(coords).to(DEV)
+    with torch.no_grad():
+        for _ in range(2):                          # eager, then the captured graph
+            got = torch.stack(model(xt, ct, all_layer_embed=True)).cpu().numpy()
+            assert np.array_equal(np.isnan(got), np.isnan(ref)), [int(np.isnan(got[i]).sum()) for i in range(13)]
+            assert np.isfinite(got[0]).all() and np.isnan(ref[1:]).all()

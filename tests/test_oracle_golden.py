@@ -120,3 +120,28 @@ def test_end_to_end_golden_c2_16k(golden_meta):
     with torch.no_grad():
         allv = torch.stack(orc.slide_encoder_forward(W, x, coords, CFG, all_layer_embed=True)).numpy()
     np.testing.assert_allclose(allv, g["all_layer"], rtol=0, atol=1e-4 * np.abs(g["all_layer"]).max())
+
+
+def test_tiny_slides_golden(golden_meta):
+    """The oracle on the tiny / ragged slides (N = 1, 2, 31, 255, 257, 1023 and 3 x 5 tiles) against the
+    reference's own fp32 outputs (tests/golden/tiny_slides.npz, make_golden.py --tiny), which also hold the
+    reference's bf16 run that pins the GPU tests' tolerance there (test_gpu_model.check_tiny)."""
+    g = load_golden("tiny_slides.npz")
+    W = orc.make_weights(CFG, seed=0)
+    assert orc.weights_sha256(W) == golden_meta["tiny"]["weights_sha256"]
+    Wt = {k: torch.from_numpy(v) for k, v in W.items()}
+    torch.set_num_threads(min(8, torch.get_num_threads()))
+    for ent in golden_meta["tiny"]["cases"]:
+        N, B = ent["N"], ent["B"]
+        if N > 300:                 # (N = 1023: ~1 min of oracle on the CPU; the GPU test still uses it)
+            continue
+        x, coords = orc.synthetic_slide(N, B=B)
+        assert sha(x) == ent["x_sha256"] and sha(coords) == ent["coords_sha256"]
+        with torch.no_grad():
+            allv = torch.stack(orc.slide_encoder_forward(Wt, x, coords, CFG, all_layer_embed=True)).numpy()
+        ref = g["N%d_B%d_fp32" % (N, B)]
+        np.testing.assert_allclose(allv, ref, rtol=0, atol=1e-4 * np.abs(ref).max())
+        # the recorded deviation is what the bf16 fixture shows, vector by vector
+        bf = g["N%d_B%d_bf16" % (N, B)]
+        vec = max(float(np.abs(bf[i] - ref[i]).max() / np.abs(ref[i]).max()) for i in np.ndindex(*ref.shape[:-1]))
+        assert vec == pytest.approx(ent["ref_bf16_rel_vec_max"], rel=1e-6)
