@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GP_ABI_VERSION 7
+#define GP_ABI_VERSION 8
 #define GP_EARG (-1)
 #define GP_MAX_BRANCHES 8
 #define GP_MAX_DESTS 8
@@ -37,6 +37,11 @@ extern "C" {
  * parameters, LSEs and readouts stay fp32 in both. */
 #define GP_FMT_BF16 0
 #define GP_FMT_F16 1
+/* fp16, except the V third of a fused [M, 3E] q | k | v buffer, which is bf16 (ABI 8).  Written by
+ * gp_linear / gp_linear_ln (output columns [2N/3, N) in bf16) and read by gp_dilated_attn_fwd(_ex) /
+ * gp_dilated_attn_fwd_varlen (fp16 S = Q.K^T, bf16 P and P.V, fp16 o): the reference pipeline's fp16
+ * autocast caller at the bf16 kernel's speed.  Other entry points take GP_FMT_F16. */
+#define GP_FMT_F16_VBF16 2
 
 /* ABI version of the loaded library (== GP_ABI_VERSION). */
 int gp_abi_version(void);

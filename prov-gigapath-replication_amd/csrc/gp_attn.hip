@@ -443,8 +443,12 @@ constexpr uint32_t kLseRedo = 0x7fc0dead;
 //     K/V tiles (global loads, addresses computed once), for k / v layouts the descriptor cannot
 //     cover (the operator seam's separate q / k / v tensors) and for D = 64.
 //   kModeExact (D = 48, q pre-scaled): the LDS-DMA staging and work decomposition of kModeFast with the
-//     exact running-max arithmetic, the -m start as the accumulator's initial value: the fp16 product
-//     kernel (GP_ATTN_FP16_EXACT below; the tile-0-offset fp16 fast mode, kM0, stays as the lab variant).
+//     exact running-max arithmetic, the -m start as the accumulator's initial value: fp16 q / k / v
+//     (GP_FMT_F16; the reference pipeline's fp16 caller when its V is fp16).
+// kH (fp16 operands) with kModeFast / kModeFix: the fp16 caller's product pair (GP_FMT_F16_VBF16): q and k
+//   fp16, S = K.Q^T on the fp16 MFMA, but V bf16 (the QKV GEMM writes the V third of qkv in bf16) so P
+//   and P.V are bf16 exactly as in the bf16 kernel -- the no-max p = 2^s needs bf16's range (fp16's ends at
+//   2^16), and the exact fp16 kernel's running max costs ~15 % of the launch.
 enum AttnMode { kModeFast = 0, kModeFix = 1, kModeGen = 2, kModeExact = 3 };
 // work items per fixup-pass block: the block reads the lse rows of kFixItems consecutive (LPT-ordered)
 // items and recomputes the flagged ones in turn.  4 (round 3): no-flag cost 1.2506 ms per 70k launch
@@ -479,18 +483,14 @@ static_assert(kNWFast == 4 || kNWFast == 8 || kNWFast == 16, "GP_ATTN_NW must be
 #ifndef GP_ATTN_ONES_SPARSE
 #define GP_ATTN_ONES_SPARSE 1
 #endif
-// GP_ATTN_FP16_EXACT (product: 1): the fp16 LDS-DMA launch is kModeExact, the exact running-max kernel
-// (lazy rescale), with no fixup pass.  0 (lab) restores round 2's fp16 fast mode (kModeFast with the
-// tile-0 offset + kModeFix): 6 % faster on random-init weights, but a row whose later keys score > 16
-// log2 units above tile 0's max overflows fp16 and its whole fixup block is recomputed serially --
-// measured 2.6x / 4.5x / 4.6x the exact kernel's time when q is 2 / 4 / 8 times sharper than random init
-// (0.05 % / 17 % / 66 % of the rows flagged; tools/fp16_flag_rate.py, profiles/r03_b_fp16_flag_rate.json).
+// fp16 formats of the LDS-DMA launch: GP_FMT_F16 (v fp16) runs kModeExact, the exact running-max kernel
+// (lazy rescale), no fixup pass; GP_FMT_F16_VBF16 (v bf16: the fp16 caller's fused QKV, round 5) runs the
+// bf16 product pair with fp16 S (kModeFast + kModeFix with kH).  Round 2's fp16 fast mode (p = 2^(s - m0),
+// m0 = tile 0's max, in fp16) is gone: with sharp attention its overflowing rows made it 2.6-4.6x slower
+// than the exact kernel (profiles/r03_b_fp16_flag_rate.json); P in bf16 has no such overflow.
 // GP_ATTN_NOFIX (lab only) skips the fixup pass, so flagged rows keep the kLseRedo marker for the count.
 #ifndef GP_ATTN_NOFIX
 #define GP_ATTN_NOFIX 0
-#endif
-#ifndef GP_ATTN_FP16_EXACT
-#define GP_ATTN_FP16_EXACT 1
 #endif
 // Measured lab variants of this kernel (the 16x16x32 P.V GP_ATTN_PV16, the 3-slot ring GP_ATTN_RING3) build
 // from round 3's source in git (make -C tools/attn_lab r3lab).
@@ -507,13 +507,12 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   constexpr int KS = D / 16;                 // k-steps of Q.K^T
   constexpr bool kOnes = (D % 32) != 0;      // spare d rows carry the row-sum ones
   constexpr bool kDMA = MODE != kModeGen;
-  constexpr bool kZM = MODE == kModeFast && !kH;   // no max, no offset
-  // fp16 fast mode: p = 2^(s - m0) with m0 the row max of tile 0 only (fp16's range ends at 2^16, so
-  // bf16's offset-free p = 2^s cannot be used); a later key more than 16 log2 units above m0
-  // overflows P to inf, the row is flagged and the fixup pass recomputes it exactly
-  constexpr bool kM0 = MODE == kModeFast && kH;
+  constexpr bool kZM = MODE == kModeFast;          // no max, no offset (P in bf16 for both formats)
   constexpr bool kFlag = MODE == kModeFast;        // flag rows for the fixup pass
-  constexpr bool kMI = MODE == kModeFix && !kH;    // -m start block from one MFMA (bf16 hi + lo pair)
+  constexpr bool kMI = MODE == kModeFix;           // -m start block from one MFMA (bf16 hi + lo pair)
+  // format of V, P and the P.V MFMA: fp16 only for the exact / register-staged fp16 kernels; the fp16
+  // caller's fast / fixup pair reads a bf16 V (GP_FMT_F16_VBF16)
+  constexpr bool kVH = kH && (MODE == kModeExact || MODE == kModeGen);
   constexpr int KROWB = D * 2 + 16;          // K image row bytes (padded)
   constexpr int VROWB = 128;                 // V image row bytes (64 bf16, swizzled 32-B blocks)
   constexpr int KTILE = KT * KROWB;
@@ -579,10 +578,10 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
       const int buf = idx / (2 * KT), rem = idx % (2 * KT), row = rem >> 1, half = rem & 1;
       char* const bb = smem + buf * BUF;
 #if GP_ATTN_ONES_SPARSE
-      constexpr uint32_t one = kH ? 0x3C00u : 0x3F80u;   // 1.0 in the operand format
+      constexpr uint32_t one = kVH ? 0x3C00u : 0x3F80u;   // 1.0 in V's format
       const uint4 ones = half ? make_uint4(0u, 0u, 0u, 0u) : make_uint4(one, 0u, one, 0u);
 #else
-      constexpr uint32_t one2 = kH ? 0x3C003C00u : 0x3F803F80u;
+      constexpr uint32_t one2 = kVH ? 0x3C003C00u : 0x3F803F80u;
       const uint4 ones = make_uint4(one2, one2, one2, one2);
 #endif
       *reinterpret_cast<uint4*>(bb + KTILE + row * VROWB + 32 * (3 ^ (row & 3)) + 16 * half) = ones;
@@ -758,7 +757,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
 
       // ---- online softmax with deferred rescale (two independent max chains)
       float mx = 0.f;
-      if (!kZM && (!kM0 || t == 0)) {
+      if (!kZM) {
         float mxa = sacc[0][0], mxb = sacc[1][0];
   #pragma unroll
         for (int r = 1; r < 16; ++r) {
@@ -774,7 +773,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
         if constexpr (!kZM) {
           // scores are s*c - m_run; rescale only when a query's max moved up by > kThr
           // (tile 0: always, which sets m_run to that tile's exact max)
-          const bool need = (t == 0) || (!kM0 && mx > kThr);
+          const bool need = (t == 0) || mx > kThr;
           if (__builtin_amdgcn_ballot_w64(need)) {
             if constexpr (kMI) {
               // m kept as an exact hi + lo pair of bf16 values (two rows of the init MFMA), so it
@@ -832,7 +831,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
             for (int e = 0; e < 8; ++e) {
               const float p = fast_exp2(sacc[u][8 * s + e]);
               if constexpr (!kOnes) lsum += p;
-              pf[u][s][e] = f2e_slot<kH>(p);
+              pf[u][s][e] = f2e_slot<kVH>(p);
             }
       } else {
         const float tm = mx * a.c_log2;
@@ -855,7 +854,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
             for (int e = 0; e < 8; ++e) {
               const float p = fast_exp2(fmaf(sacc[u][8 * s + e], a.c_log2, -m_run));
               if constexpr (!kOnes) lsum += p;
-              pf[u][s][e] = f2e_slot<kH>(p);
+              pf[u][s][e] = f2e_slot<kVH>(p);
             }
       }
 
@@ -873,7 +872,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
             const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
             const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p1);
             const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-            oacc[mt] = mfma_32x32x16<kH>(vf, pf[u][s], oacc[mt]);
+            oacc[mt] = mfma_32x32x16<kVH>(vf, pf[u][s], oacc[mt]);
           }
         }
 
@@ -1218,10 +1217,11 @@ extern "C" int gp_dilated_gather(const uint16_t* src, int64_t row_stride, int64_
   return gp_check_launch("gp_dilated_gather");
 }
 
-// kh: fp16 operands (the register-staged exact kernels); bf16 otherwise
+// fmt: GP_FMT_BF16, GP_FMT_F16 (fp16 q / k / v) or GP_FMT_F16_VBF16 (fp16 q / k, bf16 v; o fp16)
 static int attn_fwd_impl(const uint16_t* q, int64_t q_row_stride, int64_t q_tok_base, int64_t B, int64_t L, int H,
                          int D, int64_t win_lo, int64_t win_hi, const GpAttnBranch* branches, int nbranch,
-                         float softmax_scale, int q_log2_prescaled, bool kh, void* stream) {
+                         float softmax_scale, int q_log2_prescaled, int fmt, void* stream) {
+  const bool kh = fmt != GP_FMT_BF16;
   // bf16: the no-max LDS-DMA kernel + fixup pass (kModeFast / kModeFix) when the layout allows LDS-DMA
   // staging, else the register-staged exact kernel; fp16 likewise (its fast mode offsets p by the
   // row max of tile 0)
@@ -1258,6 +1258,8 @@ static int attn_fwd_impl(const uint16_t* q, int64_t q_row_stride, int64_t q_tok_
     kv_desc_ok = kv_desc_ok && dv >= 0 && rs2 >= dv + 2 * D && dv + 64 * (int64_t)d.ratio * rs2 < 0x7fffffff;
   }
   const bool fast = D == 48 && q_log2_prescaled && kv_desc_ok;   // LDS-DMA staging (8 waves x 32 queries)
+  GP_REQUIRE(fmt != GP_FMT_F16_VBF16 || fast,
+             "gp_dilated_attn_fwd: fmt F16_VBF16 needs D = 48, a pre-scaled q and k / v in one row layout");
   const int qblk = fast ? 32 * kNWFast : 128;   // query rows per workgroup
   // order branches by keys per work item (descending) so the longest items start first
   int order[GP_MAX_BRANCHES];
@@ -1320,16 +1322,15 @@ static int attn_fwd_impl(const uint16_t* q, int64_t q_row_stride, int64_t q_tok_
   a.ntab = 0;
   GP_REQUIRE(items < (int64_t)0x7fffffff, "gp_dilated_attn_fwd: too many work items");
   hipStream_t s = gp_stream(stream);
-  if (kh) {
-    if (fast) {        // fp16: the exact running-max kernel (GP_ATTN_FP16_EXACT above)
-      if constexpr (GP_ATTN_FP16_EXACT != 0) {
-        dilated_attn32_kernel<48, true, kModeExact, false, kNWFast, true><<<(unsigned)items, 64 * kNWFast, 0, s>>>(a);
-      } else {
-        dilated_attn32_kernel<48, true, kModeFast, false, kNWFast, true><<<(unsigned)items, 64 * kNWFast, 0, s>>>(a);
-        if constexpr (GP_ATTN_NOFIX == 0)
-          dilated_attn32_kernel<48, true, kModeFix, false, kNWFast, true>
-              <<<(unsigned)((items + kFixItems - 1) / kFixItems), 64 * kNWFast, 0, s>>>(a);
-      }
+  if (fmt == GP_FMT_F16_VBF16) {
+    // fp16 q / k, bf16 v: the bf16 product pair with the fp16 S MFMA (no max; fixup pass)
+    dilated_attn32_kernel<48, true, kModeFast, false, kNWFast, true><<<(unsigned)items, 64 * kNWFast, 0, s>>>(a);
+    if constexpr (GP_ATTN_NOFIX == 0)
+      dilated_attn32_kernel<48, true, kModeFix, false, kNWFast, true>
+          <<<(unsigned)((items + kFixItems - 1) / kFixItems), 64 * kNWFast, 0, s>>>(a);
+  } else if (kh) {
+    if (fast) {        // fp16 v: the exact running-max kernel
+      dilated_attn32_kernel<48, true, kModeExact, false, kNWFast, true><<<(unsigned)items, 64 * kNWFast, 0, s>>>(a);
     } else if (D == 96) dilated_attn_kernel<96, true><<<(unsigned)items, 256, 0, s>>>(a);
     else if (D == 48 && q_log2_prescaled) dilated_attn32_kernel<48, true, kModeGen, false, 4, true><<<(unsigned)items, 256, 0, s>>>(a);
     else if (D == 48) dilated_attn32_kernel<48, false, kModeGen, false, 4, true><<<(unsigned)items, 256, 0, s>>>(a);
@@ -1357,9 +1358,9 @@ extern "C" int gp_dilated_attn_fwd_ex(const uint16_t* q, int64_t q_row_stride, i
                                       int64_t L, int H, int D, int64_t win_lo, int64_t win_hi,
                                       const GpAttnBranch* branches, int nbranch, float softmax_scale,
                                       int q_log2_prescaled, int fmt, void* stream) {
-  GP_REQUIRE(fmt == GP_FMT_BF16 || fmt == GP_FMT_F16, "gp_dilated_attn_fwd: bad fmt %d", fmt);
+  GP_REQUIRE(fmt == GP_FMT_BF16 || fmt == GP_FMT_F16 || fmt == GP_FMT_F16_VBF16, "gp_dilated_attn_fwd: bad fmt %d", fmt);
   return attn_fwd_impl(q, q_row_stride, q_tok_base, B, L, H, D, win_lo, win_hi, branches, nbranch, softmax_scale,
-                       q_log2_prescaled, fmt == GP_FMT_F16, stream);
+                       q_log2_prescaled, fmt, stream);
 }
 
 extern "C" int gp_dilated_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, int64_t row_stride,
@@ -1399,7 +1400,8 @@ static int seg_attn(const uint16_t* q, const uint16_t* k, const uint16_t* v, int
   br.kv_sparse_cols = 0;
   br.o = o;
   br.lse = lse;
-  return attn_fwd_impl(q, (int64_t)H * D, 0, nbatch, seqlen, H, D, 0, seqlen, &br, 1, softmax_scale, 0, kh, stream);
+  return attn_fwd_impl(q, (int64_t)H * D, 0, nbatch, seqlen, H, D, 0, seqlen, &br, 1, softmax_scale, 0,
+                       kh ? GP_FMT_F16 : GP_FMT_BF16, stream);
 }
 
 extern "C" int gp_seg_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, int64_t nbatch,
@@ -1608,7 +1610,8 @@ static int varlen_header(const void* plan_host, const void* plan_dev, const char
 
 extern "C" int gp_dilated_attn_fwd_varlen(const void* plan_host, const void* plan_dev, int q_log2_prescaled,
                                           int fmt, void* stream) {
-  GP_REQUIRE(fmt == GP_FMT_BF16 || fmt == GP_FMT_F16, "gp_dilated_attn_fwd_varlen: bad fmt %d", fmt);
+  GP_REQUIRE(fmt == GP_FMT_BF16 || fmt == GP_FMT_F16 || fmt == GP_FMT_F16_VBF16, "gp_dilated_attn_fwd_varlen: bad fmt %d",
+             fmt);
   VarlenHdr h;
   if (int rc = varlen_header(plan_host, plan_dev, "gp_dilated_attn_fwd_varlen", h)) return rc;
   GP_REQUIRE(h.D == 48 && q_log2_prescaled, "gp_dilated_attn_fwd_varlen: needs D = 48 and a pre-scaled q (D=%d)", h.D);
@@ -1625,15 +1628,15 @@ extern "C" int gp_dilated_attn_fwd_varlen(const void* plan_host, const void* pla
   a.d_H = make_div_magic((uint32_t)h.H);
   // the single-slide default's variant, so each packed slide's outputs equal its own launch's
   if (fmt == GP_FMT_F16) {
-    if constexpr (GP_ATTN_FP16_EXACT != 0) {
-      dilated_attn32_kernel<48, true, kModeExact, true, kNWFast, true>
-          <<<(unsigned)h.total_items, 64 * kNWFast, 0, gp_stream(stream)>>>(a);
-    } else {
-      dilated_attn32_kernel<48, true, kModeFast, true, kNWFast, true>
-          <<<(unsigned)h.total_items, 64 * kNWFast, 0, gp_stream(stream)>>>(a);
-      dilated_attn32_kernel<48, true, kModeFix, true, kNWFast, true>
-          <<<(unsigned)((h.total_items + kFixItems - 1) / kFixItems), 64 * kNWFast, 0, gp_stream(stream)>>>(a);
-    }
+    dilated_attn32_kernel<48, true, kModeExact, true, kNWFast, true>
+        <<<(unsigned)h.total_items, 64 * kNWFast, 0, gp_stream(stream)>>>(a);
+    return gp_check_launch("gp_dilated_attn_fwd_varlen");
+  }
+  if (fmt == GP_FMT_F16_VBF16) {
+    dilated_attn32_kernel<48, true, kModeFast, true, kNWFast, true>
+        <<<(unsigned)h.total_items, 64 * kNWFast, 0, gp_stream(stream)>>>(a);
+    dilated_attn32_kernel<48, true, kModeFix, true, kNWFast, true>
+        <<<(unsigned)((h.total_items + kFixItems - 1) / kFixItems), 64 * kNWFast, 0, gp_stream(stream)>>>(a);
     return gp_check_launch("gp_dilated_attn_fwd_varlen");
   }
   dilated_attn32_kernel<48, true, kModeFast, true, kNWFast><<<(unsigned)h.total_items, 64 * kNWFast, 0, gp_stream(stream)>>>(a);

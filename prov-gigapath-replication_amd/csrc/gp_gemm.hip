@@ -9,7 +9,7 @@ extern "C" int64_t gp_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K) {
 extern "C" int gp_linear(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, const float* bias,
                          uint16_t* C, int64_t ldc, int64_t M, int64_t N, int64_t K, void* ws, int64_t ws_bytes,
                          int fmt, void* stream) {
-  if (int rc = check_shapes("gp_linear", A, lda, W, ldw, C, ldc, M, N, K, fmt)) return rc;
+  if (int rc = check_shapes("gp_linear", A, lda, W, ldw, C, ldc, M, N, K, fmt, true)) return rc;
   GP_REQUIRE(!bias || gp_aligned(bias, 16), "gp_linear: misaligned bias");
   const Plan p = make_plan(M, N, K, ws != nullptr);
   GP_REQUIRE(p.ws_bytes <= ws_bytes, "gp_linear: workspace of %lld bytes, %lld needed", (long long)ws_bytes,
@@ -20,7 +20,8 @@ extern "C" int gp_linear(const uint16_t* A, int64_t lda, const uint16_t* W, int6
   g.lda = lda; g.ldw = ldw; g.ldc = ldc;
   g.M = (int)M; g.N = (int)N; g.K = (int)K;
   g.ws = static_cast<float*>(ws);
-  const int lrc = fmt == GP_FMT_F16 ? launch<kEpiLinear, true, kKE | kKF>(g, p, gp_stream(stream)) : launch<kEpiLinear, false, kKE | kKF>(g, p, gp_stream(stream));
+  g.vcol0 = fmt == GP_FMT_F16_VBF16 ? (int)(2 * N / 3) : INT_MAX;
+  const int lrc = fmt != GP_FMT_BF16 ? launch<kEpiLinear, true, kKE | kKF>(g, p, gp_stream(stream)) : launch<kEpiLinear, false, kKE | kKF>(g, p, gp_stream(stream));
   if (lrc != 0) return lrc;
   return gp_check_launch("gp_linear");
 }

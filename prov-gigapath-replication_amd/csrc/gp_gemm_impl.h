@@ -41,6 +41,7 @@
 //     during the current tile's last phases; XCD-grouped tile order (one A row panel's N-tiles on one
 //     XCD's L2); the last partial round of tiles split in K when it is at most half full (fp32
 //     partials in the caller's workspace, summed by gemm_reduce_kernel with the same epilogue).
+#include <limits.h>
 #include <math.h>
 
 #include <type_traits>
@@ -53,7 +54,8 @@ namespace {
 
 // GP_LAB_EPI (lab builds only, tools/attn_lab `make full`; 0 in the product): timing-only ablations of the
 // epilogues, results deliberately wrong -- 1: no residual x loads (x = 0), 2: no x stores, 4: no 16-bit
-// output stores (xb / h / C), 8: no GELU evaluation (h = the packed pre-activation)
+// output stores (xb / h / C; a plain epilogue's MFMAs are then dead code), 8: no GELU evaluation (h = the
+// packed pre-activation), 16: the 16-bit output stores skipped by a run-time test (MFMAs stay live)
 #ifndef GP_LAB_EPI
 #define GP_LAB_EPI 0
 #endif
@@ -121,6 +123,8 @@ struct GemmArgs {
   int M, N, K;
   int nst;              // LN fold: statistics groups per row (F / 256)
   float eps;
+  int vcol0 = INT_MAX;  // fp16 (kH) plain / LN-fold outputs: columns >= vcol0 are stored in bf16 instead (the
+                        // V third of the fp16 caller's fused QKV, GP_FMT_F16_VBF16); INT_MAX: none
   int n_dp;             // tiles run data-parallel
   int split;            // 1: the remaining tiles are split in K (workspace ws)
   float* ws;
@@ -416,6 +420,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
         if constexpr ((GP_LAB_EPI & 4) != 0) continue;
+        if constexpr ((GP_LAB_EPI & 16) != 0) {   // stores predicated on a run-time-false test: no DCE
+          if (g.K >= 0) continue;
+        }
         __builtin_amdgcn_raw_buffer_store_b128(hh ? Y : X, rc, c_lane, mi * c_mi + hh * c_hi, NT ? 2 : 0);
         __builtin_amdgcn_sched_barrier(0);
         asm volatile("s_nop 1");
@@ -611,10 +618,18 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
         store_mfrag(mi, hp[mi]);
       } else {
         uint32_t pk[4][2];
+        if (kH && tn * kBN >= g.vcol0) {   // (wave-uniform) the bf16 V columns of an fp16 QKV
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) {
-          pk[ni][0] = pack2e<kH>(acc[mi][ni][0], acc[mi][ni][1]);
-          pk[ni][1] = pack2e<kH>(acc[mi][ni][2], acc[mi][ni][3]);
+          for (int ni = 0; ni < 4; ++ni) {
+            pk[ni][0] = pack2e<false>(acc[mi][ni][0], acc[mi][ni][1]);
+            pk[ni][1] = pack2e<false>(acc[mi][ni][2], acc[mi][ni][3]);
+          }
+        } else {
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni) {
+            pk[ni][0] = pack2e<kH>(acc[mi][ni][0], acc[mi][ni][1]);
+            pk[ni][1] = pack2e<kH>(acc[mi][ni][2], acc[mi][ni][3]);
+          }
         }
         store_mfrag(mi, pk);
       }
@@ -873,10 +888,17 @@ __global__ __launch_bounds__(256) void gemm_reduce_kernel(const GemmArgs g, int 
     }
   }
   uint4 o;
-  o.x = pack2e<kH>(v[0], v[1]);
-  o.y = pack2e<kH>(v[2], v[3]);
-  o.z = pack2e<kH>(v[4], v[5]);
-  o.w = pack2e<kH>(v[6], v[7]);
+  if (kH && !kRes && n >= g.vcol0) {   // the bf16 V columns of an fp16 QKV (see GemmArgs::vcol0)
+    o.x = pack2e<false>(v[0], v[1]);
+    o.y = pack2e<false>(v[2], v[3]);
+    o.z = pack2e<false>(v[4], v[5]);
+    o.w = pack2e<false>(v[6], v[7]);
+  } else {
+    o.x = pack2e<kH>(v[0], v[1]);
+    o.y = pack2e<kH>(v[2], v[3]);
+    o.z = pack2e<kH>(v[4], v[5]);
+    o.w = pack2e<kH>(v[6], v[7]);
+  }
   *reinterpret_cast<uint4*>(g.C + (int64_t)m * g.ldc + n) = o;
 }
 
@@ -941,8 +963,12 @@ bool gemm_k_supported(int64_t K) {
 }
 
 int check_shapes(const char* who, const void* A, int64_t lda, const void* W, int64_t ldw, const void* C, int64_t ldc,
-                 int64_t M, int64_t N, int64_t K, int fmt) {
-  GP_REQUIRE(fmt == GP_FMT_BF16 || fmt == GP_FMT_F16, "%s: bad fmt %d", who, fmt);
+                 int64_t M, int64_t N, int64_t K, int fmt, bool qkv_fmt_ok = false) {
+  GP_REQUIRE(fmt == GP_FMT_BF16 || fmt == GP_FMT_F16 || (qkv_fmt_ok && fmt == GP_FMT_F16_VBF16), "%s: bad fmt %d", who,
+             fmt);
+  GP_REQUIRE(fmt != GP_FMT_F16_VBF16 || (N % 3 == 0 && (2 * N / 3) % kBN == 0),
+             "%s: fmt F16_VBF16 needs a fused [q | k | v] output, N = 3E with 2E a multiple of %d (N=%lld)", who, kBN,
+             (long long)N);
   GP_REQUIRE(A && W && C, "%s: null pointer", who);
   GP_REQUIRE(M > 0 && M < (int64_t)0x7fffffff && N > 0 && K > 0, "%s: bad sizes", who);
   GP_REQUIRE(N % kBN == 0, "%s: N=%lld must be a multiple of %d", who, (long long)N, kBN);

@@ -15,7 +15,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_lib", "libgigapath_hip.so")
-ABI_VERSION = 7
+ABI_VERSION = 8
 MAX_BRANCHES = 8
 MAX_DESTS = 8
 
@@ -140,7 +140,7 @@ def _dev(t: torch.Tensor, dtype=None, name="tensor"):
     return t
 
 
-FMT_BF16, FMT_F16 = 0, 1            # GP_FMT_* (include/gigapath_hip.h)
+FMT_BF16, FMT_F16, FMT_F16_VBF16 = 0, 1, 2   # GP_FMT_* (include/gigapath_hip.h)
 ACT_DTYPES = (torch.bfloat16, torch.float16)
 
 
@@ -151,6 +151,13 @@ def fmt_of(dtype: torch.dtype) -> int:
     if dtype == torch.float16:
         return FMT_F16
     raise TypeError("gigapath HIP path: 16-bit activations must be bf16 or fp16 (got %s)" % dtype)
+
+
+def qkv_fmt_of(dtype: torch.dtype, v_bf16: bool) -> int:
+    """The format of a fused q | k | v buffer: fmt_of(dtype), or FMT_F16_VBF16 for an fp16 buffer whose V
+    third holds bf16 (written by linear / linear_ln with v_bf16, read by the attention entry points)."""
+    f = fmt_of(dtype)
+    return FMT_F16_VBF16 if (v_bf16 and f == FMT_F16) else f
 
 
 def _i32_array(vals: Sequence[int]):
@@ -204,9 +211,10 @@ def dilated_gather(src, row_stride, col_off, B, L, H, D, sl, r, dst):
 
 
 def dilated_attn_fwd(q, k, v, row_stride, B, L, H, D, segs, ratios, outs, lses, softmax_scale=0.0,
-                     q_log2_prescaled=False):
+                     q_log2_prescaled=False, v_bf16=False):
+    """v_bf16 (fp16 q only): v holds bf16 values (the fused QKV of linear(..., v_bf16=True)); o stays fp16."""
     lib = load_library()
-    fmt = fmt_of(q.dtype)
+    fmt = qkv_fmt_of(q.dtype, v_bf16)
     for t in (q, k, v):
         if not t.is_cuda or t.dtype != q.dtype:
             raise TypeError("q/k/v must be device tensors of one 16-bit dtype")
@@ -228,12 +236,12 @@ def attn_branch(sl, r, k, v, kv_row_stride, kv_tok_base, kv_sparse_cols, o, lse)
 
 
 def dilated_attn_fwd_ex(q, q_row_stride, q_tok_base, B, L, H, D, win_lo, win_hi, branches, softmax_scale=0.0,
-                        q_log2_prescaled=False):
-    """branches: sequence of GpAttnBranch (attn_branch)."""
+                        q_log2_prescaled=False, v_bf16=False):
+    """branches: sequence of GpAttnBranch (attn_branch).  v_bf16: as dilated_attn_fwd."""
     lib = load_library()
     if not q.is_cuda:
         raise TypeError("q must be a device tensor")
-    fmt = fmt_of(q.dtype)     # k / v / o of the descriptors are in q's format
+    fmt = qkv_fmt_of(q.dtype, v_bf16)     # k / o of the descriptors are in q's format, v too unless v_bf16
     arr = (GpAttnBranch * len(branches))(*branches)
     _check(lib.gp_dilated_attn_fwd_ex(_ptr(q), q_row_stride, q_tok_base, B, L, H, D, win_lo, win_hi,
                                       ctypes.cast(arr, c_vp), len(branches), float(softmax_scale),
@@ -392,9 +400,10 @@ class VarlenPlan:
         return self
 
 
-def dilated_attn_fwd_varlen(plan: VarlenPlan, q_log2_prescaled: bool = True):
+def dilated_attn_fwd_varlen(plan: VarlenPlan, q_log2_prescaled: bool = True, v_bf16: bool = False):
     lib = load_library()
-    _check(lib.gp_dilated_attn_fwd_varlen(plan.host, _ptr(plan.dev), int(bool(q_log2_prescaled)), plan.fmt,
+    fmt = FMT_F16_VBF16 if (v_bf16 and plan.fmt == FMT_F16) else plan.fmt
+    _check(lib.gp_dilated_attn_fwd_varlen(plan.host, _ptr(plan.dev), int(bool(q_log2_prescaled)), fmt,
                                           _stream()), "gp_dilated_attn_fwd_varlen")
 
 
@@ -435,10 +444,11 @@ def _ws(ws):
     return (None, 0) if ws is None else (ws.data_ptr(), ws.numel() * ws.element_size())
 
 
-def linear(a, w, bias, out, ws=None):
-    """out = a . w^T (+ bias): a [M, K], w [N, K], out [M, N] act; bias [N] fp32 or None."""
+def linear(a, w, bias, out, ws=None, v_bf16=False):
+    """out = a . w^T (+ bias): a [M, K], w [N, K], out [M, N] act; bias [N] fp32 or None.  v_bf16 (fp16 a, a
+    fused q | k | v output): the last third of out's columns is written in bf16 (FMT_F16_VBF16)."""
     lib = load_library()
-    fmt = fmt_of(a.dtype)
+    fmt = qkv_fmt_of(a.dtype, v_bf16)
     _rows(a, "a"); _rows(w, "w"); _rows(out, "out")
     if w.dtype != a.dtype or out.dtype != a.dtype:
         raise TypeError("linear: a, w and out must share one 16-bit dtype")
@@ -518,11 +528,12 @@ def linear_resid(a, w, bias, x, shift, gamma, xb, xstats, ws=None):
            "gp_linear_resid")
 
 
-def linear_ln(a, w, stats, nst, c, d, eps, s_in, s_out, out, ws=None):
+def linear_ln(a, w, stats, nst, c, d, eps, s_in, s_out, out, ws=None, v_bf16=False):
     """out = act(LN(x) . w^T + b) through the fold: a = xb = act(gamma * (x - s_in)), stats planes 0 .. nst-1
-    merged into plane nst (s_out = s_in + mean' when given), c = w . gamma, d = w . beta + b."""
+    merged into plane nst (s_out = s_in + mean' when given), c = w . gamma, d = w . beta + b.  v_bf16: as
+    linear."""
     lib = load_library()
-    fmt = fmt_of(a.dtype)
+    fmt = qkv_fmt_of(a.dtype, v_bf16)
     _rows(a, "a"); _rows(w, "w"); _rows(out, "out")
     if w.dtype != a.dtype or out.dtype != a.dtype:
         raise TypeError("linear_ln: a, w and out must share one 16-bit dtype")

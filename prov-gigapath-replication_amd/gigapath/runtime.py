@@ -213,6 +213,10 @@ class PackedAttention:
 
     prescaled: bool = True
     b_qkv_f32: Optional[torch.Tensor] = None   # [3E] fp32 (gp_linear's bias)
+    # fp16 packing only: the engine's QKV GEMMs write the V third of qkv in bf16 and the attention reads it so
+    # (GP_FMT_F16_VBF16): bf16 P.V at the bf16 kernel's speed instead of the exact fp16 running-max kernel
+    # (DESIGN §3.3).  Every engine producer and consumer of qkv passes it; the standalone module does not.
+    v_bf16: bool = False
 
     @staticmethod
     def from_module(m, dev, act: torch.dtype = torch.bfloat16) -> "PackedAttention":
@@ -229,7 +233,8 @@ class PackedAttention:
             w_o=_act(m.out_proj.weight, dev, act), b_o=_f32(m.out_proj.bias, dev),
             b_o_act=_act(m.out_proj.bias, dev, act),
             ln_w=_f32(m.inner_attn_ln.weight, dev), ln_b=_f32(m.inner_attn_ln.bias, dev),
-            ln_eps=float(m.inner_attn_ln.eps), prescaled=D in (48, 64))
+            ln_eps=float(m.inner_attn_ln.eps), prescaled=D in (48, 64),
+            v_bf16=(act == torch.float16 and D == 48 and OWN_GEMMS and _hip.gemm_supported(3 * E, E)))
 
 
 @dataclass
@@ -313,9 +318,10 @@ OWN_GEMMS = os.environ.get("GIGAPATH_OWN_GEMMS", "1") == "1"
 
 
 def linear(a: torch.Tensor, w: torch.Tensor, b_act: Optional[torch.Tensor], b_f32: Optional[torch.Tensor],
-           out: torch.Tensor, gemm_ws: Optional[torch.Tensor] = None):
+           out: torch.Tensor, gemm_ws: Optional[torch.Tensor] = None, v_bf16: bool = False):
     """out = a . w^T (+ b): nn.Linear on gp_linear when OWN_GEMMS and its instantiations cover the
-    shape, else hipBLASLt (torch.addmm / mm).  b_act / b_f32: the bias in the act format / fp32."""
+    shape, else hipBLASLt (torch.addmm / mm).  b_act / b_f32: the bias in the act format / fp32.
+    v_bf16: a fused fp16 QKV whose V third is written in bf16 (PackedAttention.v_bf16; own GEMM only)."""
     N, K = w.shape
     if OWN_GEMMS and a.is_cuda and _hip.gemm_supported(N, K) and (b_act is None or b_f32 is not None):
         if gemm_ws is not None and gemm_ws.numel() < _hip.gemm_workspace_bytes(a.shape[0], N, K):
@@ -325,12 +331,14 @@ def linear(a: torch.Tensor, w: torch.Tensor, b_act: Optional[torch.Tensor], b_f3
         if not _gemm_rows_ok(a):
             a = a.clone(memory_format=torch.contiguous_format)
         if _gemm_rows_ok(out):
-            _hip.linear(a, w, b_f32, out, gemm_ws)
+            _hip.linear(a, w, b_f32, out, gemm_ws, v_bf16=v_bf16)
         else:
             tmp = torch.empty(out.shape, dtype=out.dtype, device=out.device)
-            _hip.linear(a, w, b_f32, tmp, gemm_ws)
+            _hip.linear(a, w, b_f32, tmp, gemm_ws, v_bf16=v_bf16)
             out.copy_(tmp)
     else:
+        if v_bf16:
+            raise RuntimeError("runtime.linear: a bf16 V third needs the own GEMM (OWN_GEMMS and a covered shape)")
         with blaslt_serialized():
             if b_act is not None:
                 torch.addmm(b_act, a, w.t(), out=out)
@@ -422,7 +430,7 @@ def fused_qkv(pl: "PackedLayer", ws, qkv: torch.Tensor):
     pa = pl.attn
     E = pa.E
     _hip.linear_ln(ws.y, pa.w_qkv, ws.xstats, E // 256, pl.c_qkv, pl.d_qkv, pl.ln1_eps, ws.shift[1], ws.shift[0],
-                   qkv, ws.gemm_ws)
+                   qkv, ws.gemm_ws, v_bf16=pa.v_bf16)
 
 
 def fused_post_attention(pl: "PackedLayer", nxt: Optional["PackedLayer"], ws):
@@ -507,22 +515,23 @@ class VarlenScratch:
 
 
 def dilated_attention_core(pa: PackedAttention, qkv: torch.Tensor, B: int, L: int, scratch: AttentionScratch,
-                           out: torch.Tensor, inner_ln: bool = True):
-    """qkv: [B*L, 3E] 16-bit (q | k | v); out: [B*L, E] same format = inner_attn_ln(merge(branches)).
-    With a VarlenScratch (bound to this qkv), every packed slide in one launch each."""
+                           out: torch.Tensor, inner_ln: bool = True, v_bf16: bool = False):
+    """qkv: [B*L, 3E] 16-bit (q | k | v; v_bf16: an fp16 qkv whose V third is bf16, see PackedAttention);
+    out: [B*L, E] same format = inner_attn_ln(merge(branches)).  With a VarlenScratch (bound to this qkv),
+    every packed slide in one launch each."""
     E, H, D = pa.E, pa.H, pa.D
     if isinstance(scratch, VarlenScratch):
         if not pa.prescaled:
             raise RuntimeError("varlen packing needs the pre-scaled q of D = 48")
         with TIMER.span("attn"):
-            _hip.dilated_attn_fwd_varlen(scratch.plan, True)
+            _hip.dilated_attn_fwd_varlen(scratch.plan, True, v_bf16=v_bf16)
         with TIMER.span("merge"):
             _hip.branch_merge_ln_varlen(scratch.plan, pa.ln_w if inner_ln else None, pa.ln_b if inner_ln else None,
                                         pa.ln_eps, out)
         return
     with TIMER.span("attn"):
         _hip.dilated_attn_fwd(qkv, qkv[:, E:], qkv[:, 2 * E:], 3 * E, B, L, H, D, pa.segs, pa.ratios,
-                              scratch.outs, scratch.lses, 0.0, pa.prescaled)
+                              scratch.outs, scratch.lses, 0.0, pa.prescaled, v_bf16=v_bf16)
     with TIMER.span("merge"):
         _hip.branch_merge_ln(scratch.outs, scratch.lses, pa.segs, pa.ratios, B, L, H, D,
                              pa.ln_w if inner_ln else None, pa.ln_b if inner_ln else None, pa.ln_eps, out)
@@ -666,10 +675,10 @@ class EncoderEngine:
                 pa = pl.attn
                 with TIMER.span("gemm_qkv"):
                     if li == 0:
-                        linear(ws.a, pa.w_qkv, pa.b_qkv, pa.b_qkv_f32, ws.qkv, ws.gemm_ws)
+                        linear(ws.a, pa.w_qkv, pa.b_qkv, pa.b_qkv_f32, ws.qkv, ws.gemm_ws, v_bf16=pa.v_bf16)
                     else:
                         fused_qkv(pl, ws, ws.qkv)
-                dilated_attention_core(pa, ws.qkv, B, L, ws.attn, ws.a)
+                dilated_attention_core(pa, ws.qkv, B, L, ws.attn, ws.a, v_bf16=pa.v_bf16)
                 fused_post_attention(pl, self.layers[li + 1] if li + 1 < nl else None, ws)
                 if layer_hook is not None:
                     layer_hook(li + 1)
@@ -677,8 +686,8 @@ class EncoderEngine:
         for li, pl in enumerate(self.layers):
             pa = pl.attn
             with TIMER.span("gemm_qkv"):
-                linear(ws.a, pa.w_qkv, pa.b_qkv, pa.b_qkv_f32, ws.qkv, ws.gemm_ws)
-            dilated_attention_core(pa, ws.qkv, B, L, ws.attn, ws.a)
+                linear(ws.a, pa.w_qkv, pa.b_qkv, pa.b_qkv_f32, ws.qkv, ws.gemm_ws, v_bf16=pa.v_bf16)
+            dilated_attention_core(pa, ws.qkv, B, L, ws.attn, ws.a, v_bf16=pa.v_bf16)
             with TIMER.span("gemm_out"):
                 linear(ws.a, pa.w_o, None, None, ws.y, ws.gemm_ws)
             with TIMER.span("resid_ln"):

@@ -565,7 +565,7 @@ class SeqParallelEngine:
                                           ws.kv_base[b], True, ws.attn.outs[b], ws.attn.lses[b]))
         with runtime.TIMER.span("attn"):
             _hip.dilated_attn_fwd_ex(ws.qkv_ext, 3 * plan.E, a - ws.hq, 1, plan.L, plan.H, plan.D, a, e, descs, 0.0,
-                                     pa.prescaled)
+                                     pa.prescaled, v_bf16=pa.v_bf16)
 
     def _segment(self, key, fn):
         """Run fn (launches on the current stream only, no collectives, no host syncs); with
@@ -619,7 +619,7 @@ class SeqParallelEngine:
                     if fused and li > 0:
                         runtime.fused_qkv(pl, ws, ws.qkv)
                     else:
-                        runtime.linear(ws.a, pa.w_qkv, pa.b_qkv, pa.b_qkv_f32, ws.qkv, ws.gemm_ws)
+                        runtime.linear(ws.a, pa.w_qkv, pa.b_qkv, pa.b_qkv_f32, ws.qkv, ws.gemm_ws, v_bf16=pa.v_bf16)
                 self.sparsify(ws)
 
             def tail(pa=pa, pl=pl, nxt=nxt):

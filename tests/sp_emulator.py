@@ -137,7 +137,8 @@ def linear_resid(a, w, bias, x, shift, gamma, xb, xstats, ws=None):
     _resid_out(x, x[:M, :N] + y, shift, gamma, xb, xstats)
 
 
-def linear_ln(a, w, stats, nst, c, d, eps, s_in, s_out, out, ws=None):
+def linear_ln(a, w, stats, nst, c, d, eps, s_in, s_out, out, ws=None, v_bf16=False):
+    assert not v_bf16          # (the bf16 model: no bf16 V third in an fp16 buffer)
     M = a.shape[0]
     mean, rstd = _merge_stats(stats, nst, M, eps, s_in, s_out)
     acc = a.float() @ w.float().t()
@@ -211,8 +212,8 @@ def _kv_tensor(k, v, stride, sparse, H, D, r):
 
 
 def dilated_attn_fwd_ex(q, q_row_stride, q_tok_base, B, L, H, D, win_lo, win_hi, branches, softmax_scale=0.0,
-                        q_log2_prescaled=False):
-    assert B == 1 and q.shape[1] == q_row_stride
+                        q_log2_prescaled=False, v_bf16=False):
+    assert B == 1 and not v_bf16 and q.shape[1] == q_row_stride
     scale = 1.0 if q_log2_prescaled else (softmax_scale or D ** -0.5) / LN2   # -> log2-domain logits
     for br in branches:
         geo = orc.branch_geometry(L, br["sl"], br["r"], H)

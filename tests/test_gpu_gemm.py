@@ -433,3 +433,45 @@ def test_runtime_linear_takes_strided_and_offset_operands():
     big = torch.zeros(M, N + 4, dtype=torch.bfloat16, device=DEV)
     runtime.linear(a, w, b.bfloat16(), b, big[:, 4:])  # output rows 8 bytes off alignment
     assert torch.equal(big[:, 4:], ref)
+
+
+@pytest.mark.parametrize("M", [1, 4097, 70001])
+def test_fp16_qkv_with_bf16_v_third(M):
+    """GP_FMT_F16_VBF16 (round 5): gp_linear / gp_linear_ln of an fp16 fused QKV write the V third (columns
+    [2N/3, N)) in bf16 and the rest in fp16 -- each exactly the plain fp16 launch's fp32 result rounded to
+    its format (bit-identical q / k columns; V = bf16 of the same accumulators); split tail and unsplit."""
+    h = _hip()
+    E, N = 768, 2304
+    g = torch.Generator(device=DEV).manual_seed(M + 31)
+    a = _rand((M, E), g).half()
+    w = _rand((N, E), g, E ** -0.5).half()
+    b = _rand((N,), g, 0.1)
+    ref = a.float() @ w.float().t() + b
+    nb = h.gemm_workspace_bytes(M, N, E)
+    ws = torch.empty(max(nb, 16), dtype=torch.uint8, device=DEV)
+    for use_ws in (True, False):
+        plain = torch.empty(M, N, dtype=torch.float16, device=DEV)
+        h.linear(a, w, b, plain, ws if use_ws else None)
+        out = torch.full((M, N), float("nan"), dtype=torch.float16, device=DEV)
+        h.linear(a, w, b, out, ws if use_ws else None, v_bf16=True)
+        torch.cuda.synchronize()
+        assert torch.equal(out[:, :2 * E], plain[:, :2 * E])
+        vb = out[:, 2 * E:].view(torch.bfloat16).float()
+        assert torch.isfinite(vb).all()
+        assert _rel(vb, ref[:, 2 * E:]) <= 1e-2
+        # the V third is the bf16 rounding of the same accumulators the fp16 columns were rounded from
+        assert (vb - plain[:, 2 * E:].float()).abs().max().item() <= 2 ** -8 * plain[:, 2 * E:].float().abs().max().item()
+    # the LN-folded QKV (layers 1..): same split of formats
+    x, s, gam, bet, xb, st = _fold_setup(g, torch.float16, M, E, N)
+    c = (w.double() @ gam.double()).float()
+    d = (w.double() @ bet.double() + b.double()).float()
+    plain = torch.empty(M, N, dtype=torch.float16, device=DEV)
+    h.linear_ln(xb, w, st, E // 256, c, d, 1e-5, s, torch.empty(M, device=DEV), plain, ws)
+    out = torch.empty(M, N, dtype=torch.float16, device=DEV)
+    h.linear_ln(xb, w, st, E // 256, c, d, 1e-5, s, torch.empty(M, device=DEV), out, ws, v_bf16=True)
+    torch.cuda.synchronize()
+    assert torch.equal(out[:, :2 * E], plain[:, :2 * E])
+    vb = out[:, 2 * E:].view(torch.bfloat16).float()
+    assert (vb - plain[:, 2 * E:].float()).abs().max().item() <= 2 ** -8 * plain[:, 2 * E:].float().abs().max().item()
+    with pytest.raises(RuntimeError, match="F16_VBF16"):        # N = 512: not a fused q | k | v (N % 3 != 0)
+        h.linear(a, w[:512], b[:512], torch.empty(M, 512, dtype=torch.float16, device=DEV), ws, v_bf16=True)

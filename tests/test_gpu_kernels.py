@@ -377,6 +377,96 @@ def test_dilated_attention_fp16_vs_oracle(name, B, L, segs, ratios, prescaled):
         assert (l - l_ref).abs()[mask].max().item() <= 1.5e-3, (name, b)
 
 
+def _fp16_qkv_vbf16(qkv_f32, E):
+    """An fp16 [M, 3E] q | k | v buffer whose V third holds bf16 bit patterns (GP_FMT_F16_VBF16, the fp16
+    caller's fused QKV), and the fp32 values it represents."""
+    qkv16 = qkv_f32.half()
+    vb = qkv_f32[:, 2 * E:].bfloat16()
+    qkv16[:, 2 * E:] = vb.view(torch.float16)
+    ref = qkv16.float()
+    ref[:, 2 * E:] = vb.float()
+    return qkv16, ref
+
+
+@pytest.mark.parametrize("name,B,L,segs,ratios", ATTN_CASES)
+def test_dilated_attention_fp16_qk_bf16_v_vs_oracle(name, B, L, segs, ratios):
+    """GP_FMT_F16_VBF16 (the fp16 caller's product launch since round 5): fp16 q / k (S on the fp16 MFMA),
+    bf16 v, P and P.V in bf16 as in the bf16 product kernel (no max + fixup pass), o written fp16 -- so the
+    bf16 kernel's tolerances (P rounded to 8 significant bits)."""
+    h = _hip()
+    H, D = 16, 48
+    E = H * D
+    qkv = _rand_qkv(B, L, E, seed=L + 9).float()
+    qkv[:, :E] *= D ** -0.5 * 1.4426950408889634
+    qkv16, ref = _fp16_qkv_vbf16(qkv, E)
+    outs, lses = [], []
+    for sl, r in zip(segs, ratios):
+        geo = orc.branch_geometry(L, sl, r, H)
+        outs.append(torch.full((B * geo["nseg"] * geo["m"] * H * D,), float("nan"), dtype=torch.float16, device=DEV))
+        lses.append(torch.full((B * geo["nseg"] * H * geo["m"],), float("nan"), dtype=torch.float32, device=DEV))
+    qd = qkv16.to(DEV)
+    h.dilated_attn_fwd(qd, qd[:, E:], qd[:, 2 * E:], 3 * E, B, L, H, D, segs, ratios, outs, lses, 0.0, True,
+                       v_bf16=True)
+    torch.cuda.synchronize()
+    q, k, v = (ref[:, i * E:(i + 1) * E].view(B, L, H, D) for i in range(3))
+    for b, (sl, r) in enumerate(zip(segs, ratios)):
+        o_ref, l_ref = orc.branch_attention(q, k, v, sl, r, scale=0.6931471805599453)
+        geo = orc.branch_geometry(L, sl, r, H)
+        o = outs[b].float().cpu().view(B, geo["nseg"], geo["m"], H, D).permute(0, 1, 3, 2, 4)
+        l = lses[b].cpu().view(B, geo["nseg"], H, geo["m"])
+        need = _rows_needed(L, sl, r, H)
+        mask = torch.from_numpy(np.arange(geo["m"])[None, None, :] < need[:, :, None]).unsqueeze(0)
+        mask = mask.expand(B, -1, -1, -1)
+        assert torch.isfinite(o[mask]).all() and torch.isfinite(l[mask]).all(), (name, b)
+        assert (o - o_ref).abs()[mask].max().item() <= 1.2e-2 * max(1.0, o_ref.abs().max().item()), (name, b)
+        assert (l - l_ref).abs()[mask].max().item() <= LSE_ATOL, (name, b)
+
+
+def test_attention_fp16_qk_bf16_v_overflow_fixup():
+    """The no-max overflow case of test_attention_no_max_overflow_fixup in GP_FMT_F16_VBF16: a score of 200
+    log2 units (exp2 overflows fp32) and a 30-per-tile climb are flagged and recomputed by the exact fixup
+    pass, whose fp16 S MFMA starts from the bf16 hi + lo -m block."""
+    h = _hip()
+    B, L, H, D = 1, 300, 16, 48
+    E = H * D
+    qkv = _rand_qkv(B, L, E, seed=22).float() * 0.3
+    qkv[:, 0 * D:2 * D] = 0.0
+    qkv[:, 0 * D] = 8.0
+    qkv[:, 1 * D] = 8.0
+    qkv[:, E:E + 2 * D] = 0.0
+    qkv[150, E] = 25.0
+    qkv[:, E + D] = torch.from_numpy((np.arange(L) // 64) * 3.75).float()
+    qkv16, ref = _fp16_qkv_vbf16(qkv, E)
+    geo = orc.branch_geometry(L, 300, 1, H)
+    outs = [torch.full((L * H * D,), float("nan"), dtype=torch.float16, device=DEV)]
+    lses = [torch.full((H * L,), float("nan"), dtype=torch.float32, device=DEV)]
+    qd = qkv16.to(DEV)
+    h.dilated_attn_fwd(qd, qd[:, E:], qd[:, 2 * E:], 3 * E, B, L, H, D, [300], [1], outs, lses, 0.0, True, v_bf16=True)
+    torch.cuda.synchronize()
+    q, k, v = (ref[:, i * E:(i + 1) * E].view(B, L, H, D) for i in range(3))
+    o_ref, l_ref = orc.branch_attention(q, k, v, 300, 1, scale=0.6931471805599453)
+    o = outs[0].float().cpu().view(B, 1, L, H, D).permute(0, 1, 3, 2, 4)
+    l = lses[0].cpu().view(B, 1, H, L)
+    assert geo["m"] == L and torch.isfinite(o).all() and torch.isfinite(l).all()
+    assert (o - o_ref).abs().max().item() <= 1.2e-2 * max(1.0, o_ref.abs().max().item())
+    assert (l - l_ref).abs().max().item() <= LSE_ATOL + 1e-5 * l_ref.abs().max().item()
+    assert (o[0, 0, 0] - v[0, 150, 0]).abs().max().item() <= 1e-2 * max(1.0, v[0, 150, 0].abs().max().item())
+
+
+def test_fp16_qk_bf16_v_format_errors():
+    """GP_FMT_F16_VBF16 is refused where the bf16-V kernels do not apply (D = 64; not pre-scaled)."""
+    h = _hip()
+    B, L, H = 1, 64, 12
+    for D, pre in ((64, True), (48, False)):
+        E = H * D
+        qkv = torch.zeros(L, 3 * E, dtype=torch.float16, device=DEV)
+        outs = [torch.empty(L * H * D, dtype=torch.float16, device=DEV)]
+        lses = [torch.empty(H * L, dtype=torch.float32, device=DEV)]
+        with pytest.raises(RuntimeError, match="F16_VBF16"):
+            h.dilated_attn_fwd(qkv, qkv[:, E:], qkv[:, 2 * E:], 3 * E, B, L, H, D, [64], [1], outs, lses, 0.0, pre,
+                               v_bf16=True)
+
+
 # ------------------------------------------------------------------ branch merge
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("name,B,L,segs,ratios", ATTN_CASES[:4])
