@@ -492,6 +492,13 @@ static_assert(kNWFast == 4 || kNWFast == 8 || kNWFast == 16, "GP_ATTN_NW must be
 #ifndef GP_ATTN_NOFIX
 #define GP_ATTN_NOFIX 0
 #endif
+// GP_ATTN_SCHED (round 5, lab): 1 = the last, partial K/V tile of an item peeled off the LDS-DMA tile loop,
+// so a full tile's S, softmax and P.V are one basic block (no key-mask branch) the scheduler can interleave;
+// 2 = 1 + sched_group_barrier hints: the first sub-tile's exps inside the second sub-tile's S MFMAs, and
+// per P.V MFMA two V reads and four VALU (exps / conversions)
+#ifndef GP_ATTN_SCHED
+#define GP_ATTN_SCHED 0
+#endif
 // Measured lab variants of this kernel (the 16x16x32 P.V GP_ATTN_PV16, the 3-slot ring GP_ATTN_RING3) build
 // from round 3's source in git (make -C tools/attn_lab r3lab).
 
@@ -713,8 +720,9 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   // q-block of a segment) skips the MFMAs and the softmax -- its outputs are never stored -- and
   // only issues its share of the K/V staging and the barriers (~2 % of the wave-tiles at 70k)
   const bool wact = !GP_ATTN_SKIP_IDLE || __builtin_amdgcn_readfirstlane(q0 + w * 32) < rows_needed;
-  auto tile_step = [&](int t, auto setc) {
+  auto tile_step = [&](int t, auto setc, auto maskc) {
     constexpr int SET = decltype(setc)::value;
+    constexpr int MASK = decltype(maskc)::value;   // 0: full tile (no key mask), 1: partial, 2: run-time test
     if (t + 1 < ntiles) load_tile((t + 1) * KT, std::integral_constant<int, 1 - SET>());
     const int kv0 = t * KT;
     const char* Kb = kDMA ? (const char*)bufc(setc) : smem + (t & 1) * BUF;
@@ -747,7 +755,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
         }
         sacc[u] = acc;
       }
-      if (kv0 + 64 > c) {      // keys >= c are zero pads (added analytically at the end)
+      if (MASK == 1 || (MASK == 2 && kv0 + 64 > c)) {      // keys >= c are zero pads (added analytically at the end)
   #pragma unroll
         for (int u = 0; u < 2; ++u)
   #pragma unroll
@@ -875,19 +883,53 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
             oacc[mt] = mfma_32x32x16<kVH>(vf, pf[u][s], oacc[mt]);
           }
         }
+      if constexpr (GP_ATTN_SCHED >= 2 && kZM && MASK == 0) {
+        // one region from the K reads to the last P.V MFMA (see GP_ATTN_SCHED)
+        __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);   // K fragment reads
+        __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);     // S(u = 0) x 3, S(u = 1) k-step 0
+        __builtin_amdgcn_sched_group_barrier(0x2, 3, 0);     // exps of S(u = 0)
+        __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x2, 3, 0);
+        __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x2, 6, 0);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // V^T reads of this P.V MFMA
+          __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x2, 4, 0);
+        }
+      }
 
     }
     if (t + 1 < ntiles) store_tile((t + 1) & 1);
     if constexpr (kDMA) __builtin_amdgcn_s_waitcnt(0x0f70);   // this wave's DMA pieces landed
     __syncthreads();
   };
-  if constexpr (kDMA) {
+  using M0 = std::integral_constant<int, 0>;
+  using M1 = std::integral_constant<int, 1>;
+  using M2 = std::integral_constant<int, 2>;
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  if constexpr (kDMA && GP_ATTN_SCHED >= 1) {
+    // full tiles unmasked (one basic block each), the partial last tile on its own
+    const int nmain = (c % KT) != 0 ? ntiles - 1 : ntiles;
+    int t = 0;
+    for (; t + 1 < nmain; t += 2) {
+      tile_step(t, S0(), M0());
+      tile_step(t + 1, S1(), M0());
+    }
+    if (t < nmain) tile_step(t++, S0(), M0());
+    if (t < ntiles) {
+      if (t & 1) tile_step(t, S1(), M1());
+      else tile_step(t, S0(), M1());
+    }
+  } else if constexpr (kDMA) {
     for (int t = 0; t < ntiles; t += 2) {
-      tile_step(t, std::integral_constant<int, 0>());
-      if (t + 1 < ntiles) tile_step(t + 1, std::integral_constant<int, 1>());
+      tile_step(t, S0(), M2());
+      if (t + 1 < ntiles) tile_step(t + 1, S1(), M2());
     }
   } else {
-    for (int t = 0; t < ntiles; ++t) tile_step(t, std::integral_constant<int, 0>());
+    for (int t = 0; t < ntiles; ++t) tile_step(t, S0(), M2());
   }
 
   // ---- epilogue

@@ -55,7 +55,8 @@ namespace {
 // GP_LAB_EPI (lab builds only, tools/attn_lab `make full`; 0 in the product): timing-only ablations of the
 // epilogues, results deliberately wrong -- 1: no residual x loads (x = 0), 2: no x stores, 4: no 16-bit
 // output stores (xb / h / C; a plain epilogue's MFMAs are then dead code), 8: no GELU evaluation (h = the
-// packed pre-activation), 16: the 16-bit output stores skipped by a run-time test (MFMAs stay live)
+// packed pre-activation), 16: the 16-bit output stores skipped by a run-time test (MFMAs stay live),
+// 32 / 64: no W / A K-tile staging past K-tile 1 (the MFMAs read stale tiles)
 #ifndef GP_LAB_EPI
 #define GP_LAB_EPI 0
 #endif
@@ -250,6 +251,12 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
   const int n_my = sid < n_dp ? (n_dp - 1 - sid) / G + 1 : 0;
   const bool tail = S > 1 && g.split && sid < (ntiles - n_dp) * S;
   if (n_my == 0 && !tail) return;
+#ifdef GP_LAB_STAGGER
+  // lab: half of each XCD's workgroups start ~GP_LAB_STAGGER x 0.25 us late (desynchronises the CUs' tile
+  // boundaries, so their epilogue HBM bursts stop coinciding)
+  if (((int)blockIdx.x >> 3) & 1)
+    for (int z = 0; z < GP_LAB_STAGGER; ++z) __builtin_amdgcn_s_sleep(8);
+#endif
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const int wm = w >> 2, wn = w & 3;
@@ -293,6 +300,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
   auto issue = [&](auto opc, auto hc, auto bc, const __amdgpu_buffer_rsrc_t& rs, int kt) {
     constexpr int OP = decltype(opc)::value, H = decltype(hc)::value, B = decltype(bc)::value;
     char* dst = bufp<B>() + OP * kOpT + H * kHalf;
+    if constexpr ((GP_LAB_EPI & (OP == 0 ? 64 : 32)) != 0) {   // lab: no re-staging past K-tile 1
+      if (kt >= 2) return;
+    }
 #pragma unroll
     for (int j = 0; j < 2; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + (2 * w + j) * 1024),
