@@ -351,7 +351,8 @@ def main():
         mine = _b.lpt_assign([_b.slide_cost(n, segs, ratios) for n in sizes], world)[rank]
         att_flops_launch = sum(runtime.attention_valid_flops(sizes[i] + 1, segs, ratios, 16, 48) for i in mine)
     n_att, ms_att = kt.get("attn", (0, 0.0))
-    if sp:
+    if sp:          # (the SP engine labels its launches by exchange phase: attn_local / attn_A / attn_B)
+        ms_att = sum(v[1] for k, v in kt.items() if k.startswith("attn"))
         # this rank's attention launches cover its query window: price them with its share of the
         # valid FLOPs (two launches per layer: local branches, then exchanged ones)
         plan = model._sp.plan

@@ -255,6 +255,17 @@ class ShardPlan:
                 out.append((v, lo, hi))
         return out
 
+    def phase_pair_bytes(self, v: int, branches: Sequence[int], halo: bool) -> int:
+        """Bytes rank v receives over its busiest incoming link (one source rank) in one exchange phase."""
+        per: Dict[int, int] = {}
+        for b, w, lo, hi in self.recvs(v):
+            if b in branches:
+                per[w] = per.get(w, 0) + (hi - lo) * 2 * self.C[b] * 2
+        if halo:
+            for w, lo, hi in self.halo_recvs(v):
+                per[w] = per.get(w, 0) + (hi - lo) * 3 * self.E * 2
+        return max(per.values(), default=0)
+
     def exchange_bytes(self, v: int) -> int:
         """bf16 bytes rank v receives from other ranks per layer."""
         tot = sum((hi - lo) * 2 * self.C[b] * 2 for b, _, lo, hi in self.recvs(v))
@@ -423,8 +434,15 @@ class ShardWorkspace:
         self.f = torch.empty(self.n, F, dtype=act, device=dev)
         self.fstats, self.gemm_ws = runtime.ffn_buffers(dev, self.n, E, F)
         self.xstats, self.shift = runtime.resid_buffers(dev, self.n, E)
-        # per branch: K/V receive buffer = the need range in token order; send buffer packed by peer
+        # per branch: K/V receive buffer = the need range in token order.  W > 1: every peer's chunk is a row
+        # range of this rank's own tokens, so the own sparse rows are written ONCE -- those the rank needs
+        # itself straight into its receive buffer, and (only where the peers' chunks reach past that, as
+        # misaligned schedules do) the peers' row range into a send buffer -- and each peer is sent a view:
+        # round 4 wrote one copy per destination (up to 8) and let RCCL copy the self chunk.  W = 1 (the
+        # single-rank RCCL transport test): a send buffer and a self-only all-to-all, so the collective path
+        # still runs.
         self.kvs, self.kv_base, self.send, self.send_off = [], [], [], []
+        self.self_rng, self.peer_rng, self.send_base = [], [], []
         for b in range(len(plan.geo)):
             lo, hi = plan.need[rank][b]
             if plan.no_xfer[b]:              # keys come from qkv_ext (dense rows)
@@ -432,27 +450,63 @@ class ShardWorkspace:
                 lo = hi
             self.kvs.append(torch.empty(hi - lo, 2 * plan.C[b], dtype=act, device=dev))
             self.kv_base.append(lo)
-            splits = [0] * plan.world if plan.no_xfer[b] else plan.send_splits(rank, b)
-            self.send.append(torch.empty(sum(splits), 2 * plan.C[b], dtype=act, device=dev))
+            srng = _isect((a, e), (lo, hi)) if not plan.no_xfer[b] else (0, 0)
+            ch = [plan.chunk(rank, v, b) for v in range(plan.world) if v != rank]
+            ch = [c for c in ch if c[1] > c[0]] if not plan.no_xfer[b] else []
+            prng = (min(c[0] for c in ch), max(c[1] for c in ch)) if ch else (0, 0)
+            self.self_rng.append(srng)
+            in_self = prng[1] <= prng[0] or (srng[0] <= prng[0] and prng[1] <= srng[1])
+            self.peer_rng.append(None if in_self else prng)    # None: peers are sent views of kvs
+            if plan.world == 1:
+                splits = [0] if plan.no_xfer[b] else plan.send_splits(rank, b)
+                n_send = sum(splits)
+            else:
+                splits, n_send = [0] * plan.world, 0 if in_self else prng[1] - prng[0]
+            self.send.append(torch.empty(n_send, 2 * plan.C[b], dtype=act, device=dev))
             self.send_off.append(list(np.cumsum([0] + splits[:-1])))
+            self.send_base.append(prng[0])
         self.plan = plan
         # branch outputs keep the single-device layout; only the window's rows are written/read
         self.attn = runtime.AttentionScratch(dev, 1, plan.L, H, D, plan.segs, plan.ratios, act)
 
     def dest(self, b: int, v: int) -> Tuple[torch.Tensor, int]:
-        """(buffer, first row) where this rank's branch-b rows for rank v go: the send buffer's chunk."""
+        """(buffer, first row) where this rank's branch-b rows for rank v go: the send buffer's chunk (W = 1)."""
         assert not self.plan.no_xfer[b], "branch %d is read from qkv directly" % b
         return self.send[b], int(self.send_off[b][v])
+
+    def sparsify_dests(self, b: int) -> List[Tuple[int, int, torch.Tensor, int]]:
+        """W > 1: where sparsify writes this rank's own rows of branch b, (tok_lo, tok_hi, buffer, row)."""
+        out = []
+        lo, hi = self.self_rng[b]
+        if hi > lo:
+            out.append((lo, hi, self.kvs[b], lo - self.kv_base[b]))
+        if self.peer_rng[b] is not None:
+            lo, hi = self.peer_rng[b]
+            out.append((lo, hi, self.send[b], 0))
+        return out
+
+    def send_rows(self, b: int, lo: int, hi: int) -> torch.Tensor:
+        """W > 1: this rank's own rows [lo, hi) of branch b as a contiguous view (of kvs, or of the send buffer)."""
+        if self.peer_rng[b] is None:
+            return self.kv_rows(b, lo, hi)
+        return self.send[b][lo - self.send_base[b]:hi - self.send_base[b]]
+
+    def kv_rows(self, b: int, lo: int, hi: int) -> torch.Tensor:
+        """Rows of tokens [lo, hi) of branch b's receive buffer (a contiguous view)."""
+        base = self.kv_base[b]
+        return self.kvs[b][lo - base:hi - base]
 
 
 class SeqParallelEngine:
     """Runs the encoder layers of one rank's shard.  `layers` are runtime.PackedLayer."""
 
-    # True: the transfer-free branches' attention in a launch of its own before any wait (it would
-    # overlap every transfer).  Off: measured +1.05 ms of compute per 256k/8 rank forward (the long
-    # branches' launch loses its 32,768-token work items, r02_s10_sp_rank_probe_localfirst.json) against
-    # a modelled ~2 ms of exposed transfers at 64 GB/s per link -- not worth it unmeasured.
-    local_first = False
+    # True (round 5 default): the transfer-free branches' attention in a launch of its own before any
+    # wait, so it overlaps every transfer.  Measured per 256k/8 rank forward on one GPU
+    # (profiles/r05_sp1_sp_rank_probe_w1_w8.json, tools/sp_rank_probe.py): max rank compute 20.39 ms with it
+    # vs 19.11 ms without (+1.28 ms: the long branches' launch keeps 384 work items for 512 workgroup
+    # slots), but the modelled exposed transfer at 64 GB/s per xGMI link direction is 0 with it vs 1.6 ms
+    # without -- 20.39 vs 20.73 ms, and it stays exposure-free down to ~37 GB/s per link.
+    local_first = True
 
     def __init__(self, plan: ShardPlan, rank: int, exchange: Exchange):
         self.plan, self.rank, self.xch = plan, rank, exchange
@@ -467,7 +521,8 @@ class SeqParallelEngine:
         self._graph_sig = None
 
     def sparsify(self, ws: ShardWorkspace):
-        """This rank's sparsified K/V rows, written into every peer's chunk of the send buffers."""
+        """This rank's sparsified K/V rows: W > 1, once, into its own rows of the receive buffers (the
+        exchange sends views of them); W = 1, into the send buffer of the self-only all-to-all."""
         plan = self.plan
         a, e = plan.bounds[self.rank]
         E = plan.E
@@ -477,6 +532,9 @@ class SeqParallelEngine:
                 continue
             segs.append(plan.segs[b])
             ratios.append(plan.ratios[b])
+            if plan.world > 1:
+                dests.append(ws.sparsify_dests(b))
+                continue
             lst = []
             for v in range(plan.world):
                 lo, hi = plan.chunk(self.rank, v, b)
@@ -498,9 +556,28 @@ class SeqParallelEngine:
             sends = [(dst, ws.qkv[lo - a:hi - a]) for dst, lo, hi in self._hsends]
             recvs = [(src, ws.qkv_ext[lo - (a - ws.hq):hi - (a - ws.hq)]) for src, lo, hi in self._hrecvs]
             handles += self.xch.p2p(sends, recvs) or []
+        if plan.world == 1:
+            for b in branches:
+                if not plan.no_xfer[b]:
+                    handles += self.xch.all_to_all(ws.kvs[b], ws.send[b], self._rsplit[b], self._ssplit[b]) or []
+            return handles
+        # W > 1: one point-to-point group for every branch of the phase -- to each peer the row range of
+        # this rank's own rows it needs, from each peer its rows straight into the receive buffer (the
+        # chunks are in token order, so the receive buffer is the attention's K/V buffer as it stands)
+        sends, recvs = [], []
         for b in branches:
-            if not plan.no_xfer[b]:
-                handles += self.xch.all_to_all(ws.kvs[b], ws.send[b], self._rsplit[b], self._ssplit[b]) or []
+            if plan.no_xfer[b]:
+                continue
+            for v in range(plan.world):
+                if v == self.rank:
+                    continue
+                lo, hi = plan.chunk(self.rank, v, b)
+                if hi > lo:
+                    sends.append((v, ws.send_rows(b, lo, hi)))
+                lo, hi = plan.chunk(v, self.rank, b)
+                if hi > lo:
+                    recvs.append((v, ws.kv_rows(b, lo, hi)))
+        handles += self.xch.p2p(sends, recvs) or []
         return handles
 
     def _peers(self, branches: List[int]) -> List[int]:
@@ -546,7 +623,9 @@ class SeqParallelEngine:
         mon.disarm()
         mon._pending.append((li, ph, e0, e1))
 
-    def attention(self, pa: runtime.PackedAttention, ws: ShardWorkspace, branches: List[int]):
+    def attention(self, pa: runtime.PackedAttention, ws: ShardWorkspace, branches: List[int], span: str = "attn"):
+        """One windowed attention launch over `branches` (runtime.TIMER span `span`: the probe times the
+        overlap windows of the exchange phases by it)."""
         if not branches:
             return
         plan = self.plan
@@ -563,7 +642,7 @@ class SeqParallelEngine:
             kv = ws.kvs[b]
             descs.append(_hip.attn_branch(plan.segs[b], plan.ratios[b], kv, kv.data_ptr() + 2 * C, 2 * C,
                                           ws.kv_base[b], True, ws.attn.outs[b], ws.attn.lses[b]))
-        with runtime.TIMER.span("attn"):
+        with runtime.TIMER.span(span):
             _hip.dilated_attn_fwd_ex(ws.qkv_ext, 3 * plan.E, a - ws.hq, 1, plan.L, plan.H, plan.D, a, e, descs, 0.0,
                                      pa.prescaled, v_bf16=pa.v_bf16)
 
@@ -623,7 +702,7 @@ class SeqParallelEngine:
                 self.sparsify(ws)
 
             def tail(pa=pa, pl=pl, nxt=nxt):
-                self.attention(pa, ws, ph_b2 if plan.phase_b2 else ph_b1)
+                self.attention(pa, ws, ph_b2 if plan.phase_b2 else ph_b1, "attn_B")
                 with runtime.TIMER.span("merge"):
                     _hip.branch_merge_ln_window(ws.attn.outs, ws.attn.lses, plan.segs, plan.ratios, 1, plan.L, a, M,
                                                 H, D, pa.ln_w, pa.ln_b, pa.ln_eps, ws.a)
@@ -643,12 +722,12 @@ class SeqParallelEngine:
             h_a = self._post(ws, plan.phase_a, True, li, "A")
             h_b1 = self._post(ws, plan.phase_b1, False, li, "B1")
             h_b2 = self._post(ws, plan.phase_b2, False, li, "B2")
-            self.attention(pa, ws, local)          # needs no transfer: runs while they all fly
+            self.attention(pa, ws, local, "attn_local")   # needs no transfer: runs while they all fly
             self._wait(h_a, li, "A", plan.phase_a)
-            self.attention(pa, ws, ph_a)
+            self.attention(pa, ws, ph_a, "attn_A")
             self._wait(h_b1, li, "B1", plan.phase_b1)
             if plan.phase_b2:                      # the middle phase runs while the last transfers
-                self.attention(pa, ws, ph_b1)
+                self.attention(pa, ws, ph_b1, "attn_B1")
             self._wait(h_b2, li, "B2", plan.phase_b2)
             self._segment(("tail", li, wsig), tail)
             if layer_hook is not None:

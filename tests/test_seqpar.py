@@ -170,12 +170,10 @@ def _exchange_worker(rank, world, port, L, segs, ratios, q):
             t.fill_(float("nan"))
         ws.qkv_ext.fill_(float("nan"))
         ws.qkv.copy_(torch.from_numpy(qkv[a:e]).to(ws.qkv.dtype))
-        for b in range(len(segs)):                       # this rank's sparsified rows, packed per peer
-            for v in range(world):
-                lo, hi = plan.chunk(rank, v, b)
-                if hi <= lo or plan.no_xfer[b]:
-                    continue
-                buf, off = ws.dest(b, v)
+        for b in range(len(segs)):                       # this rank's sparsified rows, where sparsify writes
+            if plan.no_xfer[b]:                          # them (its own rows of the receive buffer and, if
+                continue                                 # the peers' chunks reach past those, a send buffer)
+            for lo, hi, buf, off in ws.sparsify_dests(b):
                 buf[off:off + hi - lo] = torch.from_numpy(ref[b][lo:hi]).to(buf.dtype)
         eng = seqpar.SeqParallelEngine(plan, rank, seqpar.Exchange())
         seqpar.Exchange.wait(eng.exchange(ws, list(range(len(segs))), halo=True))
