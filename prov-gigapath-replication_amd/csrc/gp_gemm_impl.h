@@ -253,7 +253,11 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
   if (n_my == 0 && !tail) return;
 #ifdef GP_LAB_STAGGER
   // lab: half of each XCD's workgroups start ~GP_LAB_STAGGER x 0.25 us late (desynchronises the CUs' tile
-  // boundaries, so their epilogue HBM bursts stop coinciding)
+  // boundaries, so their epilogue HBM bursts stop coinciding); GP_LAB_STAGGER_EPI: only for the fc1 (GELU)
+  // and fc2 (residual) epilogues
+#ifdef GP_LAB_STAGGER_EPI
+  if constexpr (EPI == kEpiLnFoldGelu || EPI == kEpiLnFoldResid)
+#endif
   if (((int)blockIdx.x >> 3) & 1)
     for (int z = 0; z < GP_LAB_STAGGER; ++z) __builtin_amdgcn_s_sleep(8);
 #endif
@@ -358,7 +362,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
   };
   auto sync = [&]() {
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
+    if constexpr ((GP_LAB_EPI & 256) == 0) __builtin_amdgcn_s_barrier();   // (lab 256: no K-loop barriers)
     __builtin_amdgcn_sched_barrier(0);
   };
 

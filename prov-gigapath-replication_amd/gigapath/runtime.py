@@ -308,7 +308,10 @@ class PackedLayer:
 
 
 FFN_FUSED = os.environ.get("GIGAPATH_FFN_FUSED", "1") != "0"
-# the residual adds + pre-LNs inside the out-proj / fc2 epilogues and the QKV / fc1 folds (round 4)
+# the residual adds + pre-LNs inside the out-proj / fc2 epilogues and the QKV / fc1 folds (round 4).
+# A deliberate trade: ~1 % slower in the HIP-graph forward than the round-3 sequence
+# (31.83 vs 31.55 ms, same box) for 2.3x more headroom under the north star's 1e-2 parity bound (C3
+# max-rel 6.94e-3 vs 8.65e-3: the residual stream is rounded once per layer fewer).  =0 picks speed.
 RESID_FUSED = os.environ.get("GIGAPATH_RESID_FUSED", "1") != "0"
 # the QKV / out-proj / patch projections on gp_linear (own MFMA GEMM, the default) instead of hipBLASLt.
 # With every GEMM of the forward on gp_gemm.hip kernels (persistent, data-parallel tiles, no workgroup ever
