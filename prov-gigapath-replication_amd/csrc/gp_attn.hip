@@ -473,6 +473,11 @@ constexpr int kNWFast = GP_ATTN_NW;
 #ifndef GP_ATTN_PRIO
 #define GP_ATTN_PRIO 1
 #endif
+// the fast kernel at three workgroups per CU (GP_ATTN_FAST_WPS, round 5): no static priority -- with six
+// waves per SIMD arbitration by age alone measured 1.1-1.8 % faster (profiles/r05_occ6b_*, r05_occ6c_*)
+#ifndef GP_ATTN_PRIO_FAST
+#define GP_ATTN_PRIO_FAST 0
+#endif
 static_assert(kNWFast == 4 || kNWFast == 8 || kNWFast == 16, "GP_ATTN_NW must be 4, 8 or 16");
 #ifndef GP_ATTN_SKIP_IDLE
 #define GP_ATTN_SKIP_IDLE 1
@@ -492,13 +497,26 @@ static_assert(kNWFast == 4 || kNWFast == 8 || kNWFast == 16, "GP_ATTN_NW must be
 #ifndef GP_ATTN_NOFIX
 #define GP_ATTN_NOFIX 0
 #endif
-// GP_ATTN_SCHED (round 5, lab): 1 = the last, partial K/V tile of an item peeled off the LDS-DMA tile loop,
-// so a full tile's S, softmax and P.V are one basic block (no key-mask branch) the scheduler can interleave;
-// 2 = 1 + sched_group_barrier hints: the first sub-tile's exps inside the second sub-tile's S MFMAs, and
-// per P.V MFMA two V reads and four VALU (exps / conversions)
-#ifndef GP_ATTN_SCHED
-#define GP_ATTN_SCHED 0
+// GP_ATTN_FAST_WPS (round 5): waves per SIMD the fast kernel's registers are sized for -- 6 = three 8-wave
+// workgroups per CU (<= 80 VGPRs, LDS 3 x 30 KiB), which needs the one-sub-tile-at-a-time order of its tile
+// body (S, exps and P.V of keys 0-31, then of keys 32-63: half the live S / P registers of the interleaved
+// order).  Against round 4's two workgroups per CU with both sub-tiles' S first: the new order at four waves
+// per SIMD is 6 % slower, at six 1.2-2.3 % faster per 70k launch (fp16 V-bf16 pair 1.5 %), bit-identical
+// (profiles/r05_occ6*_attn_ab_*.json, r05_occ6h_forward_ab_product_vs_r4order.json); the interleaved order
+// squeezed into 80 VGPRs spills 25 registers inside the loop (1.6x slower).  4 = round 4's kernel.
+#ifndef GP_ATTN_FAST_WPS
+#define GP_ATTN_FAST_WPS 6
 #endif
+// the same for the packed (varlen, work-table) fast kernel: 4 -- at 80 VGPRs its table decode leaves 2 spill
+// reloads per two tiles inside the loop, and the C5 launch measured 7 % slower at six waves per SIMD (12.09 vs
+// 11.30 ms, profiles/r05_occ6v_varlen_ab.json)
+#ifndef GP_ATTN_FAST_WPS_TAB
+#define GP_ATTN_FAST_WPS_TAB 4
+#endif
+// minimum waves per SIMD the kernel instantiation is sized for (HIP launch-bounds semantics; 2: no register
+// constraint at these sizes -- the fixup / exact / register-staged kernels, 104-138 VGPRs)
+template <int MODE, bool kTab>
+constexpr int attn_wps() { return MODE == 0 ? (kTab ? GP_ATTN_FAST_WPS_TAB : GP_ATTN_FAST_WPS) : 2; }
 // Measured lab variants of this kernel (the 16x16x32 P.V GP_ATTN_PV16, the 3-slot ring GP_ATTN_RING3) build
 // from round 3's source in git (make -C tools/attn_lab r3lab).
 
@@ -711,7 +729,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   // prefetch -- before the first MFMA of every tile
   __builtin_amdgcn_s_waitcnt(0x0f70);
 
-  if constexpr (GP_ATTN_PRIO != 0 && NW >= 8) {
+  if constexpr ((attn_wps<MODE, kTab>() >= 6 ? GP_ATTN_PRIO_FAST : GP_ATTN_PRIO) != 0 && NW >= 8) {
     if (__builtin_amdgcn_readfirstlane((int)threadIdx.x) >= NT / 2) __builtin_amdgcn_s_setprio(1);
   }
   // one 64-key tile; SET = the tile's LDS buffer when the loop is unrolled by two (kDMA), so the
@@ -720,14 +738,53 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   // q-block of a segment) skips the MFMAs and the softmax -- its outputs are never stored -- and
   // only issues its share of the K/V staging and the barriers (~2 % of the wave-tiles at 70k)
   const bool wact = !GP_ATTN_SKIP_IDLE || __builtin_amdgcn_readfirstlane(q0 + w * 32) < rows_needed;
-  auto tile_step = [&](int t, auto setc, auto maskc) {
+  auto tile_step = [&](int t, auto setc) {
     constexpr int SET = decltype(setc)::value;
-    constexpr int MASK = decltype(maskc)::value;   // 0: full tile (no key mask), 1: partial, 2: run-time test
     if (t + 1 < ntiles) load_tile((t + 1) * KT, std::integral_constant<int, 1 - SET>());
     const int kv0 = t * KT;
     const char* Kb = kDMA ? (const char*)bufc(setc) : smem + (t & 1) * BUF;
     const char* Vb = Kb + KTILE;
-    if (wact) {   // (GP_ATTN_SKIP_IDLE) waves with no needed query only stage K/V and join the barriers
+    if constexpr (attn_wps<MODE, kTab>() >= 6) {
+      // the fast kernel (GP_ATTN_FAST_WPS): one 32-key sub-tile at a time -- S, exps and P.V of sub-tile u before
+      // sub-tile u + 1's S -- so the body fits 80 VGPRs and three workgroups share each CU
+      if (wact) {
+  #pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          f32x16 acc;
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  #pragma unroll
+          for (int ks = 0; ks < KS; ++ks) {
+            const bf16x8 kk = *reinterpret_cast<const bf16x8*>(Kb + (32 * u + l32) * KROWB + 32 * ks + 16 * h);
+            acc = mfma_32x32x16<kH>(kk, qf[ks], acc);
+          }
+          if (kv0 + 64 > c) {
+  #pragma unroll
+            for (int r = 0; r < 16; ++r)
+              if (kv0 + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * h >= c) acc[r] = -INFINITY;
+          }
+          bf16x8 pu[2];
+  #pragma unroll
+          for (int s = 0; s < 2; ++s)
+  #pragma unroll
+            for (int e = 0; e < 8; ++e) pu[s][e] = f2e_slot<kVH>(fast_exp2(acc[8 * s + e]));
+  #pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const int row = 32 * u + 16 * s + 4 * (lane >> 5) + ((lane >> 2) & 3);
+  #pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+              const int blk = 2 * mt + ((lane >> 4) & 1);
+              const char* p0 = Vb + row * VROWB + 32 * (blk ^ (row & 3)) + 8 * (lane & 3);
+              const char* p1 = p0 + 8 * VROWB;
+              const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
+              const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p1);
+              const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+              oacc[mt] = mfma_32x32x16<kVH>(vf, pu[s], oacc[mt]);
+            }
+          }
+        }
+      }
+    } else if (wact) {   // (GP_ATTN_SKIP_IDLE) waves with no needed query only stage K/V and join the barriers
       // ---- S^T for two 32-key sub-tiles.  kPre (q pre-multiplied by scale*log2 e): the
       // accumulator starts at -m_run, so it already holds log2-domain scores minus the max.
       f32x16 sacc[2];
@@ -755,7 +812,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
         }
         sacc[u] = acc;
       }
-      if (MASK == 1 || (MASK == 2 && kv0 + 64 > c)) {      // keys >= c are zero pads (added analytically at the end)
+      if (kv0 + 64 > c) {      // keys >= c are zero pads (added analytically at the end)
   #pragma unroll
         for (int u = 0; u < 2; ++u)
   #pragma unroll
@@ -883,53 +940,21 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
             oacc[mt] = mfma_32x32x16<kVH>(vf, pf[u][s], oacc[mt]);
           }
         }
-      if constexpr (GP_ATTN_SCHED >= 2 && kZM && MASK == 0) {
-        // one region from the K reads to the last P.V MFMA (see GP_ATTN_SCHED)
-        __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);   // K fragment reads
-        __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);     // S(u = 0) x 3, S(u = 1) k-step 0
-        __builtin_amdgcn_sched_group_barrier(0x2, 3, 0);     // exps of S(u = 0)
-        __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x2, 3, 0);
-        __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x2, 6, 0);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // V^T reads of this P.V MFMA
-          __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x2, 4, 0);
-        }
-      }
 
     }
     if (t + 1 < ntiles) store_tile((t + 1) & 1);
     if constexpr (kDMA) __builtin_amdgcn_s_waitcnt(0x0f70);   // this wave's DMA pieces landed
     __syncthreads();
   };
-  using M0 = std::integral_constant<int, 0>;
-  using M1 = std::integral_constant<int, 1>;
-  using M2 = std::integral_constant<int, 2>;
   using S0 = std::integral_constant<int, 0>;
   using S1 = std::integral_constant<int, 1>;
-  if constexpr (kDMA && GP_ATTN_SCHED >= 1) {
-    // full tiles unmasked (one basic block each), the partial last tile on its own
-    const int nmain = (c % KT) != 0 ? ntiles - 1 : ntiles;
-    int t = 0;
-    for (; t + 1 < nmain; t += 2) {
-      tile_step(t, S0(), M0());
-      tile_step(t + 1, S1(), M0());
-    }
-    if (t < nmain) tile_step(t++, S0(), M0());
-    if (t < ntiles) {
-      if (t & 1) tile_step(t, S1(), M1());
-      else tile_step(t, S0(), M1());
-    }
-  } else if constexpr (kDMA) {
+  if constexpr (kDMA) {
     for (int t = 0; t < ntiles; t += 2) {
-      tile_step(t, S0(), M2());
-      if (t + 1 < ntiles) tile_step(t + 1, S1(), M2());
+      tile_step(t, S0());
+      if (t + 1 < ntiles) tile_step(t + 1, S1());
     }
   } else {
-    for (int t = 0; t < ntiles; ++t) tile_step(t, S0(), M2());
+    for (int t = 0; t < ntiles; ++t) tile_step(t, S0());
   }
 
   // ---- epilogue
@@ -1011,7 +1036,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
 // once (independent loads per lane), exits unless one holds the kLseRedo marker, and recomputes the
 // flagged items in turn; kFixItems = 1 (lab builds) is one item per block in item order.
 template <int D, bool kPre, int MODE, bool kTab = false, int NW = 4, bool kH = false>
-__global__ __launch_bounds__(NW * 64, 2) void dilated_attn32_kernel(const AttnArgs a) {
+__global__ __launch_bounds__(NW * 64, (attn_wps<MODE, kTab>())) void dilated_attn32_kernel(const AttnArgs a) {
   if constexpr (MODE == kModeFix && kFixItems == 1) {
     attn32_item<D, kPre, MODE, kTab, NW, kH>(a, (int)blockIdx.x);   // its own flagged-row check first
   } else if constexpr (MODE == kModeFix) {

@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--merge", action="store_true")
     ap.add_argument("--fp16", action="store_true", help="fp16 operands (the pipeline's autocast caller: the exact kernel)")
+    ap.add_argument("--vbf16", action="store_true",
+                    help="fp16 q / k with a bf16 V third (GP_FMT_F16_VBF16: the fp16 caller's fused-QKV product pair)")
     args = ap.parse_args()
     if args.merge:
         args.branches = "all"
@@ -49,8 +51,11 @@ def main():
     g = torch.Generator(device="cuda").manual_seed(0)
     qkv = torch.randn(L, 3 * E, device="cuda", generator=g)
     qkv[:, :E] *= 0.35
-    act = torch.float16 if args.fp16 else torch.bfloat16
+    act = torch.float16 if (args.fp16 or args.vbf16) else torch.bfloat16
+    vb = qkv[:, 2 * E:].to(torch.bfloat16)
     qkv = qkv.to(act)
+    if args.vbf16:      # the V third holds bf16 bits, as the fp16 caller's QKV GEMM writes them
+        qkv[:, 2 * E:].view(torch.int16).copy_(vb.view(torch.int16))
     sets = []
     for b in args.branches.split(","):
         sel = list(range(5)) if b == "all" else [int(b)]
@@ -71,7 +76,7 @@ def main():
             for name, s, r in sets:
                 sc = scratch[name]
                 run = lambda: _hip.dilated_attn_fwd(qkv, qkv[:, E:], qkv[:, 2 * E:], 3 * E, 1, L, H, D, s, r,  # noqa
-                                                    sc.outs, sc.lses, 0.0, True)
+                                                    sc.outs, sc.lses, 0.0, True, v_bf16=args.vbf16)
                 if args.merge:
                     if name not in merge_out:       # attention outputs once, from the product build
                         _hip._lib = prod
