@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GP_ABI_VERSION 8
+#define GP_ABI_VERSION 9
 #define GP_EARG (-1)
 #define GP_MAX_BRANCHES 8
 #define GP_MAX_DESTS 8
@@ -288,33 +288,41 @@ int gp_ffn_fc2_ln(const uint16_t* h, int64_t ldh, const uint16_t* W2g, int64_t l
 
 /* out-proj + residual (multihead_attention.py:48 + encoder.py:141,147):
  *   x += A . W^T + bias  (fp32, in place; x [M, ldx]);  xb [M, ldxb] act, xstats [N/256, M, 2] fp32 as above.
- * gamma == NULL: no xb / xstats (x only).  shift: [M] fp32. */
+ * gamma == NULL: no xb / xstats (x only).  shift: [M] fp32.
+ * s_out != NULL (ABI 9): also merge the N/256 planes into plane N/256 of xstats ([N/256 + 1, M, 2]: mean, rstd
+ * with eps_next) and write s_out = shift + the row mean -- the merge the consuming gp_linear_ln /
+ * gp_ffn_fc1_gelu_ln would do; call those with nst < 0 then.  With a split-K tail the reduce launch does it
+ * (no extra launch); otherwise one merge launch follows the GEMM.  Needs gamma, eps_next > 0, N <= 2048. */
 int gp_linear_resid(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, const float* bias,
                     float* x, int64_t ldx, const float* shift, const float* gamma, uint16_t* xb,
-                    int64_t ldxb, float* xstats, int64_t M, int64_t N, int64_t K, void* ws,
-                    int64_t ws_bytes, int fmt, void* stream);
+                    int64_t ldxb, float* xstats, float eps_next, float* s_out, int64_t M, int64_t N, int64_t K,
+                    void* ws, int64_t ws_bytes, int fmt, void* stream);
 
 /* QKV with the pre-LN folded (encoder.py:126 + multihead_attention.py:43-45): merges stats planes
  * 0 .. nst-1 ([nst + 1, M, 2] fp32, gp_linear_resid / gp_ffn_fc2_ln_resid's xstats) into plane nst
- * (mean', rstd; s_out = s_in + mean' when s_out != NULL), then C = act(rstd (A . W^T - mean' c) + d). */
+ * (mean', rstd; s_out = s_in + mean' when s_out != NULL), then C = act(rstd (A . W^T - mean' c) + d).
+ * nst < 0 (ABI 9): plane -nst is already merged (the producer's s_out); no merge here. */
 int gp_linear_ln(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, float* stats, int nst,
                  const float* c, const float* d, float eps, const float* s_in, float* s_out, uint16_t* C,
                  int64_t ldc, int64_t M, int64_t N, int64_t K, void* ws, int64_t ws_bytes, int fmt,
                  void* stream);
 
 /* fc1 + GELU with final_layer_norm folded (encoder.py:147-150 + feedforward_network.py:131-135): the fold
- * of gp_linear_ln, then gp_ffn_fc1_gelu's GELU and hstats ([F/256 + 1, M, 2]).  No F limit. */
+ * of gp_linear_ln (nst < 0: merged by the producer, as there), then gp_ffn_fc1_gelu's GELU and hstats
+ * ([F/256 + 1, M, 2]).  No F limit. */
 int gp_ffn_fc1_gelu_ln(const uint16_t* A, int64_t lda, const uint16_t* W1, int64_t ldw, float* xstats,
                        int nst, const float* c1, const float* d1, float eps, const float* s_in, float* s_out,
                        uint16_t* h, int64_t ldh, float* hstats, int64_t M, int64_t F, int64_t K, int fmt,
                        void* stream);
 
 /* fc2 with ffn_layernorm folded (gp_ffn_fc2_ln) + residual (encoder.py:157-159): x += fc2(LN(h)),
- * xb / xstats for the next layer's pre-LN as gp_linear_resid (gamma == NULL: the last layer, x only). */
+ * xb / xstats for the next layer's pre-LN as gp_linear_resid (gamma == NULL: the last layer, x only;
+ * eps_next / s_out: the next LN's statistics merge, as gp_linear_resid). */
 int gp_ffn_fc2_ln_resid(const uint16_t* h, int64_t ldh, const uint16_t* W2g, int64_t ldw, float* hstats,
                         const float* c, const float* d, float eps, float* x, int64_t ldx, const float* shift,
-                        const float* gamma, uint16_t* xb, int64_t ldxb, float* xstats, int64_t M, int64_t N,
-                        int64_t F, void* ws, int64_t ws_bytes, int fmt, void* stream);
+                        const float* gamma, uint16_t* xb, int64_t ldxb, float* xstats, float eps_next,
+                        float* s_out, int64_t M, int64_t N, int64_t F, void* ws, int64_t ws_bytes, int fmt,
+                        void* stream);
 
 /* Plain fp32 LayerNorm over rows with a row stride (readout: encoder.py:387-388,
  * slide_encoder.py:213-221).  out: [rows, cols] fp32 contiguous.  cols = 64 * {12, 16, 24}. */

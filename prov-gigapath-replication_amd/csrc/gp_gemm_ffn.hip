@@ -22,6 +22,8 @@ extern "C" int gp_ffn_fc1_gelu_ln(const uint16_t* A, int64_t lda, const uint16_t
                                   float* s_out, uint16_t* h, int64_t ldh, float* hstats, int64_t M, int64_t F,
                                   int64_t K, int fmt, void* stream) {
   if (int rc = check_shapes("gp_ffn_fc1_gelu_ln", A, lda, W1, ldw, h, ldh, M, F, K, fmt)) return rc;
+  const bool merged = nst < 0;   // plane -nst merged by the producer (see gp_linear_ln)
+  if (merged) nst = -nst;
   if (int rc = check_fold("gp_ffn_fc1_gelu_ln", xstats, nst, c1, d1, F)) return rc;
   GP_REQUIRE(hstats && gp_aligned(hstats, 8), "gp_ffn_fc1_gelu_ln: null or misaligned hstats");
   const Plan p = make_plan(M, F, K, false);
@@ -31,7 +33,7 @@ extern "C" int gp_ffn_fc1_gelu_ln(const uint16_t* A, int64_t lda, const uint16_t
   g.M = (int)M; g.N = (int)F; g.K = (int)K;
   g.nst = nst;
   g.eps = eps;
-  launch_row_stats(xstats, M, nst, eps, s_in, s_out, gp_stream(stream));
+  if (!merged) launch_row_stats(xstats, M, nst, eps, s_in, s_out, gp_stream(stream));
   const int lrc = fmt == GP_FMT_F16 ? launch<kEpiLnFoldGelu, true, kKE>(g, p, gp_stream(stream)) : launch<kEpiLnFoldGelu, false, kKE>(g, p, gp_stream(stream));
   if (lrc != 0) return lrc;
   return gp_check_launch("gp_ffn_fc1_gelu_ln");

@@ -129,6 +129,11 @@ struct GemmArgs {
   int n_dp;             // tiles run data-parallel
   int split;            // 1: the remaining tiles are split in K (workspace ws)
   float* ws;
+  // resid producers (round 5): merge the N/256 statistics planes of ostats into plane N/256 (mean, rstd with
+  // mrg_eps) and write mrg_sout = shift + mean in the split-tail reduce launch -- the next LN-folding GEMM's
+  // row_stats_kernel, without its launch.  Null: no merge here.
+  float* mrg_sout;
+  float mrg_eps;
 };
 
 template <int n>
@@ -205,18 +210,24 @@ GP_DEV uint32_t gelu_fix(uint32_t xp, uint32_t hv, uint32_t half) {
   return r;
 }
 
-// Chan merge of nst (mean, M2) groups of 256 values -> (mean, rstd) of the row (biased variance + eps)
-GP_DEV float2 merge_row_stats(const float2* st, int64_t stride, int nst, float eps) {
+// Chan merge of nst (mean, M2) groups of 256 values -> (mean, rstd) of the row (biased variance + eps);
+// plane(g) yields group g.  ONE arithmetic for row_stats_kernel and the reduce kernel's merge below, so both
+// produce the same bits.
+template <class Plane>
+GP_DEV float2 merge_row_stats_f(Plane plane, int nst, float eps) {
   float msum = 0.f;
-  for (int g = 0; g < nst; ++g) msum += st[g * stride].x;
+  for (int g = 0; g < nst; ++g) msum += plane(g).x;
   const float mean = msum / (float)nst;
   float m2 = 0.f;
   for (int g = 0; g < nst; ++g) {
-    const float2 p = st[g * stride];
+    const float2 p = plane(g);
     const float dm = p.x - mean;
     m2 += p.y + 256.f * dm * dm;
   }
   return make_float2(mean, rsqrtf(m2 / (float)(256 * nst) + eps));
+}
+GP_DEV float2 merge_row_stats(const float2* st, int64_t stride, int nst, float eps) {
+  return merge_row_stats_f([&](int g) { return st[g * stride]; }, nst, eps);
 }
 
 // plane nst of the statistics = (mean, rstd) of each row, merged from planes 0 .. nst-1 (one thread per row).
@@ -916,6 +927,98 @@ __global__ __launch_bounds__(256) void gemm_reduce_kernel(const GemmArgs g, int 
   *reinterpret_cast<uint4*>(g.C + (int64_t)m * g.ldc + n) = o;
 }
 
+// Split tail of a residual producer that also merges the next LayerNorm's statistics (g.mrg_sout, round 5).
+// Blocks [0, nmb): the rows of the row panels whose tiles all ran data-parallel (their planes are final: the
+// GEMM kernel completed before this launch), one thread per row as row_stats_kernel.  Blocks [nmb, nmb +
+// 32 * tail panels): 8 rows of one tail panel each, through every tail tile of that panel in turn -- the
+// split sum and residual epilogue of gemm_reduce_kernel, same thread layout -- keeping the rows' per-tile
+// (mean, M2) in LDS, then merging them with the panel's data-parallel tiles' planes in plane order: the
+// values and the arithmetic of row_stats_kernel, so plane N/256 and mrg_sout come out bit-identical to the
+// separate launch this replaces.  No block depends on another (no atomics, no flags).
+constexpr int kMaxTilesN = 8;   // N / 256 of the residual producers (E = 768 / 1024 / 1536)
+template <int EPI, bool kH>
+__global__ __launch_bounds__(256) void gemm_reduce_merge_kernel(const GemmArgs g, int S, int nmb) {
+  static_assert(epi_res<EPI>, "");
+  constexpr bool kFold = epi_fold<EPI>;
+  const int tiles_n = g.N / kBN;
+  float2* st = reinterpret_cast<float2*>(g.ostats);
+  const int p0 = g.n_dp / tiles_n;               // first panel with a tail tile
+  if ((int)blockIdx.x < nmb) {
+    const int m = (int)blockIdx.x * 256 + (int)threadIdx.x;
+    if (m >= p0 * kBM || m >= g.M) return;
+    const float2 r = merge_row_stats(st + m, g.M, tiles_n, g.mrg_eps);
+    st[(int64_t)tiles_n * g.M + m] = r;
+    g.mrg_sout[m] = g.shift[m] + r.x;
+    return;
+  }
+  __shared__ float2 pst[kMaxTilesN][8];
+  const int b = (int)blockIdx.x - nmb;
+  const int pnl = p0 + b / 32, rg = b % 32;
+  const int row = rg * 8 + (int)threadIdx.x / 32, col = ((int)threadIdx.x % 32) * 8;
+  const int m = pnl * kBM + row;
+  const float* gam = EPI == kEpiLnFoldResid ? g.colp2 : g.colp1;
+  for (int tn = 0; tn < tiles_n; ++tn) {
+    const int T = pnl * tiles_n + tn;
+    if (T < g.n_dp || m >= g.M) continue;        // (data-parallel tile / rows past M: all 32 lanes of a row)
+    const int unit = T - g.n_dp, n = tn * kBN + col;
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < S; ++s) {
+      const float* pp = g.ws + (int64_t)(unit * S + s) * (kBM * kBN) + row * kBN + col;
+      const float4 a = *reinterpret_cast<const float4*>(pp), c = *reinterpret_cast<const float4*>(pp + 4);
+      v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += c.x; v[5] += c.y; v[6] += c.z; v[7] += c.w;
+    }
+    if constexpr (kFold) {
+      const float2 mr = reinterpret_cast<const float2*>(g.stats)[(int64_t)g.nst * g.M + m];
+      for (int e = 0; e < 8; ++e) v[e] = fmaf(mr.y, fmaf(-mr.x, g.colp0[n + e], v[e]), g.colp1[n + e]);
+    } else {
+      if (g.colp0 != nullptr)
+        for (int e = 0; e < 8; ++e) v[e] += g.colp0[n + e];
+    }
+    float* xr = g.x + (int64_t)m * g.ldx + n;
+    const float4 a = *reinterpret_cast<const float4*>(xr), c = *reinterpret_cast<const float4*>(xr + 4);
+    const float xo[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+    for (int e = 0; e < 8; ++e) v[e] = xo[e] + v[e];
+    *reinterpret_cast<float4*>(xr) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(xr + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    const float sh = g.shift[m];
+    float s = 0.f, s2 = 0.f;
+    for (int e = 0; e < 8; ++e) {
+      const float d = v[e] - sh;
+      s += d;
+      s2 = fmaf(d, d, s2);
+      v[e] = d * gam[n + e];
+    }
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) {
+      s += __shfl_xor(s, o, 64);
+      s2 += __shfl_xor(s2, o, 64);
+    }
+    if (col == 0) {
+      const float mean = s * (1.f / 256.f);
+      const float2 ms = make_float2(mean, fmaxf(fmaf(-s, mean, s2), 0.f));
+      st[(int64_t)tn * g.M + m] = ms;
+      pst[tn][row % 8] = ms;
+    }
+    uint4 o;
+    o.x = pack2e<kH>(v[0], v[1]);
+    o.y = pack2e<kH>(v[2], v[3]);
+    o.z = pack2e<kH>(v[4], v[5]);
+    o.w = pack2e<kH>(v[6], v[7]);
+    *reinterpret_cast<uint4*>(g.C + (int64_t)m * g.ldc + n) = o;
+  }
+  __syncthreads();
+  if (threadIdx.x < 8) {
+    const int r8 = (int)threadIdx.x, mm = pnl * kBM + rg * 8 + r8;
+    if (mm < g.M) {
+      const float2 r = merge_row_stats_f(
+          [&](int tn) { return pnl * tiles_n + tn < g.n_dp ? st[(int64_t)tn * g.M + mm] : pst[tn][r8]; }, tiles_n,
+          g.mrg_eps);
+      st[(int64_t)tiles_n * g.M + mm] = r;
+      g.mrg_sout[mm] = g.shift[mm] + r.x;
+    }
+  }
+}
+
 // ----------------------------------------------------------------------------------------------------
 // host side
 int device_cus() {                 // per-device cache of the CU count (one persistent workgroup per CU)
@@ -1064,6 +1167,17 @@ int launch(GemmArgs g, const Plan& p, hipStream_t s) {
   }
   GP_REQUIRE(done, "GEMM epilogue %d: K=%d not instantiated (K = E in {768, 1024, 1536} or F = 4E)", EPI, g.K);
   if constexpr (kSplit) {
+    if constexpr (epi_res<EPI>) {
+      if (p.S > 1 && g.mrg_sout != nullptr) {   // the tail's reduce + the next LN's statistics merge (see above)
+        const int tiles_n = g.N / kBN;
+        const int64_t ntile = ((int64_t)(g.M + kBM - 1) / kBM) * tiles_n;
+        const int p0 = p.n_dp / tiles_n, pend = (int)((ntile + tiles_n - 1) / tiles_n);
+        GP_REQUIRE(tiles_n <= kMaxTilesN && g.C != nullptr, "GEMM epilogue %d: bad statistics merge", EPI);
+        const int nmb = (int)(((int64_t)p0 * kBM + 255) / 256);
+        gemm_reduce_merge_kernel<EPI, kH><<<(unsigned)(nmb + 32 * (pend - p0)), 256, 0, s>>>(g, p.S, nmb);
+        return 0;
+      }
+    }
     if (p.S > 1) gemm_reduce_kernel<EPI, kH><<<(unsigned)(p.rem * (kBM * kBN / 8 / 256)), 256, 0, s>>>(g, p.S);
   }
   return 0;

@@ -6,6 +6,10 @@ extern "C" int gp_linear_ln(const uint16_t* A, int64_t lda, const uint16_t* W, i
                             int64_t ldc, int64_t M, int64_t N, int64_t K, void* ws, int64_t ws_bytes, int fmt,
                             void* stream) {
   if (int rc = check_shapes("gp_linear_ln", A, lda, W, ldw, C, ldc, M, N, K, fmt, true)) return rc;
+  // nst < 0 (round 5): plane -nst already holds (mean, rstd) and s_out the shift -- merged by the producer
+  // (gp_linear_resid / gp_ffn_fc2_ln_resid with s_out); no merge launch here
+  const bool merged = nst < 0;
+  if (merged) nst = -nst;
   if (int rc = check_fold("gp_linear_ln", stats, nst, c, d, N)) return rc;
   const Plan p = make_plan(M, N, K, ws != nullptr);
   GP_REQUIRE(p.ws_bytes <= ws_bytes, "gp_linear_ln: workspace of %lld bytes, %lld needed", (long long)ws_bytes,
@@ -19,7 +23,7 @@ extern "C" int gp_linear_ln(const uint16_t* A, int64_t lda, const uint16_t* W, i
   g.eps = eps;
   g.ws = static_cast<float*>(ws);
   g.vcol0 = fmt == GP_FMT_F16_VBF16 ? (int)(2 * N / 3) : INT_MAX;
-  launch_row_stats(stats, M, nst, eps, s_in, s_out, gp_stream(stream));
+  if (!merged) launch_row_stats(stats, M, nst, eps, s_in, s_out, gp_stream(stream));
   const int lrc = fmt != GP_FMT_BF16 ? launch<kEpiLnFold, true, kKE | kKF>(g, p, gp_stream(stream)) : launch<kEpiLnFold, false, kKE | kKF>(g, p, gp_stream(stream));
   if (lrc != 0) return lrc;
   return gp_check_launch("gp_linear_ln");

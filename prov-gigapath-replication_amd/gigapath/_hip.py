@@ -15,7 +15,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_lib", "libgigapath_hip.so")
-ABI_VERSION = 8
+ABI_VERSION = 9
 MAX_BRANCHES = 8
 MAX_DESTS = 8
 
@@ -67,14 +67,14 @@ SIGNATURES = {
     "gp_ffn_fc1_gelu": [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_i32, c_vp],
     "gp_ffn_fc2_ln": [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_f32, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64,
                       c_i32, c_vp],
-    "gp_linear_resid": [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i64,
-                        c_vp, c_i64, c_i32, c_vp],
+    "gp_linear_resid": [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_f32, c_vp, c_i64,
+                        c_i64, c_i64, c_vp, c_i64, c_i32, c_vp],
     "gp_linear_ln": [c_vp, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64,
                      c_i64, c_vp, c_i64, c_i32, c_vp],
     "gp_ffn_fc1_gelu_ln": [c_vp, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp, c_i64, c_vp,
                            c_i64, c_i64, c_i64, c_i32, c_vp],
     "gp_ffn_fc2_ln_resid": [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_f32, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64,
-                            c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i32, c_vp],
+                            c_vp, c_f32, c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i32, c_vp],
 }
 _RESTYPES = {"gp_last_error_string": ctypes.c_char_p, "gp_varlen_plan_bytes": c_i64, "gp_gemm_workspace_bytes": c_i64}
 
@@ -504,9 +504,21 @@ def _f32_vec(t, n, name):
     return t
 
 
-def linear_resid(a, w, bias, x, shift, gamma, xb, xstats, ws=None):
+def _merge_args(gamma, xstats, N, M, eps_next, s_out, who):
+    """The producer-side statistics merge (round 5): s_out [M] fp32 and eps_next, xstats with plane N/256."""
+    if s_out is None:
+        return 0.0, None
+    if gamma is None or eps_next is None or eps_next <= 0:
+        raise ValueError("%s: s_out (the statistics merge) needs gamma and eps_next > 0" % who)
+    _f32_vec(s_out, M, "s_out"); _f32_vec(xstats, (N // 256 + 1) * M * 2, "xstats")
+    return float(eps_next), s_out
+
+
+def linear_resid(a, w, bias, x, shift, gamma, xb, xstats, ws=None, eps_next=None, s_out=None):
     """x += a . w^T + bias (fp32 x [M, N], in place); with gamma: xb = act(gamma * (x - shift)) [M, N] and
-    xstats [N/256 (+1), M, 2] (mean, M2) of x - shift per 256-column group.  gamma None: x only."""
+    xstats [N/256 (+1), M, 2] (mean, M2) of x - shift per 256-column group.  gamma None: x only.
+    s_out (round 5): also merge the groups into plane N/256 (mean, rstd with eps_next) and write s_out = shift
+    + the row mean -- the next LN-folding GEMM is then called with merged=True (no merge launch there)."""
     lib = load_library()
     fmt = fmt_of(a.dtype)
     _rows(a, "a"); _rows(w, "w"); _rows(x, "x")
@@ -520,18 +532,19 @@ def linear_resid(a, w, bias, x, shift, gamma, xb, xstats, ws=None):
         _rows(xb, "xb")
         if xb.dtype != a.dtype:
             raise TypeError("linear_resid: xb must be in a's 16-bit dtype")
+    eps_next, s_out = _merge_args(gamma, xstats, N, M, eps_next, s_out, "linear_resid")
     wp, wb = _ws(ws)
     _check(lib.gp_linear_resid(_ptr(a), a.stride(0), _ptr(w), w.stride(0), _ptr(bias), _ptr(x), x.stride(0),
                                _ptr(shift if gamma is not None else None), _ptr(gamma),
                                _ptr(xb if gamma is not None else None), xb.stride(0) if gamma is not None else 0,
-                               _ptr(xstats if gamma is not None else None), M, N, K, wp, wb, fmt, _stream()),
-           "gp_linear_resid")
+                               _ptr(xstats if gamma is not None else None), eps_next, _ptr(s_out), M, N, K, wp, wb,
+                               fmt, _stream()), "gp_linear_resid")
 
 
-def linear_ln(a, w, stats, nst, c, d, eps, s_in, s_out, out, ws=None, v_bf16=False):
+def linear_ln(a, w, stats, nst, c, d, eps, s_in, s_out, out, ws=None, v_bf16=False, merged=False):
     """out = act(LN(x) . w^T + b) through the fold: a = xb = act(gamma * (x - s_in)), stats planes 0 .. nst-1
     merged into plane nst (s_out = s_in + mean' when given), c = w . gamma, d = w . beta + b.  v_bf16: as
-    linear."""
+    linear.  merged: the producer already merged plane nst and wrote s_out (linear_resid(..., s_out=))."""
     lib = load_library()
     fmt = qkv_fmt_of(a.dtype, v_bf16)
     _rows(a, "a"); _rows(w, "w"); _rows(out, "out")
@@ -543,13 +556,14 @@ def linear_ln(a, w, stats, nst, c, d, eps, s_in, s_out, out, ws=None, v_bf16=Fal
         if t is not None:
             _f32_vec(t, M, nm)
     wp, wb = _ws(ws)
-    _check(lib.gp_linear_ln(_ptr(a), a.stride(0), _ptr(w), w.stride(0), _ptr(stats), int(nst), _ptr(c), _ptr(d),
+    _check(lib.gp_linear_ln(_ptr(a), a.stride(0), _ptr(w), w.stride(0), _ptr(stats), -int(nst) if merged else int(nst),
+                            _ptr(c), _ptr(d),
                             float(eps), _ptr(s_in), _ptr(s_out), _ptr(out), out.stride(0), M, N, K, wp, wb, fmt,
                             _stream()), "gp_linear_ln")
 
 
-def ffn_fc1_gelu_ln(a, w1, xstats, nst, c1, d1, eps, s_in, s_out, h, hstats):
-    """gp_ffn_fc1_gelu with final_layer_norm folded as in linear_ln (a = xb)."""
+def ffn_fc1_gelu_ln(a, w1, xstats, nst, c1, d1, eps, s_in, s_out, h, hstats, merged=False):
+    """gp_ffn_fc1_gelu with final_layer_norm folded as in linear_ln (a = xb; merged as there)."""
     lib = load_library()
     fmt = fmt_of(a.dtype)
     _rows(a, "a"); _rows(w1, "w1"); _rows(h, "h")
@@ -561,13 +575,15 @@ def ffn_fc1_gelu_ln(a, w1, xstats, nst, c1, d1, eps, s_in, s_out, h, hstats):
     for nm, t in (("s_in", s_in), ("s_out", s_out)):
         if t is not None:
             _f32_vec(t, M, nm)
-    _check(lib.gp_ffn_fc1_gelu_ln(_ptr(a), a.stride(0), _ptr(w1), w1.stride(0), _ptr(xstats), int(nst), _ptr(c1),
+    _check(lib.gp_ffn_fc1_gelu_ln(_ptr(a), a.stride(0), _ptr(w1), w1.stride(0), _ptr(xstats),
+                                  -int(nst) if merged else int(nst), _ptr(c1),
                                   _ptr(d1), float(eps), _ptr(s_in), _ptr(s_out), _ptr(h), h.stride(0), _ptr(hstats),
                                   M, F, K, fmt, _stream()), "gp_ffn_fc1_gelu_ln")
 
 
-def ffn_fc2_ln_resid(h, w2g, hstats, c, d, eps, x, shift, gamma, xb, xstats, ws=None):
-    """x += fc2(ffn_layernorm(h)) through the fold; with gamma: xb / xstats as linear_resid."""
+def ffn_fc2_ln_resid(h, w2g, hstats, c, d, eps, x, shift, gamma, xb, xstats, ws=None, eps_next=None, s_out=None):
+    """x += fc2(ffn_layernorm(h)) through the fold; with gamma: xb / xstats (and the merge: s_out, eps_next) as
+    linear_resid."""
     lib = load_library()
     fmt = fmt_of(h.dtype)
     _rows(h, "h"); _rows(w2g, "w2g"); _rows(x, "x")
@@ -580,10 +596,11 @@ def ffn_fc2_ln_resid(h, w2g, hstats, c, d, eps, x, shift, gamma, xb, xstats, ws=
         _rows(xb, "xb")
         if xb.dtype != h.dtype:
             raise TypeError("ffn_fc2_ln_resid: xb must be in h's 16-bit dtype")
+    eps_next, s_out = _merge_args(gamma, xstats, N, M, eps_next, s_out, "ffn_fc2_ln_resid")
     wp, wb = _ws(ws)
     _check(lib.gp_ffn_fc2_ln_resid(_ptr(h), h.stride(0), _ptr(w2g), w2g.stride(0), _ptr(hstats), _ptr(c), _ptr(d),
                                    float(eps), _ptr(x), x.stride(0), _ptr(shift if gamma is not None else None),
                                    _ptr(gamma), _ptr(xb if gamma is not None else None),
                                    xb.stride(0) if gamma is not None else 0,
-                                   _ptr(xstats if gamma is not None else None), M, N, F, wp, wb, fmt, _stream()),
-           "gp_ffn_fc2_ln_resid")
+                                   _ptr(xstats if gamma is not None else None), eps_next, _ptr(s_out), M, N, F, wp,
+                                   wb, fmt, _stream()), "gp_ffn_fc2_ln_resid")

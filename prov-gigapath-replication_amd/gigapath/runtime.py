@@ -427,13 +427,18 @@ def resid_buffers(dev, M: int, E: int):
             torch.empty(2, mp, dtype=torch.float32, device=dev)[:, :M])
 
 
+# the residual producers (out-proj, fc2) merge the next LayerNorm's statistics themselves (round 5: in their
+# split-tail reduce launch, so the 24 row_stats launches of the consumers go away; the result is the same bits)
+MERGE_IN_PRODUCER = os.environ.get("GIGAPATH_MERGE_IN_PRODUCER", "1") != "0"
+
+
 def fused_qkv(pl: "PackedLayer", ws, qkv: torch.Tensor):
-    """QKV of a layer after the first: LN1 folded, A = ws.y (the previous fc2's xb); merges the
-    statistics (shift[1] -> shift[0])."""
+    """QKV of a layer after the first: LN1 folded, A = ws.y (the previous fc2's xb); the statistics merge
+    (shift[1] -> shift[0]) is the previous fc2's (MERGE_IN_PRODUCER) or done here."""
     pa = pl.attn
     E = pa.E
     _hip.linear_ln(ws.y, pa.w_qkv, ws.xstats, E // 256, pl.c_qkv, pl.d_qkv, pl.ln1_eps, ws.shift[1], ws.shift[0],
-                   qkv, ws.gemm_ws, v_bf16=pa.v_bf16)
+                   qkv, ws.gemm_ws, v_bf16=pa.v_bf16, merged=MERGE_IN_PRODUCER)
 
 
 def fused_post_attention(pl: "PackedLayer", nxt: Optional["PackedLayer"], ws):
@@ -442,14 +447,19 @@ def fused_post_attention(pl: "PackedLayer", nxt: Optional["PackedLayer"], ws):
     fc1's merge writes shift[1], fc2 reads it; the next QKV maps shift[1] -> shift[0]."""
     pa = pl.attn
     E = pa.E
+    mp = MERGE_IN_PRODUCER
     with TIMER.span("gemm_out"):
-        _hip.linear_resid(ws.a, pa.w_o, pa.b_o, ws.x, ws.shift[0], pl.ln2_w, ws.y, ws.xstats, ws.gemm_ws)
+        _hip.linear_resid(ws.a, pa.w_o, pa.b_o, ws.x, ws.shift[0], pl.ln2_w, ws.y, ws.xstats, ws.gemm_ws,
+                          eps_next=pl.ln2_eps if mp else None, s_out=ws.shift[1] if mp else None)
     with TIMER.span("gemm_fc1"):
         _hip.ffn_fc1_gelu_ln(ws.y, pl.w1, ws.xstats, E // 256, pl.c1, pl.d1, pl.ln2_eps, ws.shift[0], ws.shift[1],
-                             ws.f, ws.fstats)
+                             ws.f, ws.fstats, merged=mp)
     with TIMER.span("gemm_fc2"):
+        last = nxt is None
         _hip.ffn_fc2_ln_resid(ws.f, pl.w2g, ws.fstats, pl.c2, pl.d2, pl.fln_eps, ws.x, ws.shift[1],
-                              nxt.ln1_w if nxt is not None else None, ws.y, ws.xstats, ws.gemm_ws)
+                              None if last else nxt.ln1_w, ws.y, ws.xstats, ws.gemm_ws,
+                              eps_next=None if (last or not mp) else nxt.ln1_eps,
+                              s_out=None if (last or not mp) else ws.shift[0])
 
 
 def ffn_forward(pl: "PackedLayer", a: torch.Tensor, f: torch.Tensor, y: torch.Tensor, fstats, gemm_ws,

@@ -391,6 +391,79 @@ def test_ffn_fc2_ln_resid(act, M):
     assert torch.equal(x2, xbuf)        # the same x whether or not the next LN's operands are written
 
 
+def _consumer_merge(h, xst, nst, eps, s_in, M):
+    """The merged plane and shift as the consumer's own merge computes them (gp_linear_ln, nst > 0), on a copy
+    of the producer's planes: the reference the producer-side merge must equal bit for bit."""
+    st = xst.clone()
+    s_out = torch.full((M,), float("nan"), device=DEV)
+    E = 256 * nst
+    w = torch.zeros(256, E, dtype=torch.bfloat16, device=DEV)
+    z = torch.zeros(256, device=DEV)
+    out = torch.empty(M, 256, dtype=torch.bfloat16, device=DEV)
+    xb = torch.zeros(M, E, dtype=torch.bfloat16, device=DEV)
+    h.linear_ln(xb, w, st, nst, z, z, eps, s_in, s_out, out,
+                torch.empty(max(h.gemm_workspace_bytes(M, 256, E), 16), dtype=torch.uint8, device=DEV))
+    return st[nst], s_out
+
+
+# 25,613 rows: 303 tiles, 256 data-parallel (not a multiple of 3: the first tail panel is part data-parallel,
+# part split) + 47 split; 70,001: the C3 plan (822 tiles, whole tail panels); 1 and 10,104: no split (one merge
+# launch after the GEMM)
+@pytest.mark.parametrize("act", ACTS)
+@pytest.mark.parametrize("M", [1, 10104, 25613, 70001])
+@pytest.mark.parametrize("producer", ["out_proj", "fc2"])
+def test_resid_producer_merges_next_ln_stats(act, M, producer):
+    """ABI 9: gp_linear_resid / gp_ffn_fc2_ln_resid with s_out merge the next LayerNorm's statistics planes
+    themselves (in the split-tail reduce launch when the plan splits).  x, xb and the per-group planes equal
+    the run without the merge, and the merged plane and s_out equal the consumer's own merge bit for bit."""
+    h = _hip()
+    E = 768
+    eps = 1e-5 if producer == "out_proj" else 1e-6
+    g = torch.Generator(device=DEV).manual_seed(M + 23)
+    gam = 1.0 + _rand((E,), g, 0.3)
+    x0, s = _resid_inputs(g, M, E)
+    if producer == "out_proj":
+        K = E
+        a = _rand((M, K), g).to(act)
+        w = _rand((E, K), g, K ** -0.5).to(act)
+        b = _rand((E,), g, 0.1)
+
+        def run(xbuf, xb, xst, ws, s_out):
+            h.linear_resid(a, w, b, xbuf, s, gam, xb, xst, ws, eps_next=eps if s_out is not None else None,
+                           s_out=s_out)
+    else:
+        K = 3072
+        hh = torch.nn.functional.gelu(_rand((M, K), g)).to(act)
+        hst = torch.empty(K // 256 + 1, M, 2, device=DEV)
+        hf = hh.float().view(M, K // 256, 256).double()
+        mean = hf.mean(-1)
+        hst[:K // 256, :, 0] = mean.t().float()
+        hst[:K // 256, :, 1] = ((hf - mean[..., None]) ** 2).sum(-1).t().float()
+        w2g = _rand((E, K), g, K ** -0.5).to(act)
+        c = w2g.double().sum(1).float()
+        d = _rand((E,), g, 0.1)
+
+        def run(xbuf, xb, xst, ws, s_out):
+            h.ffn_fc2_ln_resid(hh, w2g, hst, c, d, 1e-5, xbuf, s, gam, xb, xst, ws,
+                               eps_next=eps if s_out is not None else None, s_out=s_out)
+    ws = torch.empty(max(h.gemm_workspace_bytes(M, E, K), 16), dtype=torch.uint8, device=DEV)
+    outs = []
+    for merge in (False, True):
+        xbuf = x0.clone()
+        xb = torch.full((M, E), float("nan"), dtype=act, device=DEV)
+        xst = torch.full((E // 256 + 1, M, 2), float("nan"), device=DEV)
+        s_out = torch.full((M,), float("nan"), device=DEV) if merge else None
+        run(xbuf, xb, xst, ws, s_out)
+        torch.cuda.synchronize()
+        outs.append((xbuf, xb, xst, s_out))
+    (x1, xb1, st1, _), (x2, xb2, st2, so2) = outs
+    assert torch.equal(x1, x2) and torch.equal(xb1.view(torch.int16), xb2.view(torch.int16))
+    assert torch.equal(st1[:E // 256], st2[:E // 256])
+    ref_plane, ref_s = _consumer_merge(h, st1, E // 256, eps, s, M)
+    assert torch.equal(st2[E // 256].view(torch.int32), ref_plane.view(torch.int32))
+    assert torch.equal(so2.view(torch.int32), ref_s.view(torch.int32))
+
+
 def test_resid_epilogue_errors():
     """The C ABI's checks of the residual entry points (no launch)."""
     h = _hip()
@@ -404,8 +477,13 @@ def test_resid_epilogue_errors():
     with pytest.raises(RuntimeError, match="xb"):
         lib = h.load_library()
         rc = lib.gp_linear_resid(a.data_ptr(), 768, w.data_ptr(), 768, None, x.data_ptr(), 768,
-                                 x.data_ptr(), x.data_ptr(), None, 768, x.data_ptr(), 64, 768, 768, None, 0, 0,
-                                 h._stream())
+                                 x.data_ptr(), x.data_ptr(), None, 768, x.data_ptr(), 0.0, None, 64, 768, 768, None,
+                                 0, 0, h._stream())
+        h._check(rc, "gp_linear_resid")
+    with pytest.raises(RuntimeError, match="statistics merge"):   # s_out needs gamma and eps_next > 0
+        lib = h.load_library()
+        rc = lib.gp_linear_resid(a.data_ptr(), 768, w.data_ptr(), 768, None, x.data_ptr(), 768, x.data_ptr(), None,
+                                 None, 768, x.data_ptr(), 1e-5, x.data_ptr(), 64, 768, 768, None, 0, 0, h._stream())
         h._check(rc, "gp_linear_resid")
 
 

@@ -5,7 +5,8 @@ reports the median forward time and the median per-kernel spans (runtime.TIMER) 
     python tools/forward_ab.py --libs prod,tools/attn_lab/liblab_x.so [--tiles 70000] [--rounds 5]
 
 A library entry may carry host-path options after a colon: "prod:noresid" runs the product library with
-runtime.RESID_FUSED off (the round-3 out-proj -> residual_layernorm -> FFN -> residual_layernorm sequence),
+runtime.RESID_FUSED off (the round-3 out-proj -> residual_layernorm -> FFN -> residual_layernorm sequence);
+"prod:nomerge" with runtime.MERGE_IN_PRODUCER off (the next LN's statistics merged by the consumer's launch),
 repacking the weights for it -- the in-process A/B of the residual epilogues.
 """
 import argparse
@@ -49,6 +50,7 @@ def main():
         for rnd in range(args.rounds + 1):
             for p, lib in libs:
                 _hip._lib = lib
+                runtime.MERGE_IN_PRODUCER = ":nomerge" not in p
                 want = ":noresid" not in p
                 if runtime.RESID_FUSED != want:        # (re)pack the weights for this host path
                     runtime.RESID_FUSED = want
