@@ -515,8 +515,9 @@ static_assert(kNWFast == 4 || kNWFast == 8 || kNWFast == 16, "GP_ATTN_NW must be
 #endif
 // minimum waves per SIMD the kernel instantiation is sized for (HIP launch-bounds semantics; 2: no register
 // constraint at these sizes -- the fixup / exact / register-staged kernels, 104-138 VGPRs)
-template <int MODE, bool kTab>
-constexpr int attn_wps() { return MODE == 0 ? (kTab ? GP_ATTN_FAST_WPS_TAB : GP_ATTN_FAST_WPS) : 2; }
+// (the 4-wave fast kernel of under-filled launches keeps the interleaved body, no register cap)
+template <int MODE, bool kTab, int NW>
+constexpr int attn_wps() { return MODE == 0 && NW == 8 ? (kTab ? GP_ATTN_FAST_WPS_TAB : GP_ATTN_FAST_WPS) : 2; }
 // Measured lab variants of this kernel (the 16x16x32 P.V GP_ATTN_PV16, the 3-slot ring GP_ATTN_RING3) build
 // from round 3's source in git (make -C tools/attn_lab r3lab).
 
@@ -729,7 +730,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   // prefetch -- before the first MFMA of every tile
   __builtin_amdgcn_s_waitcnt(0x0f70);
 
-  if constexpr ((attn_wps<MODE, kTab>() >= 6 ? GP_ATTN_PRIO_FAST : GP_ATTN_PRIO) != 0 && NW >= 8) {
+  if constexpr ((attn_wps<MODE, kTab, NW>() >= 6 ? GP_ATTN_PRIO_FAST : GP_ATTN_PRIO) != 0 && NW >= 8) {
     if (__builtin_amdgcn_readfirstlane((int)threadIdx.x) >= NT / 2) __builtin_amdgcn_s_setprio(1);
   }
   // one 64-key tile; SET = the tile's LDS buffer when the loop is unrolled by two (kDMA), so the
@@ -744,7 +745,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
     const int kv0 = t * KT;
     const char* Kb = kDMA ? (const char*)bufc(setc) : smem + (t & 1) * BUF;
     const char* Vb = Kb + KTILE;
-    if constexpr (attn_wps<MODE, kTab>() >= 6) {
+    if constexpr (attn_wps<MODE, kTab, NW>() >= 6) {
       // the fast kernel (GP_ATTN_FAST_WPS): one 32-key sub-tile at a time -- S, exps and P.V of sub-tile u before
       // sub-tile u + 1's S -- so the body fits 80 VGPRs and three workgroups share each CU
       if (wact) {
@@ -1036,7 +1037,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
 // once (independent loads per lane), exits unless one holds the kLseRedo marker, and recomputes the
 // flagged items in turn; kFixItems = 1 (lab builds) is one item per block in item order.
 template <int D, bool kPre, int MODE, bool kTab = false, int NW = 4, bool kH = false>
-__global__ __launch_bounds__(NW * 64, (attn_wps<MODE, kTab>())) void dilated_attn32_kernel(const AttnArgs a) {
+__global__ __launch_bounds__(NW * 64, (attn_wps<MODE, kTab, NW>())) void dilated_attn32_kernel(const AttnArgs a) {
   if constexpr (MODE == kModeFix && kFixItems == 1) {
     attn32_item<D, kPre, MODE, kTab, NW, kH>(a, (int)blockIdx.x);   // its own flagged-row check first
   } else if constexpr (MODE == kModeFix) {
@@ -1284,6 +1285,26 @@ extern "C" int gp_dilated_gather(const uint16_t* src, int64_t row_stride, int64_
   return gp_check_launch("gp_dilated_gather");
 }
 
+static int attn_num_cus(hipStream_t s) {     // per-device cache of the CU count
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipStreamGetDevice(s, &dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cache[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cache[dev] = n;
+  }
+  return cache[dev];
+}
+
+// An LDS-DMA launch whose 8-wave work items cannot fill the GPU (fewer items than the 3 per CU that are
+// resident at once: the long-branch launch of a sequence-parallel rank holds ~384 for 768 slots) runs 4-wave
+// workgroups of 128 queries instead -- twice the items, each K/V tile shared by half as many queries.  Same
+// per-query arithmetic: bit-identical outputs (round 5).  0 disables.
+#ifndef GP_ATTN_SMALL_LAUNCH_NW4
+#define GP_ATTN_SMALL_LAUNCH_NW4 1
+#endif
+
 // fmt: GP_FMT_BF16, GP_FMT_F16 (fp16 q / k / v) or GP_FMT_F16_VBF16 (fp16 q / k, bf16 v; o fp16)
 static int attn_fwd_impl(const uint16_t* q, int64_t q_row_stride, int64_t q_tok_base, int64_t B, int64_t L, int H,
                          int D, int64_t win_lo, int64_t win_hi, const GpAttnBranch* branches, int nbranch,
@@ -1327,7 +1348,11 @@ static int attn_fwd_impl(const uint16_t* q, int64_t q_row_stride, int64_t q_tok_
   const bool fast = D == 48 && q_log2_prescaled && kv_desc_ok;   // LDS-DMA staging (8 waves x 32 queries)
   GP_REQUIRE(fmt != GP_FMT_F16_VBF16 || fast,
              "gp_dilated_attn_fwd: fmt F16_VBF16 needs D = 48, a pre-scaled q and k / v in one row layout");
-  const int qblk = fast ? 32 * kNWFast : 128;   // query rows per workgroup
+  hipStream_t s = gp_stream(stream);
+  // query rows per workgroup; an under-filled 8-wave LDS-DMA launch of the bf16 / V-bf16 pair goes to 4 waves
+  // (the item count is computed for 8 first, below)
+  const bool small_ok = GP_ATTN_SMALL_LAUNCH_NW4 && fast && kNWFast == 8 && (fmt == GP_FMT_BF16 || fmt == GP_FMT_F16_VBF16);
+  int qblk = fast ? 32 * kNWFast : 128;
   // order branches by keys per work item (descending) so the longest items start first
   int order[GP_MAX_BRANCHES];
   GpBranch geo[GP_MAX_BRANCHES];
@@ -1348,6 +1373,8 @@ static int attn_fwd_impl(const uint16_t* q, int64_t q_row_stride, int64_t q_tok_
       int tmp = order[y]; order[y] = order[y - 1]; order[y - 1] = tmp;
     }
   int64_t items = 0;
+  auto plan_items = [&]() {
+  items = 0;
   for (int x = 0; x < nbranch; ++x) {
     const int b = order[x];
     const GpBranch& g = geo[b];
@@ -1382,13 +1409,32 @@ static int attn_fwd_impl(const uint16_t* q, int64_t q_row_stride, int64_t q_tok_
     attn_branch_magic(e);
     items += B * (int64_t)e.nseg_w * H * e.nqb;
   }
+  };
+  plan_items();
+  bool nw4 = false;
+  if (small_ok && items < 3 * (int64_t)attn_num_cus(s)) {
+    qblk = 128;
+    nw4 = true;
+    plan_items();
+  }
   for (int x = nbranch; x < GP_MAX_BRANCHES; ++x) a.br[x] = a.br[nbranch - 1];
   a.total_items = items;
   a.d_H = make_div_magic((uint32_t)H);
   a.tab = nullptr;
   a.ntab = 0;
   GP_REQUIRE(items < (int64_t)0x7fffffff, "gp_dilated_attn_fwd: too many work items");
-  hipStream_t s = gp_stream(stream);
+  if (nw4) {   // the under-filled launch in 4-wave workgroups (fast pair only)
+    if (fmt == GP_FMT_F16_VBF16) {
+      dilated_attn32_kernel<48, true, kModeFast, false, 4, true><<<(unsigned)items, 256, 0, s>>>(a);
+      if constexpr (GP_ATTN_NOFIX == 0)
+        dilated_attn32_kernel<48, true, kModeFix, false, 4, true><<<(unsigned)((items + kFixItems - 1) / kFixItems), 256, 0, s>>>(a);
+    } else {
+      dilated_attn32_kernel<48, true, kModeFast, false, 4><<<(unsigned)items, 256, 0, s>>>(a);
+      if constexpr (GP_ATTN_NOFIX == 0)
+        dilated_attn32_kernel<48, true, kModeFix, false, 4><<<(unsigned)((items + kFixItems - 1) / kFixItems), 256, 0, s>>>(a);
+    }
+    return gp_check_launch("gp_dilated_attn_fwd");
+  }
   if (fmt == GP_FMT_F16_VBF16) {
     // fp16 q / k, bf16 v: the bf16 product pair with the fp16 S MFMA (no max; fixup pass)
     dilated_attn32_kernel<48, true, kModeFast, false, kNWFast, true><<<(unsigned)items, 64 * kNWFast, 0, s>>>(a);

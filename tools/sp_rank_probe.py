@@ -39,12 +39,16 @@ def main():
     ap.add_argument("--ranks", default="", help="only these ranks of each W (default: all)")
     ap.add_argument("--local-first", default="0", help="comma list: 1 = transfer-free branches in a launch "
                     "of their own before the waits, 0 = in their size phase (the engine's default)")
+    ap.add_argument("--lib", default="", help="another build of the library (tools/attn_lab A/B), in place of the product")
     ap.add_argument("--product-ref", action="store_true",
                     help="also time the product's one-GPU encoder on the whole slide (the scaling denominator)")
     ap.add_argument("--phases", default="2", help="comma list of attention launch splits to time: "
                     "2 = the plan's (short branches, long branches), 3 = the long branches split by "
                     "whole-sequence vs multi-segment, 1 = one launch")
     args = ap.parse_args()
+    if args.lib:
+        from gigapath import _hip
+        _hip._lib = _hip.load_library(os.path.join(ROOT, args.lib))
     dev = torch.device("cuda", 0)
     model = slide_encoder.create_model("", "gigapath_slide_enc12l768d", 1536).to(dev).eval()
     enc = model.encoder
