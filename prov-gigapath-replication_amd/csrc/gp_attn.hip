@@ -167,7 +167,19 @@ GP_DEV void decode_item_tab(const AttnArgs& a, int item, WorkItem& w, AttnBranch
     const int mid = (lo + hi + 1) >> 1;
     if ((int64_t)item >= a.tab[mid].item_begin) lo = mid; else hi = mid - 1;
   }
+  // the entry by scalar loads (uniform index, constant address space) instead of flat loads into VGPRs
+  lo = __builtin_amdgcn_readfirstlane(lo);
+#if defined(__HIP_DEVICE_COMPILE__)
+  static_assert(sizeof(AttnBranch) % 4 == 0, "");
+  uint32_t words[sizeof(AttnBranch) / 4];
+  const __attribute__((address_space(4))) uint32_t* src =
+      (const __attribute__((address_space(4))) uint32_t*)(uintptr_t)(a.tab + lo);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(AttnBranch) / 4); ++i) words[i] = src[i];
+  __builtin_memcpy(&e, words, sizeof(AttnBranch));
+#else
   e = a.tab[lo];
+#endif
   w.bi = lo;
   decode_core(e, item - (int)e.item_begin, a.H, a.d_H, e.L, 0, e.L, w);
 }
@@ -507,11 +519,12 @@ static_assert(kNWFast == 4 || kNWFast == 8 || kNWFast == 16, "GP_ATTN_NW must be
 #ifndef GP_ATTN_FAST_WPS
 #define GP_ATTN_FAST_WPS 6
 #endif
-// the same for the packed (varlen, work-table) fast kernel: 4 -- at 80 VGPRs its table decode leaves 2 spill
-// reloads per two tiles inside the loop, and the C5 launch measured 7 % slower at six waves per SIMD (12.09 vs
-// 11.30 ms, profiles/r05_occ6v_varlen_ab.json)
+// the same for the packed (varlen, work-table) fast kernel: 6 since its table entry comes by scalar loads
+// (decode_item_tab); with the entry in VGPRs the 80-register budget spilled 12 and the C5 launch ran 7 % slower
+// (profiles/r05_occ6v_varlen_ab.json); with scalar loads 10.61 vs 11.00 ms per C5 launch, bit-identical
+// (profiles/r05_tab6_varlen_ab.json)
 #ifndef GP_ATTN_FAST_WPS_TAB
-#define GP_ATTN_FAST_WPS_TAB 4
+#define GP_ATTN_FAST_WPS_TAB 6
 #endif
 // minimum waves per SIMD the kernel instantiation is sized for (HIP launch-bounds semantics; 2: no register
 // constraint at these sizes -- the fixup / exact / register-staged kernels, 104-138 VGPRs)
