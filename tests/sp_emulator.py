@@ -131,23 +131,37 @@ def _resid_out(x, v, shift, gamma, xb, xstats):
     st[..., 1] = ((dg - mean[..., None]) ** 2).sum(-1).t()
 
 
-def linear_resid(a, w, bias, x, shift, gamma, xb, xstats, ws=None):
+def _producer_merge(xstats, N, M, shift, eps_next, s_out):
+    """ABI 9: the residual producer merges the next LN's statistics itself when s_out is given."""
+    if s_out is not None:
+        assert eps_next is not None and eps_next > 0
+        _merge_stats(xstats, N // 256, M, eps_next, shift, s_out)
+
+
+def _merged_plane(stats, nst, M):
+    """(mean, rstd) of plane nst, already merged by the producer (merged=True)."""
+    st = stats.view(-1)[:(nst + 1) * M * 2].view(nst + 1, M, 2)
+    return st[nst, :, 0].clone(), st[nst, :, 1].clone()
+
+
+def linear_resid(a, w, bias, x, shift, gamma, xb, xstats, ws=None, eps_next=None, s_out=None):
     M, N = a.shape[0], w.shape[0]
     y = a.float() @ w.float().t() + (bias.float() if bias is not None else 0)
     _resid_out(x, x[:M, :N] + y, shift, gamma, xb, xstats)
+    _producer_merge(xstats, N, M, shift, eps_next, s_out)
 
 
-def linear_ln(a, w, stats, nst, c, d, eps, s_in, s_out, out, ws=None, v_bf16=False):
+def linear_ln(a, w, stats, nst, c, d, eps, s_in, s_out, out, ws=None, v_bf16=False, merged=False):
     assert not v_bf16          # (the bf16 model: no bf16 V third in an fp16 buffer)
     M = a.shape[0]
-    mean, rstd = _merge_stats(stats, nst, M, eps, s_in, s_out)
+    mean, rstd = _merged_plane(stats, nst, M) if merged else _merge_stats(stats, nst, M, eps, s_in, s_out)
     acc = a.float() @ w.float().t()
     out[:M] = (rstd[:, None] * (acc - mean[:, None] * c.float()[None]) + d.float()[None]).to(out.dtype)
 
 
-def ffn_fc1_gelu_ln(a, w1, xstats, nst, c1, d1, eps, s_in, s_out, h, hstats):
+def ffn_fc1_gelu_ln(a, w1, xstats, nst, c1, d1, eps, s_in, s_out, h, hstats, merged=False):
     M, F = a.shape[0], w1.shape[0]
-    mean, rstd = _merge_stats(xstats, nst, M, eps, s_in, s_out)
+    mean, rstd = _merged_plane(xstats, nst, M) if merged else _merge_stats(xstats, nst, M, eps, s_in, s_out)
     v = (rstd[:, None] * (a.float() @ w1.float().t() - mean[:, None] * c1.float()[None]) + d1.float()[None])
     g = torch.nn.functional.gelu(v.to(h.dtype).float()).to(h.dtype)
     h[:M] = g
@@ -158,12 +172,13 @@ def ffn_fc1_gelu_ln(a, w1, xstats, nst, c1, d1, eps, s_in, s_out, h, hstats):
     st[..., 1] = ((gf - gm[..., None]) ** 2).sum(-1).t()
 
 
-def ffn_fc2_ln_resid(h, w2g, hstats, c, d, eps, x, shift, gamma, xb, xstats, ws=None):
+def ffn_fc2_ln_resid(h, w2g, hstats, c, d, eps, x, shift, gamma, xb, xstats, ws=None, eps_next=None, s_out=None):
     M, F = h.shape
     N = w2g.shape[0]
     mean, rstd = _merge_stats(hstats, F // 256, M, eps, None, None)
     y = rstd[:, None] * (h.float() @ w2g.float().t() - mean[:, None] * c.float()[None]) + d.float()[None]
     _resid_out(x, x[:M, :N] + y, shift, gamma, xb, xstats)
+    _producer_merge(xstats, N, M, shift, eps_next, s_out)
 
 
 def dilated_sparsify(src, src_row_stride, k_col, v_col, tok_lo, n_tok, L, H, D, segs, ratios, dsts, dst_bases=None):
