@@ -1317,6 +1317,10 @@ static int attn_num_cus(hipStream_t s) {     // per-device cache of the CU count
 #ifndef GP_ATTN_SMALL_LAUNCH_NW4
 #define GP_ATTN_SMALL_LAUNCH_NW4 1
 #endif
+// (8-wave items per CU below which a launch counts as under-filled)
+#ifndef GP_ATTN_SMALL_LAUNCH_PER_CU
+#define GP_ATTN_SMALL_LAUNCH_PER_CU 3
+#endif
 
 // fmt: GP_FMT_BF16, GP_FMT_F16 (fp16 q / k / v) or GP_FMT_F16_VBF16 (fp16 q / k, bf16 v; o fp16)
 static int attn_fwd_impl(const uint16_t* q, int64_t q_row_stride, int64_t q_tok_base, int64_t B, int64_t L, int H,
@@ -1425,7 +1429,7 @@ static int attn_fwd_impl(const uint16_t* q, int64_t q_row_stride, int64_t q_tok_
   };
   plan_items();
   bool nw4 = false;
-  if (small_ok && items < 3 * (int64_t)attn_num_cus(s)) {
+  if (small_ok && items < GP_ATTN_SMALL_LAUNCH_PER_CU * (int64_t)attn_num_cus(s)) {
     qblk = 128;
     nw4 = true;
     plan_items();
