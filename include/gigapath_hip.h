@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GP_ABI_VERSION 9
+#define GP_ABI_VERSION 10
 #define GP_EARG (-1)
 #define GP_MAX_BRANCHES 8
 #define GP_MAX_DESTS 8
@@ -117,6 +117,14 @@ typedef struct GpAttnBranch {
                                    column (H/r)*D of each row; pass v = k + (H/r)*D) */
   uint16_t* o;               /* [B*nseg, m, H, D] act */
   float* lse;                /* [B*nseg, H, m] fp32 */
+  int32_t key_part;          /* ABI 10: key_parts > 1 -- this entry attends to key part key_part of key_parts
+                                (the segment's key tiles split evenly; the reference's zero-pad keys go to
+                                the last part): o / lse are the softmax over those keys only, and the merge
+                                combines the parts as branches (gp_branch_merge_ln* with the entry repeated
+                                per part).  An empty part writes o = 0, lse = -inf.  0 / <= 1: all keys.
+                                Needs the LDS-DMA pair (D = 48, q_log2_prescaled, k / v in one row layout,
+                                fmt BF16 or F16_VBF16) and 0 <= key_part < key_parts <= 64. */
+  int32_t key_parts;
 } GpAttnBranch;
 
 /* Generalised gp_dilated_attn_fwd: per-branch K/V sources and a query window.  Computes, for

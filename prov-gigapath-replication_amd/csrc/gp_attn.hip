@@ -90,6 +90,7 @@ struct AttnBranch {
   int64_t kv_tok_base;
   uint16_t* o;          // [B*nseg, m, H, D]
   float* lse;           // [B*nseg, H, m]
+  int32_t kpart, kparts;   // key part kpart of kparts (<= 1: all keys; see GpAttnBranch.key_parts)
   // varlen table entries only (one per (slide, branch); B = 1, window = the whole slide)
   const uint16_t* q;    // the slide's first query row
   int64_t L;            // the slide's length (CLS + tiles)
@@ -534,9 +535,10 @@ constexpr int attn_wps() { return MODE == 0 && NW == 8 ? (kTab ? GP_ATTN_FAST_WP
 // Measured lab variants of this kernel (the 16x16x32 P.V GP_ATTN_PV16, the 3-slot ring GP_ATTN_RING3) build
 // from round 3's source in git (make -C tools/attn_lab r3lab).
 
-template <int D, bool kPre, int MODE, bool kTab, int NW, bool kH>
+template <int D, bool kPre, int MODE, bool kTab, int NW, bool kH, bool kParts = false>
 __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_idx) {
   static_assert(!kH || D == 48 || MODE == kModeGen, "fp16 LDS-DMA modes: D = 48");
+  static_assert(!kParts || (MODE != kModeGen && !kTab), "key parts: LDS-DMA modes, branch launches");
   static_assert(D == 48 || D == 64, "v2 kernel covers D = 48 and 64");
   static_assert(MODE == kModeGen || (D == 48 && kPre), "LDS-DMA modes need D = 48 and a pre-scaled q");
   static_assert(NW == 4 || ((NW == 8 || NW == 16) && MODE != kModeGen), "8 / 16 waves: LDS-DMA modes only");
@@ -731,9 +733,18 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
 #pragma unroll
     for (int r = 0; r < 16; ++r) oacc[mt][r] = 0.f;
 
-  const int ntiles = (c + KT - 1) / KT;
-  if (ntiles > 0) {
-    load_tile(0, IB0());
+  // key tiles of this item: all of them, or key part kpart of kparts (round 5: an under-filled launch splits a
+  // long branch's keys over several branch entries; each writes a softmax over its keys (o, lse) and the merge
+  // combines them as it combines branches).  The reference's zero-pad keys belong to the last part.  A kernel
+  // instantiation of its own (kParts): the product kernel keeps its fixed key loop (a variable start costs it
+  // spills inside the loop).
+  const int ntiles_all = (c + KT - 1) / KT;
+  const bool split = kParts && brr.kparts > 1;
+  const int t_lo = split ? (int)((int64_t)ntiles_all * brr.kpart / brr.kparts) : 0;
+  const int t_hi = split ? (int)((int64_t)ntiles_all * (brr.kpart + 1) / brr.kparts) : ntiles_all;
+  const bool last_part = !split || brr.kpart == brr.kparts - 1;
+  if (t_hi > t_lo) {
+    load_tile(t_lo * KT, IB0());
     store_tile(0);
   }
   __syncthreads();
@@ -754,7 +765,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
   const bool wact = !GP_ATTN_SKIP_IDLE || __builtin_amdgcn_readfirstlane(q0 + w * 32) < rows_needed;
   auto tile_step = [&](int t, auto setc) {
     constexpr int SET = decltype(setc)::value;
-    if (t + 1 < ntiles) load_tile((t + 1) * KT, std::integral_constant<int, 1 - SET>());
+    if (t + 1 < t_hi) load_tile((t + 1) * KT, std::integral_constant<int, 1 - SET>());
     const int kv0 = t * KT;
     const char* Kb = kDMA ? (const char*)bufc(setc) : smem + (t & 1) * BUF;
     const char* Vb = Kb + KTILE;
@@ -809,7 +820,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
         for (int r = 0; r < 16; ++r) zero[r] = 0.f;
         ini = __builtin_amdgcn_mfma_f32_32x32x16_bf16(onesA, mqB, zero, 0, 0, 0);
       }
-      const float init = (kPre && !kZM && !kMI && t > 0) ? -m_run : 0.f;
+      const float init = (kPre && !kZM && !kMI && t > t_lo) ? -m_run : 0.f;
   #pragma unroll
       for (int u = 0; u < 2; ++u) {
         f32x16 acc;
@@ -851,13 +862,13 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
       if constexpr (kPre) {
         if constexpr (!kZM) {
           // scores are s*c - m_run; rescale only when a query's max moved up by > kThr
-          // (tile 0: always, which sets m_run to that tile's exact max)
-          const bool need = (t == 0) || mx > kThr;
+          // (the first tile: always, which sets m_run to that tile's exact max)
+          const bool need = (t == t_lo) || mx > kThr;
           if (__builtin_amdgcn_ballot_w64(need)) {
             if constexpr (kMI) {
               // m kept as an exact hi + lo pair of bf16 values (two rows of the init MFMA), so it
               // tracks the max to ~2^-16 relative and numerator and denominator stay consistent
-              const float m_old = (t == 0) ? 0.f : m_run;
+              const float m_old = (t == t_lo) ? 0.f : m_run;
               float m_new = m_old;
               if (need) {
                 const float tt = -(m_old + mx);
@@ -866,7 +877,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
                 m_new = -((float)hi + (float)lo);
               }
               const float d = m_new - m_old;
-              if (t > 0) {
+              if (t > t_lo) {
                 const float alpha = fast_exp2(-d);
   #pragma unroll
                 for (int mt = 0; mt < 2; ++mt)
@@ -887,14 +898,14 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
             } else {
               const float delta = need ? mx : 0.f;
               const float alpha = fast_exp2(-delta);
-              if (t > 0) {
+              if (t > t_lo) {
   #pragma unroll
                 for (int mt = 0; mt < 2; ++mt)
   #pragma unroll
                   for (int r = 0; r < 16; ++r) oacc[mt][r] *= alpha;
                 lsum *= alpha;
               }
-              m_run = (t == 0) ? delta : m_run + delta;
+              m_run = (t == t_lo) ? delta : m_run + delta;
   #pragma unroll
               for (int u = 0; u < 2; ++u)
   #pragma unroll
@@ -956,19 +967,19 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
         }
 
     }
-    if (t + 1 < ntiles) store_tile((t + 1) & 1);
+    if (t + 1 < t_hi) store_tile((t + 1) & 1);
     if constexpr (kDMA) __builtin_amdgcn_s_waitcnt(0x0f70);   // this wave's DMA pieces landed
     __syncthreads();
   };
   using S0 = std::integral_constant<int, 0>;
   using S1 = std::integral_constant<int, 1>;
   if constexpr (kDMA) {
-    for (int t = 0; t < ntiles; t += 2) {
+    for (int t = t_lo; t < t_hi; t += 2) {
       tile_step(t, S0());
-      if (t + 1 < ntiles) tile_step(t + 1, S1());
+      if (t + 1 < t_hi) tile_step(t + 1, S1());
     }
   } else {
-    for (int t = 0; t < ntiles; ++t) tile_step(t, S0());
+    for (int t = t_lo; t < t_hi; ++t) tile_step(t, S0());
   }
 
   // ---- epilogue
@@ -979,14 +990,17 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
     const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(lsum), __float_as_uint(lsum), false, false);
     l = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
   }
-  const int npad = g.m - c;
+  const int npad = last_part ? g.m - c : 0;
+  // a key part with no keys at all (a short last segment split in parts): an empty softmax -- o = 0,
+  // lse = -inf, which the merge weighs 0 -- not a flagged row
+  const bool empty = kParts && t_hi <= t_lo && npad == 0;
   bool zm_bad = false;
   if constexpr (kFlag) {
     if constexpr (kZM) m_run = 0.f;
     const uint32_t eb = __float_as_uint(l) & 0x7f800000u;
     // with zero-pad keys (p = 1 each) a tiny real-key sum is not flagged: the pads then dominate
     // exactly as in the reference
-    zm_bad = eb == 0x7f800000u || !(l <= 0x1p100f) || (npad == 0 && !(l >= 0x1p-100f));
+    zm_bad = !empty && (eb == 0x7f800000u || !(l <= 0x1p100f) || (npad == 0 && !(l >= 0x1p-100f)));
   }
   // the reference's unmasked zero-padded keys (dilated_attention.py:85-91): npad keys of score 0
   float mr = m_run, so = 1.f;
@@ -996,7 +1010,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
     l = l * so + (float)npad * fast_exp2(-mf);
     mr = mf;
   }
-  const float inv = so / l;
+  const float inv = empty ? 0.f : so / l;
   const int i = q0 + w * 32 + l32;
   if constexpr (GP_ATTN_WIDE_STORE != 0) {
     // lane (q, h) holds d = 8k + 4h .. +3 for the D/8 groups k.  For each pair of groups (k, k+1)
@@ -1037,9 +1051,10 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
       }
   }
   if (i < rows_needed && fixrow) {
-    float lse = (mr + __builtin_amdgcn_logf(l)) * 0.69314718055994530942f;
+    float lse = empty ? -INFINITY : (mr + __builtin_amdgcn_logf(l)) * 0.69314718055994530942f;
     if constexpr (kFlag) {   // overflowed / out of range: flag the row for the fixup pass
-      if ((__float_as_uint(l) & 0x7f800000u) == 0x7f800000u || !(l > 0.f) || zm_bad) lse = __uint_as_float(kLseRedo);
+      if (!empty && ((__float_as_uint(l) & 0x7f800000u) == 0x7f800000u || !(l > 0.f) || zm_bad))
+        lse = __uint_as_float(kLseRedo);
     }
     if (h == 0) brr.lse[((int64_t)bn * a.H + hh) * g.m + i] = lse;
   }
@@ -1049,10 +1064,10 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
 // (GP_ATTN_FIX_ITEMS): a block reads the lse of every needed row of its kFixItems consecutive items at
 // once (independent loads per lane), exits unless one holds the kLseRedo marker, and recomputes the
 // flagged items in turn; kFixItems = 1 (lab builds) is one item per block in item order.
-template <int D, bool kPre, int MODE, bool kTab = false, int NW = 4, bool kH = false>
+template <int D, bool kPre, int MODE, bool kTab = false, int NW = 4, bool kH = false, bool kParts = false>
 __global__ __launch_bounds__(NW * 64, (attn_wps<MODE, kTab, NW>())) void dilated_attn32_kernel(const AttnArgs a) {
   if constexpr (MODE == kModeFix && kFixItems == 1) {
-    attn32_item<D, kPre, MODE, kTab, NW, kH>(a, (int)blockIdx.x);   // its own flagged-row check first
+    attn32_item<D, kPre, MODE, kTab, NW, kH, kParts>(a, (int)blockIdx.x);   // its own flagged-row check first
   } else if constexpr (MODE == kModeFix) {
     constexpr int QB = NW * 32;
     const int it0 = (int)blockIdx.x * kFixItems;
@@ -1086,9 +1101,9 @@ __global__ __launch_bounds__(NW * 64, (attn_wps<MODE, kTab, NW>())) void dilated
 #pragma unroll
     for (int n = 0; n < NV; ++n) flagged |= use[n] && vals[n] == kLseRedo;
     if (!__syncthreads_or(flagged)) return;
-    for (int k = 0; k < kFixItems && it0 + k < a.total_items; ++k) attn32_item<D, kPre, MODE, kTab, NW, kH>(a, it0 + k);
+    for (int k = 0; k < kFixItems && it0 + k < a.total_items; ++k) attn32_item<D, kPre, MODE, kTab, NW, kH, kParts>(a, it0 + k);
   } else {
-    attn32_item<D, kPre, MODE, kTab, NW, kH>(a, (int)xcd_group(blockIdx.x, gridDim.x));
+    attn32_item<D, kPre, MODE, kTab, NW, kH, kParts>(a, (int)xcd_group(blockIdx.x, gridDim.x));
   }
 }
 // ---------------------------------------------------------------------------------------
@@ -1376,6 +1391,9 @@ static int attn_fwd_impl(const uint16_t* q, int64_t q_row_stride, int64_t q_tok_
   for (int b = 0; b < nbranch; ++b) {
     const GpAttnBranch& d = branches[b];
     GP_REQUIRE(d.seg_len > 0 && d.ratio > 0, "gp_dilated_attn_fwd: branch %d has sl=%d r=%d", b, d.seg_len, d.ratio);
+    GP_REQUIRE(d.key_parts <= 1 || (d.key_part >= 0 && d.key_part < d.key_parts && d.key_parts <= 64 && D != 96),
+               "gp_dilated_attn_fwd: branch %d key part %d of %d (0 <= part < parts <= 64, D != 96)", b, d.key_part,
+               d.key_parts);
     GP_REQUIRE(d.o && d.lse && gp_aligned(d.o, 8), "gp_dilated_attn_fwd: branch %d output null/misaligned", b);
     GP_REQUIRE(d.k && d.v && gp_aligned(d.k, 16) && gp_aligned(d.v, 16) && d.kv_row_stride % 8 == 0,
                "gp_dilated_attn_fwd: branch %d k/v must be 16-byte aligned with a row stride multiple of 8", b);
@@ -1423,13 +1441,19 @@ static int attn_fwd_impl(const uint16_t* q, int64_t q_row_stride, int64_t q_tok_
     e.kv_sparse = d.kv_sparse_cols ? 1 : 0;
     e.o = d.o;
     e.lse = d.lse;
+    e.kpart = d.key_parts > 1 ? d.key_part : 0;
+    e.kparts = d.key_parts > 1 ? d.key_parts : 1;
     attn_branch_magic(e);
     items += B * (int64_t)e.nseg_w * H * e.nqb;
   }
   };
   plan_items();
+  bool parts = false;
+  for (int b = 0; b < nbranch; ++b) parts = parts || branches[b].key_parts > 1;
+  GP_REQUIRE(!parts || (fast && kNWFast == 8 && (fmt == GP_FMT_BF16 || fmt == GP_FMT_F16_VBF16)),
+             "gp_dilated_attn_fwd: key parts need the LDS-DMA bf16 pair (D = 48, pre-scaled q, k / v in one layout)");
   bool nw4 = false;
-  if (small_ok && items < GP_ATTN_SMALL_LAUNCH_PER_CU * (int64_t)attn_num_cus(s)) {
+  if (small_ok && !parts && items < GP_ATTN_SMALL_LAUNCH_PER_CU * (int64_t)attn_num_cus(s)) {
     qblk = 128;
     nw4 = true;
     plan_items();
@@ -1440,6 +1464,18 @@ static int attn_fwd_impl(const uint16_t* q, int64_t q_row_stride, int64_t q_tok_
   a.tab = nullptr;
   a.ntab = 0;
   GP_REQUIRE(items < (int64_t)0x7fffffff, "gp_dilated_attn_fwd: too many work items");
+  if (parts) {   // key parts (sequence-parallel under-filled launches): the 8-wave pair built with parts
+    if (fmt == GP_FMT_F16_VBF16) {
+      dilated_attn32_kernel<48, true, kModeFast, false, 8, true, true><<<(unsigned)items, 512, 0, s>>>(a);
+      if constexpr (GP_ATTN_NOFIX == 0)
+        dilated_attn32_kernel<48, true, kModeFix, false, 8, true, true><<<(unsigned)((items + kFixItems - 1) / kFixItems), 512, 0, s>>>(a);
+    } else {
+      dilated_attn32_kernel<48, true, kModeFast, false, 8, false, true><<<(unsigned)items, 512, 0, s>>>(a);
+      if constexpr (GP_ATTN_NOFIX == 0)
+        dilated_attn32_kernel<48, true, kModeFix, false, 8, false, true><<<(unsigned)((items + kFixItems - 1) / kFixItems), 512, 0, s>>>(a);
+    }
+    return gp_check_launch("gp_dilated_attn_fwd");
+  }
   if (nw4) {   // the under-filled launch in 4-wave workgroups (fast pair only)
     if (fmt == GP_FMT_F16_VBF16) {
       dilated_attn32_kernel<48, true, kModeFast, false, 4, true><<<(unsigned)items, 256, 0, s>>>(a);
@@ -1500,7 +1536,7 @@ extern "C" int gp_dilated_attn_fwd(const uint16_t* q, const uint16_t* k, const u
   GP_REQUIRE(D == 48 || D == 64 || D == 96, "gp_dilated_attn_fwd: head dim %d unsupported (48, 64, 96)", D);
   GP_REQUIRE(nbranch >= 1 && nbranch <= GP_MAX_BRANCHES, "gp_dilated_attn_fwd: nbranch must be 1..%d", GP_MAX_BRANCHES);
   GP_REQUIRE(k && v && seg_len && ratios && o_out && lse_out, "gp_dilated_attn_fwd: null pointer");
-  GpAttnBranch br[GP_MAX_BRANCHES];
+  GpAttnBranch br[GP_MAX_BRANCHES] = {};
   for (int b = 0; b < nbranch; ++b) {
     br[b].seg_len = seg_len[b];
     br[b].ratio = ratios[b];
@@ -1520,7 +1556,7 @@ static int seg_attn(const uint16_t* q, const uint16_t* k, const uint16_t* v, int
                     int D, float softmax_scale, uint16_t* o, float* lse, bool kh, void* stream) {
   GP_REQUIRE(seqlen > 0 && seqlen < (int64_t)0x7fffffff, "gp_seg_attn_fwd: bad seqlen");
   GP_REQUIRE(k && v && o && lse, "gp_seg_attn_fwd: null pointer");
-  GpAttnBranch br;
+  GpAttnBranch br = {};
   br.seg_len = (int32_t)seqlen;
   br.ratio = 1;
   br.k = k;
@@ -1559,6 +1595,8 @@ static void launch_merge(const MergeArgs& a, int E, int D, int nbranch, unsigned
   switch (E) {
     case 768:
       if (D == 48 && nbranch == 5) branch_merge_kernel<12, 48, false, 5, kH><<<nb, 256, 0, s>>>(a);
+      // (5 branches, two of them in two key parts: the sequence-parallel long-branch split, seqpar.plan_key_parts)
+      else if (D == 48 && nbranch == 7) branch_merge_kernel<12, 48, false, 7, kH><<<nb, 256, 0, s>>>(a);
       else if (D == 48) branch_merge_kernel<12, 48, false, GP_MAX_BRANCHES, kH><<<nb, 256, 0, s>>>(a);
       else if (D == 96) branch_merge_kernel<12, 96, false, GP_MAX_BRANCHES, kH><<<nb, 256, 0, s>>>(a);
       else branch_merge_kernel<12, 12, false, GP_MAX_BRANCHES, kH><<<nb, 256, 0, s>>>(a);

@@ -15,7 +15,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_lib", "libgigapath_hip.so")
-ABI_VERSION = 9
+ABI_VERSION = 10
 MAX_BRANCHES = 8
 MAX_DESTS = 8
 
@@ -30,7 +30,8 @@ class GpRowDest(ctypes.Structure):
 class GpAttnBranch(ctypes.Structure):
     """struct GpAttnBranch (include/gigapath_hip.h)."""
     _fields_ = [("seg_len", c_i32), ("ratio", c_i32), ("k", c_vp), ("v", c_vp), ("kv_row_stride", c_i64),
-                ("kv_tok_base", c_i64), ("kv_sparse_cols", c_i32), ("o", c_vp), ("lse", c_vp)]
+                ("kv_tok_base", c_i64), ("kv_sparse_cols", c_i32), ("o", c_vp), ("lse", c_vp),
+                ("key_part", c_i32), ("key_parts", c_i32)]
 
 # name -> argtypes (mirrors include/gigapath_hip.h)
 SIGNATURES = {
@@ -227,12 +228,14 @@ def dilated_attn_fwd(q, k, v, row_stride, B, L, H, D, segs, ratios, outs, lses, 
            "gp_dilated_attn_fwd")
 
 
-def attn_branch(sl, r, k, v, kv_row_stride, kv_tok_base, kv_sparse_cols, o, lse) -> GpAttnBranch:
-    """One GpAttnBranch descriptor; k / v are device tensors (views allowed) or raw pointers."""
+def attn_branch(sl, r, k, v, kv_row_stride, kv_tok_base, kv_sparse_cols, o, lse, key_part=0,
+                key_parts=1) -> GpAttnBranch:
+    """One GpAttnBranch descriptor; k / v are device tensors (views allowed) or raw pointers.  key_part /
+    key_parts (ABI 10): attend to one part of the keys only (GpAttnBranch.key_parts)."""
     kp = k if isinstance(k, int) else k.data_ptr()
     vp = v if isinstance(v, int) else v.data_ptr()
     return GpAttnBranch(int(sl), int(r), kp, vp, int(kv_row_stride), int(kv_tok_base), int(bool(kv_sparse_cols)),
-                        o.data_ptr(), lse.data_ptr())
+                        o.data_ptr(), lse.data_ptr(), int(key_part), int(key_parts))
 
 
 def dilated_attn_fwd_ex(q, q_row_stride, q_tok_base, B, L, H, D, win_lo, win_hi, branches, softmax_scale=0.0,

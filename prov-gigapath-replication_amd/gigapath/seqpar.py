@@ -116,6 +116,50 @@ def snapped_bounds(bounds: List[Tuple[int, int]], unit: int, L: int) -> Optional
     return [(cuts[w], cuts[w + 1]) for w in range(len(bounds))]
 
 
+def launch_items(geo: BranchGeo, H: int, win_lo: int, win_hi: int, qblk: int = 256) -> int:
+    """Work items of branch `geo` in a windowed attention launch of 8-wave (256-query) workgroups: segments
+    the window meets x heads x query blocks of the fullest (segment, phase) -- gp_attn.hip's item plan."""
+    n_lo, n_hi = win_lo // geo.g, (win_hi - 1) // geo.g
+    most = 0
+    for n in sorted({n_lo, min(n_lo + 1, n_hi), max(n_hi - 1, n_lo), n_hi}):
+        for j in range(geo.r):
+            base = n * geo.g + j
+            lo = -(-(win_lo - base) // geo.r) if win_lo > base else 0
+            hi = min(-(-(win_hi - base) // geo.r) if win_hi > base else 0, geo.m)
+            most = max(most, hi - lo)
+    if n_hi - n_lo > 3:
+        most = max(most, geo.m)                       # interior segments are full
+    return (n_hi - n_lo + 1) * H * max(1, -(-most // qblk))
+
+
+# resident 8-wave attention workgroups per CU (gp_attn.hip GP_ATTN_FAST_WPS: three)
+ATTN_WG_PER_CU = 3
+
+
+def plan_key_parts(plan: "ShardPlan", rank: int, launches: List[List[int]], n_cu: int = 256) -> List[int]:
+    """Key parts per branch for one rank's attention launches (1 = all keys in one entry).
+
+    A launch whose 8-wave work items cannot fill the GPU once (fewer than ATTN_WG_PER_CU x CUs: the long
+    branches' launch of a 256k slide's rank on 8 GPUs holds ~384-480 items of 16,000-23,170 keys for 768
+    slots) splits every branch's keys into P = max(2, round(slots / items)) parts, P lowered until the merge's
+    entries fit GP_MAX_BRANCHES; items of P parts fill the slots with P x shorter items.  Measured at 256k / 8
+    ranks (profiles/r05_kp_*): long-branch attention 5.36 -> 4.90 ms per forward, the merge + 0.10 ms; splitting
+    the mid branch's launch (1,152-1,344 items, 1.5-1.75 slot rounds) instead lost 0.1-0.4 ms."""
+    kp = [1] * len(plan.geo)
+    a, e = plan.bounds[rank]
+    slots = ATTN_WG_PER_CU * n_cu
+    for br in launches:
+        items = sum(launch_items(plan.geo[b], plan.H, a, e) for b in br)
+        if items >= slots:
+            continue
+        P = max(2, int(round(slots / items)))
+        while P >= 2 and sum(kp) + len(br) * (P - 1) > _hip.MAX_BRANCHES:
+            P -= 1
+        for b in br:
+            kp[b] = max(1, P)
+    return kp
+
+
 def _isect(a: Tuple[int, int], b: Tuple[int, int]) -> Tuple[int, int]:
     lo, hi = max(a[0], b[0]), min(a[1], b[1])
     return (lo, hi) if lo < hi else (0, 0)
@@ -468,6 +512,16 @@ class ShardWorkspace:
         self.plan = plan
         # branch outputs keep the single-device layout; only the window's rows are written/read
         self.attn = runtime.AttentionScratch(dev, 1, plan.L, H, D, plan.segs, plan.ratios, act)
+        self._parts: Dict[Tuple[int, int], Tuple[torch.Tensor, torch.Tensor]] = {}
+
+    def part_out(self, b: int, p: int) -> Tuple[torch.Tensor, torch.Tensor]:
+        """(o, lse) of key part p of branch b: part 0 is the branch's own output, later parts get buffers of
+        the same layout on first use."""
+        if p == 0:
+            return self.attn.outs[b], self.attn.lses[b]
+        if (b, p) not in self._parts:
+            self._parts[(b, p)] = (torch.empty_like(self.attn.outs[b]), torch.empty_like(self.attn.lses[b]))
+        return self._parts[(b, p)]
 
     def dest(self, b: int, v: int) -> Tuple[torch.Tensor, int]:
         """(buffer, first row) where this rank's branch-b rows for rank v go: the send buffer's chunk (W = 1)."""
@@ -507,6 +561,10 @@ class SeqParallelEngine:
     # slots), but the modelled exposed transfer at 64 GB/s per xGMI link direction is 0 with it vs 1.6 ms
     # without -- 20.39 vs 20.73 ms, and it stays exposure-free down to ~37 GB/s per link.
     local_first = True
+    # Key parts (ABI 10, GpAttnBranch.key_parts): branch b's keys split over key_parts[b] entries of its
+    # attention launch, each a softmax of its own that the merge combines like a branch -- for the launches a
+    # rank's window leaves under-filled.  None: plan_key_parts' choice; a dict {branch: parts} overrides it.
+    key_parts: Optional[Dict[int, int]] = None
 
     def __init__(self, plan: ShardPlan, rank: int, exchange: Exchange):
         self.plan, self.rank, self.xch = plan, rank, exchange
@@ -519,6 +577,22 @@ class SeqParallelEngine:
         self.monitor: Optional[ExchangeMonitor] = None   # diagnostic steps only (bench.py)
         self.graphs = {}                    # (segment, layer, weights signature) -> CUDAGraph
         self._graph_sig = None
+        self.key_parts = type(self).key_parts
+        self._kp = [1] * len(plan.geo)
+
+    def parts(self) -> List[int]:
+        """Key parts per branch this forward runs with."""
+        if self.key_parts is not None:
+            return [max(1, int(self.key_parts.get(b, 1))) for b in range(len(self.plan.geo))]
+        n_cu = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count \
+            if torch.cuda.is_available() else 256
+        return plan_key_parts(self.plan, self.rank, self._launches(), n_cu)
+
+    def _launches(self) -> List[List[int]]:
+        plan = self.plan
+        local = [b for b in range(len(plan.geo)) if plan.no_xfer[b]] if self.local_first else []
+        out = [local] + [[b for b in ph if b not in local] for ph in (plan.phase_a, plan.phase_b1, plan.phase_b2)]
+        return [x for x in out if x]
 
     def sparsify(self, ws: ShardWorkspace):
         """This rank's sparsified K/V rows: W > 1, once, into its own rows of the receive buffers (the
@@ -633,15 +707,18 @@ class SeqParallelEngine:
         descs = []
         E = plan.E
         for b in branches:
-            if plan.no_xfer[b]:              # dense K / V columns of the rank's own qkv rows
-                k = ws.qkv_ext[:, E:]
-                descs.append(_hip.attn_branch(plan.segs[b], plan.ratios[b], k, k.data_ptr() + 2 * E, 3 * E,
-                                              a - ws.hq, False, ws.attn.outs[b], ws.attn.lses[b]))
-                continue
-            C = plan.C[b]
-            kv = ws.kvs[b]
-            descs.append(_hip.attn_branch(plan.segs[b], plan.ratios[b], kv, kv.data_ptr() + 2 * C, 2 * C,
-                                          ws.kv_base[b], True, ws.attn.outs[b], ws.attn.lses[b]))
+            P = self._kp[b]
+            for p in range(P):
+                o, lse = ws.part_out(b, p)
+                if plan.no_xfer[b]:              # dense K / V columns of the rank's own qkv rows
+                    k = ws.qkv_ext[:, E:]
+                    descs.append(_hip.attn_branch(plan.segs[b], plan.ratios[b], k, k.data_ptr() + 2 * E, 3 * E,
+                                                  a - ws.hq, False, o, lse, p, P))
+                    continue
+                C = plan.C[b]
+                kv = ws.kvs[b]
+                descs.append(_hip.attn_branch(plan.segs[b], plan.ratios[b], kv, kv.data_ptr() + 2 * C, 2 * C,
+                                              ws.kv_base[b], True, o, lse, p, P))
         with runtime.TIMER.span(span):
             _hip.dilated_attn_fwd_ex(ws.qkv_ext, 3 * plan.E, a - ws.hq, 1, plan.L, plan.H, plan.D, a, e, descs, 0.0,
                                      pa.prescaled, v_bf16=pa.v_bf16)
@@ -682,11 +759,24 @@ class SeqParallelEngine:
         ph_a = [b for b in plan.phase_a if b not in local]
         ph_b1 = [b for b in plan.phase_b1 if b not in local]
         ph_b2 = [b for b in plan.phase_b2 if b not in local]
-        wsig = weights_sig if weights_sig is not None else id(layers)
-        if wsig != self._graph_sig:          # new weights: captures of the old ones never replay
+        self._kp = self.parts()
+        wsig = (weights_sig if weights_sig is not None else id(layers), tuple(self._kp))
+        if wsig != self._graph_sig:          # new weights / parts: captures of the old ones never replay
             self.graphs.clear()
             self._graph_sig = wsig
         fused = bool(layers) and all(pl.resid_fused for pl in layers) and ws.fstats is not None
+        # the merge's branch entries: every key part of every branch (part p of branch b in ws.part_out)
+        m_outs, m_lses, m_segs, m_ratios = [], [], [], []
+        for b in range(len(plan.geo)):
+            for p in range(self._kp[b]):
+                o, lse = ws.part_out(b, p)
+                m_outs.append(o)
+                m_lses.append(lse)
+                m_segs.append(plan.segs[b])
+                m_ratios.append(plan.ratios[b])
+        if len(m_outs) > _hip.MAX_BRANCHES:
+            raise ValueError("sequence parallel: %d branch entries with key parts %s (at most %d)"
+                             % (len(m_outs), self._kp, _hip.MAX_BRANCHES))
         if fused and not shift_ready:
             torch.mean(ws.x, 1, out=ws.shift[0])
         for li, pl in enumerate(layers):
@@ -704,7 +794,7 @@ class SeqParallelEngine:
             def tail(pa=pa, pl=pl, nxt=nxt):
                 self.attention(pa, ws, ph_b2 if plan.phase_b2 else ph_b1, "attn_B")
                 with runtime.TIMER.span("merge"):
-                    _hip.branch_merge_ln_window(ws.attn.outs, ws.attn.lses, plan.segs, plan.ratios, 1, plan.L, a, M,
+                    _hip.branch_merge_ln_window(m_outs, m_lses, m_segs, m_ratios, 1, plan.L, a, M,
                                                 H, D, pa.ln_w, pa.ln_b, pa.ln_eps, ws.a)
                 if fused:
                     runtime.fused_post_attention(pl, nxt, ws)

@@ -212,8 +212,9 @@ def dilated_sparsify_dests(src, src_row_stride, k_col, v_col, tok_lo, n_tok, L, 
             t[rows, C:] = vrow[sel].to(t.dtype)
 
 
-def attn_branch(sl, r, k, v, kv_row_stride, kv_tok_base, kv_sparse_cols, o, lse):
-    return dict(sl=sl, r=r, k=k, v=v, stride=kv_row_stride, base=kv_tok_base, sparse=kv_sparse_cols, o=o, lse=lse)
+def attn_branch(sl, r, k, v, kv_row_stride, kv_tok_base, kv_sparse_cols, o, lse, key_part=0, key_parts=1):
+    return dict(sl=sl, r=r, k=k, v=v, stride=kv_row_stride, base=kv_tok_base, sparse=kv_sparse_cols, o=o, lse=lse,
+                kp=key_part, kparts=key_parts)
 
 
 def _kv_tensor(k, v, stride, sparse, H, D, r):
@@ -248,9 +249,14 @@ def dilated_attn_fwd_ex(q, q_row_stride, q_tok_base, B, L, H, D, win_lo, win_hi,
                 rem = min(L - n * s, s) - j
                 c = -(-rem // r) if rem > 0 else 0
                 col = (h % hpg) * D if br["sparse"] else h * D
-                ktok = n * s + j + r * torch.arange(c)
+                # key part kp of kparts (GpAttnBranch.key_parts): 64-key tiles [t_lo, t_hi); pads in the last
+                P, kp = max(1, br["kparts"]), br["kp"]
+                nt = -(-c // 64)
+                k_lo, k_hi = 64 * (nt * kp // P), min(c, 64 * (nt * (kp + 1) // P))
+                last = kp == P - 1
+                ktok = n * s + j + r * torch.arange(k_lo, max(k_lo, k_hi))
                 krow = ktok - br["base"]
-                assert c == 0 or (krow.min() >= 0 and krow.max() < kt.shape[0]), ("k rows", n, h)
+                assert len(krow) == 0 or (krow.min() >= 0 and krow.max() < kt.shape[0]), ("k rows", n, h)
                 K, V = kt[krow, col:col + D].float(), vt[krow, col:col + D].float()
                 i = torch.arange(i_lo, i_hi)
                 qtok = n * s + j + r * i
@@ -260,8 +266,13 @@ def dilated_attn_fwd_ex(q, q_row_stride, q_tok_base, B, L, H, D, win_lo, win_hi,
                 Q = torch.zeros(len(i), D)
                 Q[valid] = q[qrow[valid], h * D:(h + 1) * D].float()
                 s2 = (Q @ K.T) * scale                               # log2-domain logits
-                npad = m - c
+                npad = m - c if last else 0
                 full = torch.cat([s2 * LN2, torch.zeros(len(i), npad)], 1)
+                if full.shape[1] == 0:                               # an empty part: o = 0, lse = -inf
+                    o[n, i_lo:i_hi, h] = 0
+                    lse[n, h, i_lo:i_hi] = -float("inf")
+                    wr[n, i_lo:i_hi, h] = True
+                    continue
                 l_ = torch.logsumexp(full, 1)
                 p = torch.exp(s2 * LN2 - l_[:, None])
                 o[n, i_lo:i_hi, h] = (p @ V).to(o.dtype)

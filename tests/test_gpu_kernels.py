@@ -655,6 +655,88 @@ def test_window_and_sparsified_kv_match_full_launch(name, L, segs, ratios, wins)
     assert torch.equal(merged.view(torch.int16), full_merge.view(torch.int16))
 
 
+KEY_PART_CASES = [
+    # name, L, segs, ratios, {branch: parts}, q gain (> 1: logits past the no-max kernel's range -> fixup pass)
+    ("default_20000", 20000, [1024, 5792, 32768, 185363, 1048576], [1, 2, 4, 8, 16], {2: 3, 3: 2, 4: 3}, 1.0),
+    ("tiny_700_empty_parts", 700, [64, 130, 250, 333, 1000], [1, 2, 4, 8, 16], {0: 3, 1: 2, 4: 3}, 1.0),
+    ("fixup_9000", 9000, [1024, 5792, 32768, 185363, 1048576], [1, 2, 4, 8, 16], {1: 2, 2: 3, 4: 3}, 40.0),
+]
+
+
+@pytest.mark.parametrize("name,L,segs,ratios,parts,gain", KEY_PART_CASES)
+def test_key_parts_combine_to_the_branch_softmax(name, L, segs, ratios, parts, gain):
+    """GpAttnBranch.key_parts (ABI 10): a branch's keys split over P entries of one launch; each part is a
+    softmax over its 64-key tiles (the zero-pad keys in the last part; a part without keys o = 0, lse = -inf),
+    and the parts combined by their LSEs give the branch's own (o, lse) -- lse to 2^-7 (bf16 P row sums), o to
+    bf16 rounding (each part's o is rounded once before the combination).  The merge of the part entries equals the
+    merge of the whole branches to the same bound."""
+    h = _hip()
+    H, D = 16, 48
+    E = H * D
+    qkv = _rand_qkv(1, L, E, seed=L + 11).float()
+    qkv[:, :E] *= D ** -0.5 * 1.4426950408889634 * gain
+    qkv = qkv.bfloat16().to(DEV)
+    k = qkv[:, E:]
+    bs = sorted(parts)
+    whole, split = {}, {}
+    for b in bs:
+        geo = orc.branch_geometry(L, segs[b], ratios[b], H)
+        n_o, n_l = geo["nseg"] * geo["m"] * H * D, geo["nseg"] * H * geo["m"]
+        whole[b] = (torch.full((n_o,), float("nan"), dtype=torch.bfloat16, device=DEV),
+                    torch.full((n_l,), float("nan"), dtype=torch.float32, device=DEV))
+        split[b] = [(torch.full((n_o,), float("nan"), dtype=torch.bfloat16, device=DEV),
+                     torch.full((n_l,), float("nan"), dtype=torch.float32, device=DEV)) for _ in range(parts[b])]
+    d_whole = [h.attn_branch(segs[b], ratios[b], k, k.data_ptr() + 2 * E, 3 * E, 0, False, *whole[b]) for b in bs]
+    d_split = [h.attn_branch(segs[b], ratios[b], k, k.data_ptr() + 2 * E, 3 * E, 0, False, o, l, p, parts[b])
+               for b in bs for p, (o, l) in enumerate(split[b])]
+    assert len(d_split) <= h.MAX_BRANCHES
+    h.dilated_attn_fwd_ex(qkv, 3 * E, 0, 1, L, H, D, 0, L, d_whole, 0.0, True)
+    h.dilated_attn_fwd_ex(qkv, 3 * E, 0, 1, L, H, D, 0, L, d_split, 0.0, True)
+    torch.cuda.synchronize()
+    for b in bs:
+        geo = orc.branch_geometry(L, segs[b], ratios[b], H)
+        nseg, m = geo["nseg"], geo["m"]
+        need = _rows_needed(L, segs[b], ratios[b], H)
+        mask = torch.from_numpy(np.arange(m)[None, None, :] < need[:, :, None])      # [nseg, H, m]
+        wo = whole[b][0].view(nseg, m, H, D).permute(0, 2, 1, 3).cpu().float()[mask]
+        wl = whole[b][1].view(nseg, H, m).cpu()[mask]
+        po = torch.stack([o.view(nseg, m, H, D).permute(0, 2, 1, 3).cpu().float()[mask] for o, _ in split[b]])
+        pl = torch.stack([l.view(nseg, H, m).cpu()[mask] for _, l in split[b]]).double()
+        assert torch.isfinite(wl).all() and not torch.isnan(pl).any() and not torch.isnan(po).any(), (name, b)
+        lc = torch.logsumexp(pl, 0)
+        # the no-max kernel's row sums come from bf16 P (the ones-column MFMA, 2^-9 per term: a row one key
+        # dominates is off by up to ~2^-8 in lse, whole and parts each); the fixup kernel's max is a bf16 hi + lo
+        # pair (2^-16 relative)
+        lerr = ((lc - wl.double()).abs() - 2e-5 * wl.double().abs()).max().item()
+        assert lerr <= 2 ** -7, (name, b, lerr)
+        oc = (torch.exp(pl - lc)[..., None] * po.double()).sum(0)
+        err = (oc - wo.double()).abs().max().item()
+        assert err <= 2 ** -7 * wo.abs().max().item() + 1e-6, (name, b, err)
+        empty = torch.isinf(pl) & (pl < 0)
+        assert (po[empty] == 0).all(), (name, b)
+    if name.startswith("tiny"):
+        assert any((torch.isinf(l) & (l < 0)).any() for b in bs for _, l in split[b]), "no empty part exercised"
+    # merge of the part entries vs the whole branches (branches not split ride along whole in both)
+    full_o, full_l = _run_attn(h, qkv.cpu(), 1, L, H, D, segs, ratios, prescaled=True)
+    ref = torch.empty(L, E, dtype=torch.bfloat16, device=DEV)
+    h.branch_merge_ln(full_o, full_l, segs, ratios, 1, L, H, D, None, None, 1e-5, ref)
+    chosen, n_ent = [], len(segs)          # as many split branches as fit the merge's 8 entries
+    for b in bs:
+        if n_ent + parts[b] - 1 <= h.MAX_BRANCHES:
+            chosen.append(b)
+            n_ent += parts[b] - 1
+    assert chosen
+    outs, lses, ss, rs = [], [], [], []
+    for b in range(len(segs)):
+        for o, l in (split[b] if b in chosen else [(full_o[b], full_l[b])]):
+            outs.append(o); lses.append(l); ss.append(segs[b]); rs.append(ratios[b])
+    got = torch.empty(L, E, dtype=torch.bfloat16, device=DEV)
+    h.branch_merge_ln(outs, lses, ss, rs, 1, L, H, D, None, None, 1e-5, got)
+    torch.cuda.synchronize()
+    err = (got.float() - ref.float()).abs().max().item()
+    assert err <= 2 ** -6 * ref.float().abs().max().item(), (name, chosen, err)
+
+
 def test_sparsify_bit_exact_and_partial_buffers():
     h = _hip()
     H, D, L = 16, 48, 1000

@@ -135,6 +135,29 @@ def test_branches_without_transfers():
     assert not any(bal.no_xfer)
 
 
+def test_key_parts_split_only_underfilled_launches():
+    """seqpar.plan_key_parts: at 256k / 8 ranks the long branches' launch (~384-480 8-wave items for 768 slots)
+    splits both branches' keys in two; the filled launches (and every launch at W = 2) keep whole branches;
+    the merge's entries never exceed GP_MAX_BRANCHES."""
+    segs, ratios = [1024, 5792, 32768, 185363, 1048576], [1, 2, 4, 8, 16]
+    for W in (2, 4, 8):
+        plan = seqpar.ShardPlan(256001, W, segs, ratios, 16, 48, 3072)
+        for r in range(W):
+            eng = seqpar.SeqParallelEngine(plan, r, None)
+            kp = eng.parts()
+            assert sum(kp) <= 8
+            a, e = plan.bounds[r]
+            for br in eng._launches():
+                items = sum(seqpar.launch_items(plan.geo[b], 16, a, e) for b in br)
+                assert all(kp[b] == 1 for b in br) == (items >= 3 * 256), (W, r, br, items, kp)
+            if W == 8:
+                assert kp == [1, 1, 1, 2, 2], (r, kp)
+            if W == 2:
+                assert kp == [1] * 5
+    eng.key_parts = {4: 3}
+    assert eng.parts() == [1, 1, 1, 1, 3]
+
+
 def test_exchange_volume_is_sparse():
     """At 256k / 8 ranks each rank receives far less than the dense K/V (786 MB per layer)."""
     plan = seqpar.ShardPlan(256001, 8, *DEFAULT, H, D, F)
@@ -228,14 +251,15 @@ def _sp_model(segs, ratios):
     return m.eval(), cfg
 
 
-def _sp_forward_worker(rank, world, port, N, gp, q, local_first=False, monitor=False):
+def _sp_forward_worker(rank, world, port, N, gp, q, local_first=False, monitor=False, key_parts=None):
     try:
         import sp_emulator
         sp_emulator.install()
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)
         torch.set_num_threads(2)
-        seqpar.SeqParallelEngine.local_first = local_first      # class default for the engine built below
+        seqpar.SeqParallelEngine.local_first = local_first      # class defaults for the engine built below
+        seqpar.SeqParallelEngine.key_parts = key_parts
         model, _ = _sp_model(*SP_SCHED)
         model.global_pool = gp
         model.enable_sequence_parallel()
@@ -253,17 +277,19 @@ def _sp_forward_worker(rank, world, port, N, gp, q, local_first=False, monitor=F
         q.put((rank, traceback.format_exc()))
 
 
-@pytest.mark.parametrize("world,N,gp,local_first", [(2, 600, False, False), (3, 700, True, False),
-                                                    (2, 600, False, True)])
-def test_sharded_forward_matches_oracle_with_cpu_kernels(world, N, gp, local_first):
-    monitor = world == 2 and not local_first
+@pytest.mark.parametrize("world,N,gp,local_first,key_parts", [(2, 600, False, False, None), (3, 700, True, False, None),
+                                                              (2, 600, False, True, None),
+                                                              (2, 600, False, True, {1: 2, 4: 3})])
+def test_sharded_forward_matches_oracle_with_cpu_kernels(world, N, gp, local_first, key_parts):
     """LongNetViT._forward_sp end to end over gloo with every HIP call replaced by an
     address-checking CPU stand-in (tests/sp_emulator.py): shard bounds, K/V and q-halo
-    exchange, query windows, window merge, readouts, all-reduce/broadcast."""
+    exchange, query windows, window merge, readouts, all-reduce/broadcast.  key_parts: branch 1's two key
+    tiles in two parts, branch 4's one tile in three (two empty parts: o = 0, lse = -inf)."""
+    monitor = world == 2 and not local_first and not key_parts
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_sp_forward_worker, args=(r, world, port, N, gp, q, local_first, monitor))
+    procs = [ctx.Process(target=_sp_forward_worker, args=(r, world, port, N, gp, q, local_first, monitor, key_parts))
              for r in range(world)]
     for p in procs:
         p.start()

@@ -45,6 +45,8 @@ def main():
     ap.add_argument("--phases", default="2", help="comma list of attention launch splits to time: "
                     "2 = the plan's (short branches, long branches), 3 = the long branches split by "
                     "whole-sequence vs multi-segment, 1 = one launch")
+    ap.add_argument("--key-parts", default="default",
+                    help="comma list of key-part settings: default (the engine's rule), none, or b=P[/b=P...]")
     args = ap.parse_args()
     if args.lib:
         from gigapath import _hip
@@ -58,8 +60,15 @@ def main():
     L = args.tiles + 1
     g = torch.Generator(device=dev).manual_seed(0)
     out = {"tiles": args.tiles, "worlds": {}}
-    for W, nph, lf in [(int(w), int(p), int(f)) for w in args.worlds.split(",") for p in args.phases.split(",")
-                       for f in args.local_first.split(",")]:
+    def parse_kp(spec):
+        if spec == "default":
+            return None
+        if spec == "none":
+            return {}
+        return {int(x.split("=")[0]): int(x.split("=")[1]) for x in spec.split("/")}
+    for W, nph, lf, kps in [(int(w), int(p), int(f), k) for w in args.worlds.split(",")
+                            for p in args.phases.split(",") for f in args.local_first.split(",")
+                            for k in args.key_parts.split(",")]:
         plan = seqpar.ShardPlan(L, W, pa.segs, pa.ratios, pa.H, pa.D, F)
         if nph == 3:            # the round-2 plan: whole-sequence branches in a launch of their own
             long_ = plan.phase_b1
@@ -83,6 +92,7 @@ def main():
             eng = seqpar.SeqParallelEngine(plan, r, NullExchange())
             eng.use_graphs = True
             eng.local_first = bool(lf)
+            eng.key_parts = parse_kp(kps)
             x0 = ws.x.clone()
             with torch.no_grad():
                 eng.run_layers(layers, ws, shift_ready=True)               # eager + capture
@@ -117,14 +127,15 @@ def main():
             aA = spans.get("attn_A", 0.0) / nl
             expA = max(0.0, tA - aL)
             expB = max(0.0, tA + tB - max(tA, aL) - aA)
-            ranks.append({"rank": r, "tokens": b - a, "ms": round(best, 3),
+            ranks.append({"rank": r, "tokens": b - a, "ms": round(best, 3), "key_parts": eng.parts(),
                           "recv_MB_per_layer": round(plan.exchange_bytes(r) / 1e6, 1), "spans_ms": spans,
                           "link_ms_per_layer": {"A": round(tA, 3), "B": round(tB, 3)},
                           "modelled_exposed_ms": round(nl * (expA + expB), 3),
                           "ms_plus_exposed": round(best + nl * (expA + expB), 3)})
             del eng, ws
             torch.cuda.empty_cache()
-        key = str(W) + ("" if nph == 2 else "/phases%d" % nph) + ("/local-first" if lf else "")
+        key = str(W) + ("" if nph == 2 else "/phases%d" % nph) + ("/local-first" if lf else "") + \
+            ("" if kps == "default" else "/kp:" + kps)
         out["worlds"][key] = {"max_ms": max(x["ms"] for x in ranks), "ranks": ranks,
                               "max_ms_plus_exposed": max(x["ms_plus_exposed"] for x in ranks),
                               "link_bytes_per_s": seqpar.LINK_BYTES_PER_S}
