@@ -47,6 +47,8 @@ def main():
                     "whole-sequence vs multi-segment, 1 = one launch")
     ap.add_argument("--key-parts", default="default",
                     help="comma list of key-part settings: default (the engine's rule), none, or b=P[/b=P...]")
+    ap.add_argument("--bounds", default="plan", help="comma list: plan (ShardPlan's choice), balanced (the "
+                    "cost-balanced cuts, never snapped to a segment multiple)")
     args = ap.parse_args()
     if args.lib:
         from gigapath import _hip
@@ -66,10 +68,13 @@ def main():
         if spec == "none":
             return {}
         return {int(x.split("=")[0]): int(x.split("=")[1]) for x in spec.split("/")}
-    for W, nph, lf, kps in [(int(w), int(p), int(f), k) for w in args.worlds.split(",")
-                            for p in args.phases.split(",") for f in args.local_first.split(",")
-                            for k in args.key_parts.split(",")]:
-        plan = seqpar.ShardPlan(L, W, pa.segs, pa.ratios, pa.H, pa.D, F)
+    for W, nph, lf, kps, bnd in [(int(w), int(p), int(f), k, bd) for w in args.worlds.split(",")
+                                 for p in args.phases.split(",") for f in args.local_first.split(",")
+                                 for k in args.key_parts.split(",") for bd in args.bounds.split(",")]:
+        cuts = None
+        if bnd == "balanced":
+            cuts = seqpar.balanced_bounds(seqpar.token_cost(L, pa.segs, pa.ratios, pa.H, pa.D, F), W)
+        plan = seqpar.ShardPlan(L, W, pa.segs, pa.ratios, pa.H, pa.D, F, bounds=cuts)
         if nph == 3:            # the round-2 plan: whole-sequence branches in a launch of their own
             long_ = plan.phase_b1
             plan.phase_b1 = [b for b in long_ if plan.geo[b].nseg > 1]
@@ -135,7 +140,7 @@ def main():
             del eng, ws
             torch.cuda.empty_cache()
         key = str(W) + ("" if nph == 2 else "/phases%d" % nph) + ("/local-first" if lf else "") + \
-            ("" if kps == "default" else "/kp:" + kps)
+            ("" if kps == "default" else "/kp:" + kps) + ("" if bnd == "plan" else "/bounds:" + bnd)
         out["worlds"][key] = {"max_ms": max(x["ms"] for x in ranks), "ranks": ranks,
                               "max_ms_plus_exposed": max(x["ms_plus_exposed"] for x in ranks),
                               "link_bytes_per_s": seqpar.LINK_BYTES_PER_S}
