@@ -160,7 +160,8 @@ def sp_rank_report(model, kt, rank, timing_steps, L, segs, ratios, monitor):
     send = sum((hi - lo) * 2 * plan.C[b] * 2 for b, _, lo, hi in plan.sends(rank))
     send += sum((hi - lo) * 3 * plan.E * 2 for _, lo, hi in plan.halo_sends(rank))
     fl = runtime.attention_valid_flops_window(L, segs, ratios, 16, 48, a_w, b_w)
-    n_att, ms_att = kt.get("attn", (0, 0.0))
+    # (the SP engine labels its attention launches by exchange phase: attn_local / attn_A / attn_B)
+    ms_att = sum(v[1] for k, v in kt.items() if k.startswith("attn"))
     att_s = ms_att / max(timing_steps * nl, 1) / 1e3
     sp_bytes = sum((b_w - a_w) * 2 * plan.C[b] * 2 + sum(plan.send_splits(rank, b)) * 2 * plan.C[b] * 2
                    for b in range(len(plan.C)) if not plan.no_xfer[b])
