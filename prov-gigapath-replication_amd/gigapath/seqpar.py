@@ -580,10 +580,14 @@ class SeqParallelEngine:
         self.key_parts = type(self).key_parts
         self._kp = [1] * len(plan.geo)
 
-    def parts(self) -> List[int]:
-        """Key parts per branch this forward runs with."""
+    def parts(self, pa: Optional[runtime.PackedAttention] = None, act: Optional[torch.dtype] = None) -> List[int]:
+        """Key parts per branch this forward runs with.  The rule splits only where the kernel has parts: the
+        LDS-DMA pair (D = 48, pre-scaled q) on a bf16 qkv or the fp16 caller's bf16-V qkv (an explicit
+        key_parts dict is passed through; the library refuses it elsewhere)."""
         if self.key_parts is not None:
             return [max(1, int(self.key_parts.get(b, 1))) for b in range(len(self.plan.geo))]
+        if pa is not None and not (pa.D == 48 and pa.prescaled and (act == torch.bfloat16 or pa.v_bf16)):
+            return [1] * len(self.plan.geo)
         n_cu = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count \
             if torch.cuda.is_available() else 256
         return plan_key_parts(self.plan, self.rank, self._launches(), n_cu)
@@ -759,7 +763,7 @@ class SeqParallelEngine:
         ph_a = [b for b in plan.phase_a if b not in local]
         ph_b1 = [b for b in plan.phase_b1 if b not in local]
         ph_b2 = [b for b in plan.phase_b2 if b not in local]
-        self._kp = self.parts()
+        self._kp = self.parts(layers[0].attn if layers else None, ws.qkv.dtype)
         wsig = (weights_sig if weights_sig is not None else id(layers), tuple(self._kp))
         if wsig != self._graph_sig:          # new weights / parts: captures of the old ones never replay
             self.graphs.clear()
