@@ -48,7 +48,7 @@ def main():
     ap.add_argument("--key-parts", default="default",
                     help="comma list of key-part settings: default (the engine's rule), none, or b=P[/b=P...]")
     ap.add_argument("--bounds", default="plan", help="comma list: plan (ShardPlan's choice), balanced (the "
-                    "cost-balanced cuts, never snapped to a segment multiple)")
+                    "cost-balanced cuts, never snapped to a segment multiple), cuts:c1/c2/... (explicit)")
     args = ap.parse_args()
     if args.lib:
         from gigapath import _hip
@@ -74,6 +74,10 @@ def main():
         cuts = None
         if bnd == "balanced":
             cuts = seqpar.balanced_bounds(seqpar.token_cost(L, pa.segs, pa.ratios, pa.H, pa.D, F), W)
+        elif bnd.startswith("cuts:"):                  # explicit cuts, e.g. cuts:124928 at W = 2
+            cs = [0] + [int(x) for x in bnd[5:].split("/")] + [L]
+            assert len(cs) == W + 1, bnd
+            cuts = [(cs[w], cs[w + 1]) for w in range(W)]
         plan = seqpar.ShardPlan(L, W, pa.segs, pa.ratios, pa.H, pa.D, F, bounds=cuts)
         if nph == 3:            # the round-2 plan: whole-sequence branches in a launch of their own
             long_ = plan.phase_b1
