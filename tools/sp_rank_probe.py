@@ -49,6 +49,8 @@ def main():
                     help="comma list of key-part settings: default (the engine's rule), none, or b=P[/b=P...]")
     ap.add_argument("--bounds", default="plan", help="comma list: plan (ShardPlan's choice), balanced (the "
                     "cost-balanced cuts, never snapped to a segment multiple), cuts:c1/c2/... (explicit)")
+    ap.add_argument("--per-branch", action="store_true",
+                    help="also time each branch's attention as a launch of its own (valid TFLOP/s per branch)")
     args = ap.parse_args()
     if args.lib:
         from gigapath import _hip
@@ -125,6 +127,22 @@ def main():
                 eng.run_layers(layers, ws, shift_ready=True)
                 spans = {k: round(v[1], 3) for k, v in sorted(runtime.TIMER.totals_ms().items())}
                 runtime.TIMER.enabled = False
+                per_branch = {}
+                if args.per_branch:        # each branch alone, the engine's key parts, median of 5
+                    a_, e_ = plan.bounds[r]
+                    for b in range(len(plan.geo)):
+                        ts = []
+                        for _ in range(6):
+                            s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                            s0.record()
+                            eng.attention(pa, ws, [b], "br")
+                            s1.record()
+                            s1.synchronize()
+                            ts.append(s0.elapsed_time(s1))
+                        ms = sorted(ts[1:])[2]
+                        fl = runtime.attention_valid_flops_window(L, [pa.segs[b]], [pa.ratios[b]], pa.H, pa.D, a_, e_)
+                        per_branch[b] = {"ms": round(ms, 4), "valid_tflops": round(fl / ms / 1e9, 1),
+                                         "parts": eng._kp[b]}
             a, b = plan.bounds[r]
             # modelled exposed transfer: per layer, both phases posted together after the head;
             # phase A's busiest incoming link must land before the short-branch attention (only the
@@ -138,6 +156,7 @@ def main():
             expB = max(0.0, tA + tB - max(tA, aL) - aA)
             ranks.append({"rank": r, "tokens": b - a, "ms": round(best, 3), "key_parts": eng.parts(),
                           "recv_MB_per_layer": round(plan.exchange_bytes(r) / 1e6, 1), "spans_ms": spans,
+                          "per_branch_attention": per_branch,
                           "link_ms_per_layer": {"A": round(tA, 3), "B": round(tB, 3)},
                           "modelled_exposed_ms": round(nl * (expA + expB), 3),
                           "ms_plus_exposed": round(best + nl * (expA + expB), 3)})
