@@ -656,15 +656,18 @@ def test_window_and_sparsified_kv_match_full_launch(name, L, segs, ratios, wins)
 
 
 KEY_PART_CASES = [
-    # name, L, segs, ratios, {branch: parts}, q gain (> 1: logits past the no-max kernel's range -> fixup pass)
-    ("default_20000", 20000, [1024, 5792, 32768, 185363, 1048576], [1, 2, 4, 8, 16], {2: 3, 3: 2, 4: 3}, 1.0),
-    ("tiny_700_empty_parts", 700, [64, 130, 250, 333, 1000], [1, 2, 4, 8, 16], {0: 3, 1: 2, 4: 3}, 1.0),
-    ("fixup_9000", 9000, [1024, 5792, 32768, 185363, 1048576], [1, 2, 4, 8, 16], {1: 2, 2: 3, 4: 3}, 40.0),
+    # name, L, segs, ratios, {branch: parts}, q gain (> 1: logits past the no-max kernel's range -> fixup pass),
+    # fp16 q / k with a bf16 V (GP_FMT_F16_VBF16, the fp16 caller's pair)
+    ("default_20000", 20000, [1024, 5792, 32768, 185363, 1048576], [1, 2, 4, 8, 16], {2: 3, 3: 2, 4: 3}, 1.0, False),
+    ("tiny_700_empty_parts", 700, [64, 130, 250, 333, 1000], [1, 2, 4, 8, 16], {0: 3, 1: 2, 4: 3}, 1.0, False),
+    ("fixup_9000", 9000, [1024, 5792, 32768, 185363, 1048576], [1, 2, 4, 8, 16], {1: 2, 2: 3, 4: 3}, 40.0, False),
+    ("fp16_vbf16_9000", 9000, [1024, 5792, 32768, 185363, 1048576], [1, 2, 4, 8, 16], {2: 3, 3: 2, 4: 3}, 1.0,
+     True),
 ]
 
 
-@pytest.mark.parametrize("name,L,segs,ratios,parts,gain", KEY_PART_CASES)
-def test_key_parts_combine_to_the_branch_softmax(name, L, segs, ratios, parts, gain):
+@pytest.mark.parametrize("name,L,segs,ratios,parts,gain,vbf16", KEY_PART_CASES)
+def test_key_parts_combine_to_the_branch_softmax(name, L, segs, ratios, parts, gain, vbf16):
     """GpAttnBranch.key_parts (ABI 10): a branch's keys split over P entries of one launch; each part is a
     softmax over its 64-key tiles (the zero-pad keys in the last part; a part without keys o = 0, lse = -inf),
     and the parts combined by their LSEs give the branch's own (o, lse) -- lse to 2^-7 (bf16 P row sums), o to
@@ -675,23 +678,24 @@ def test_key_parts_combine_to_the_branch_softmax(name, L, segs, ratios, parts, g
     E = H * D
     qkv = _rand_qkv(1, L, E, seed=L + 11).float()
     qkv[:, :E] *= D ** -0.5 * 1.4426950408889634 * gain
-    qkv = qkv.bfloat16().to(DEV)
+    qkv = (_fp16_qkv_vbf16(qkv, E)[0] if vbf16 else qkv.bfloat16()).to(DEV)
+    act = qkv.dtype
     k = qkv[:, E:]
     bs = sorted(parts)
     whole, split = {}, {}
     for b in bs:
         geo = orc.branch_geometry(L, segs[b], ratios[b], H)
         n_o, n_l = geo["nseg"] * geo["m"] * H * D, geo["nseg"] * H * geo["m"]
-        whole[b] = (torch.full((n_o,), float("nan"), dtype=torch.bfloat16, device=DEV),
+        whole[b] = (torch.full((n_o,), float("nan"), dtype=act, device=DEV),
                     torch.full((n_l,), float("nan"), dtype=torch.float32, device=DEV))
-        split[b] = [(torch.full((n_o,), float("nan"), dtype=torch.bfloat16, device=DEV),
+        split[b] = [(torch.full((n_o,), float("nan"), dtype=act, device=DEV),
                      torch.full((n_l,), float("nan"), dtype=torch.float32, device=DEV)) for _ in range(parts[b])]
     d_whole = [h.attn_branch(segs[b], ratios[b], k, k.data_ptr() + 2 * E, 3 * E, 0, False, *whole[b]) for b in bs]
     d_split = [h.attn_branch(segs[b], ratios[b], k, k.data_ptr() + 2 * E, 3 * E, 0, False, o, l, p, parts[b])
                for b in bs for p, (o, l) in enumerate(split[b])]
     assert len(d_split) <= h.MAX_BRANCHES
-    h.dilated_attn_fwd_ex(qkv, 3 * E, 0, 1, L, H, D, 0, L, d_whole, 0.0, True)
-    h.dilated_attn_fwd_ex(qkv, 3 * E, 0, 1, L, H, D, 0, L, d_split, 0.0, True)
+    h.dilated_attn_fwd_ex(qkv, 3 * E, 0, 1, L, H, D, 0, L, d_whole, 0.0, True, v_bf16=vbf16)
+    h.dilated_attn_fwd_ex(qkv, 3 * E, 0, 1, L, H, D, 0, L, d_split, 0.0, True, v_bf16=vbf16)
     torch.cuda.synchronize()
     for b in bs:
         geo = orc.branch_geometry(L, segs[b], ratios[b], H)
@@ -716,6 +720,8 @@ def test_key_parts_combine_to_the_branch_softmax(name, L, segs, ratios, parts, g
         assert (po[empty] == 0).all(), (name, b)
     if name.startswith("tiny"):
         assert any((torch.isinf(l) & (l < 0)).any() for b in bs for _, l in split[b]), "no empty part exercised"
+    if vbf16:        # (the merge below compares with the bf16 single-launch path)
+        return
     # merge of the part entries vs the whole branches (branches not split ride along whole in both)
     full_o, full_l = _run_attn(h, qkv.cpu(), 1, L, H, D, segs, ratios, prescaled=True)
     ref = torch.empty(L, E, dtype=torch.bfloat16, device=DEV)
