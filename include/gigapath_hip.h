@@ -140,6 +140,14 @@ int gp_dilated_attn_fwd_ex(const uint16_t* q, int64_t q_row_stride, int64_t q_to
                            const GpAttnBranch* branches, int nbranch, float softmax_scale,
                            int q_log2_prescaled, int fmt, void* stream);
 
+/* The attention launch plan's build constants, for host-side planners that size work against it
+ * (gigapath/seqpar.py's key-part rule; no reference counterpart -- the reference has no launch plan):
+ * params[0] = query rows per 8-wave LDS-DMA work item (256), params[1] = such workgroups resident per
+ * CU (3), params[2] = 8-wave items per CU below which a launch counts as under-filled and runs 4-wave
+ * workgroups (3; 0 when that switch is built off), params[3] = largest key_parts (64).  n: entries of
+ * params (at most 4 are written).  Host only, no device work. */
+int gp_attn_launch_params(int32_t* params, int n);
+
 /* Token-major sparsified K/V rows for sequence parallelism (one rank's share of
  * DilatedAttention.gathering, dilated_attention.py:16-31,76-98).  For tokens
  * p in [tok_lo, tok_lo + n_tok) (rows of src, first row = tok_lo) and branch b with

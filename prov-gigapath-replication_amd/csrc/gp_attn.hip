@@ -1273,6 +1273,192 @@ __global__ __launch_bounds__(256) void branch_merge_kernel(const MergeArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
+// Merge for E = 768, D = 48 (H = 16: every registered 768-wide arch, the product path), one token per
+// wave as branch_merge_kernel, with fewer vector instructions per token (that kernel issues ~380 VALU
+// per token-wave, ~70 of them 64-bit per-lane address arithmetic, and 12 dependent ds_bpermute for the
+// LN sums):
+//  * a lane owns two column chunks: 8 columns (one 16-byte access) and 4 columns (one 8-byte access)
+//    instead of three 8-byte accesses of 12 contiguous columns.  kMap 0: both in head l / 4 (lane k of
+//    a head: columns 8k.. and 32 + 4k.. of the head); kMap 1 ("x8"): [8l, 8l + 8) of head l / 6 and
+//    [512 + 4l, 516 + 4l) of head (128 + l) / 12, so each wave-instruction covers one contiguous span;
+//  * loads address a wave-uniform row base plus a 32-bit lane offset (no per-lane 64-bit math);
+//  * the LN row sums are xor-butterflies (DPP quad_perm / row_half_mirror / row_ror:8, then
+//    v_permlane16/32_swap): the same sum in every lane, no LDS round trips.
+// Per (token, head) the branch weights and the fp32 accumulation are branch_merge_kernel's bit for bit
+// (dilated_attention.py:100-131).
+#ifndef GP_MERGE_MAP
+#define GP_MERGE_MAP 0
+#endif
+
+// A 32-bit lane offset the compiler may not re-associate with constants: keeps a uniform-base + lane-offset
+// load in its SGPR-base (saddr) form instead of a per-lane 64-bit address.
+GP_DEV uint32_t opaque_u32(uint32_t x) {
+  __asm__("" : "+v"(x));
+  return x;
+}
+
+GP_DEV float wave_sum_xor(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xf, 0xf, false));   // quad_perm 1,0,3,2
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xf, 0xf, false));   // quad_perm 2,3,0,1
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xf, 0xf, false));  // row_half_mirror
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, false));  // row_ror:8
+  const auto s16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(s16[0]) + __uint_as_float(s16[1]);
+  const auto s32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(s32[0]) + __uint_as_float(s32[1]);
+}
+
+template <int NBR, bool kTab, bool kH, int kMap = GP_MERGE_MAP>
+__global__ __launch_bounds__(256) void branch_merge_v2_kernel(const MergeArgs a) {
+  constexpr int E = 768, H = 16, D = 48;
+  constexpr bool k1h = kMap == 0;          // one head per lane
+  const int nbr = NBR < GP_MAX_BRANCHES ? NBR : a.nbranch;
+  const int lane = threadIdx.x & 63;
+  const int row = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + (int)(threadIdx.x >> 6));
+  const int total = (int)(a.B * a.ntok);
+  if (row >= total) return;
+  // the lane's chunks: columns c0 .. c0 + 7 (head h0) and c1 .. c1 + 3 (head h1)
+  const int kq = lane & 3;
+  const int h0 = k1h ? lane >> 2 : lane / 6;
+  const int h1 = k1h ? h0 : (128 + lane) / 12;
+  const int c0 = k1h ? D * h0 + 8 * kq : 8 * lane;
+  const int c1 = k1h ? D * h0 + 32 + 4 * kq : 512 + 4 * lane;
+  // LN affine (L1-resident): issued with the branch loads; a null ln_w reads the output row's own
+  // location instead (valid memory, unused) so the registers need no zero-fill
+  const bool ln = a.ln_w != nullptr;
+  const float* lw = ln ? a.ln_w : reinterpret_cast<const float*>(a.out);
+  const float* lb = ln ? a.ln_b : reinterpret_cast<const float*>(a.out);
+  float w0[8], w1[4], b0[8], b1[4];
+  load_f32<8>(lw + c0, w0);
+  load_f32<4>(lw + c1, w1);
+  load_f32<8>(lb + c0, b0);
+  load_f32<4>(lb + c1, b1);
+  int bidx = 0, p;
+  MergeBranch tb[kTab ? GP_MAX_BRANCHES : 1];
+  if constexpr (kTab) {
+    int lo = 0, hi = a.nslide - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if ((int64_t)row >= a.tok_off[mid]) lo = mid; else hi = mid - 1;
+    }
+    p = (int)(row - a.tok_off[lo]);
+#pragma unroll
+    for (int b = 0; b < NBR; ++b)
+      if (b < nbr) tb[b] = a.mtab[lo * a.nbranch + b];
+  } else {
+    bidx = (int)div_magic((uint32_t)row, a.dnt);
+    p = (int)a.tok_lo + (row - bidx * (int)a.ntok);
+  }
+  // every branch's loads before any wait; a lane outside the branch's head group reads the group's
+  // first head (same cache lines as the covered lanes) and gets weight 0
+  uint4 o0[NBR];
+  uint2 o1[NBR];
+  float l0[NBR], l1[NBR];
+  bool cv0[NBR], cv1[NBR];
+#pragma unroll
+  for (int b = 0; b < NBR; ++b) {
+    cv0[b] = cv1[b] = false;
+    l0[b] = l1[b] = -1e8f;
+    o0[b] = make_uint4(0, 0, 0, 0);
+    o1[b] = make_uint2(0, 0);
+    if (b < nbr) {
+      const MergeBranch& mb = kTab ? tb[b] : a.br[b];
+      const int pn = (int)div_magic((uint32_t)p, mb.dg);
+      const int pt = p - pn * mb.g.g;
+      const int pi = (int)div_magic((uint32_t)pt, mb.dr);
+      const int pj = pt - pi * mb.g.r;
+      const int hpg = mb.g.hpg;
+      const int hf = pj * hpg;                                 // the covered group's first head
+      // 32-bit byte offsets: the launch checks every branch's o / lse buffer is below 4 GiB
+      const uint32_t rb = (uint32_t)(bidx * mb.g.nseg + pn);
+      const char* orow = reinterpret_cast<const char*>(mb.o) + (rb * (uint32_t)mb.g.m + (uint32_t)pi) * (uint32_t)(E * 2);
+      const char* lrow = reinterpret_cast<const char*>(mb.lse) + (rb * (uint32_t)(H * mb.g.m) + (uint32_t)pi) * 4u;
+      const uint32_t m4 = (uint32_t)mb.g.m * 4u;
+      cv0[b] = (unsigned)(h0 - hf) < (unsigned)hpg;
+      const int s0 = cv0[b] ? h0 : hf;
+      // (m < 2^22 for any segment of the schedule: 24-bit multiplies)
+      l0[b] = *reinterpret_cast<const float*>(lrow + opaque_u32(__umul24((uint32_t)s0, m4)));
+      if constexpr (k1h) {
+        cv1[b] = cv0[b];
+        const uint32_t off0 = __umul24((uint32_t)s0, 2u * D) + 16u * kq;   // head s0, lane kq's columns
+        const uint32_t off1 = off0 + (uint32_t)(64 - 8 * kq);
+        o0[b] = *reinterpret_cast<const uint4*>(orow + opaque_u32(off0));
+        o1[b] = *reinterpret_cast<const uint2*>(orow + opaque_u32(off1));
+      } else {
+        cv1[b] = (unsigned)(h1 - hf) < (unsigned)hpg;
+        l1[b] = *reinterpret_cast<const float*>(lrow + opaque_u32(__umul24((uint32_t)(cv1[b] ? h1 : hf), m4)));
+        o0[b] = *reinterpret_cast<const uint4*>(orow + opaque_u32(cv0[b] ? 2 * c0 : 2 * D * hf));
+        o1[b] = *reinterpret_cast<const uint2*>(orow + opaque_u32(cv1[b] ? 2 * c1 : 2 * D * hf));
+      }
+    }
+  }
+  // per-head softmax over the branches (k1h: one head per lane)
+  float mx0 = -INFINITY, mx1 = -INFINITY;
+#pragma unroll
+  for (int b = 0; b < NBR; ++b)
+    if (b < nbr) {
+      if (!cv0[b] || l0[b] == 0.f) l0[b] = -1e8f;   // dilated_attention.py:46
+      mx0 = fmaxf(mx0, l0[b]);
+      if constexpr (!k1h) {
+        if (!cv1[b] || l1[b] == 0.f) l1[b] = -1e8f;
+        mx1 = fmaxf(mx1, l1[b]);
+      }
+    }
+  float ws0 = 0.f, ws1 = 0.f;
+#pragma unroll
+  for (int b = 0; b < NBR; ++b)
+    if (b < nbr) {
+      l0[b] = fast_exp2((l0[b] - mx0) * 1.44269504088896340736f);
+      ws0 += l0[b];
+      if constexpr (!k1h) {
+        l1[b] = fast_exp2((l1[b] - mx1) * 1.44269504088896340736f);
+        ws1 += l1[b];
+      }
+    }
+  const float inv0 = __builtin_amdgcn_rcpf(ws0), inv1 = k1h ? inv0 : __builtin_amdgcn_rcpf(ws1);
+  float v[12];
+#pragma unroll
+  for (int e = 0; e < 12; ++e) v[e] = 0.f;
+#pragma unroll
+  for (int b = 0; b < NBR; ++b)
+    if (b < nbr) {
+      const float wb0 = cv0[b] ? l0[b] * inv0 : 0.f;   // + 0 * finite leaves v unchanged
+      const float wb1 = k1h ? wb0 : (cv1[b] ? l1[b] * inv1 : 0.f);
+      const uint32_t u0[4] = {o0[b].x, o0[b].y, o0[b].z, o0[b].w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        v[2 * k] = __builtin_fmaf(e2f<kH>(u0[k]), wb0, v[2 * k]);
+        v[2 * k + 1] = __builtin_fmaf(e2f_hi<kH>(u0[k]), wb0, v[2 * k + 1]);
+      }
+      v[8] = __builtin_fmaf(e2f<kH>(o1[b].x), wb1, v[8]);
+      v[9] = __builtin_fmaf(e2f_hi<kH>(o1[b].x), wb1, v[9]);
+      v[10] = __builtin_fmaf(e2f<kH>(o1[b].y), wb1, v[10]);
+      v[11] = __builtin_fmaf(e2f_hi<kH>(o1[b].y), wb1, v[11]);
+    }
+  if (ln) {
+    float s = 0.f;
+#pragma unroll
+    for (int e = 0; e < 12; ++e) s += v[e];
+    const float mean = wave_sum_xor(s) * (1.0f / E);
+    float q = 0.f;
+#pragma unroll
+    for (int e = 0; e < 12; ++e) {
+      const float d = v[e] - mean;
+      q += d * d;
+    }
+    const float rstd = rsqrtf(wave_sum_xor(q) * (1.0f / E) + a.eps);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (v[e] - mean) * rstd * w0[e] + b0[e];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[8 + e] = (v[8 + e] - mean) * rstd * w1[e] + b1[e];
+  }
+  char* orow = reinterpret_cast<char*>(a.out) + (int64_t)row * (E * 2);
+  *reinterpret_cast<uint4*>(orow + 2 * c0) =
+      make_uint4(pack2e<kH>(v[0], v[1]), pack2e<kH>(v[2], v[3]), pack2e<kH>(v[4], v[5]), pack2e<kH>(v[6], v[7]));
+  *reinterpret_cast<uint2*>(orow + 2 * c1) = make_uint2(pack2e<kH>(v[8], v[9]), pack2e<kH>(v[10], v[11]));
+}
+
+// ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void dilated_gather_kernel(const uint16_t* __restrict__ src, int64_t row_stride,
                                                              int64_t col_off, int64_t L, int H, int D, GpBranch g,
                                                              int64_t total_rows, uint16_t* __restrict__ dst) {
@@ -1336,6 +1522,14 @@ static int attn_num_cus(hipStream_t s) {     // per-device cache of the CU count
 #ifndef GP_ATTN_SMALL_LAUNCH_PER_CU
 #define GP_ATTN_SMALL_LAUNCH_PER_CU 3
 #endif
+
+extern "C" int gp_attn_launch_params(int32_t* params, int n) {
+  GP_REQUIRE(params && n >= 0, "gp_attn_launch_params: null params");
+  const int32_t v[4] = {32 * kNWFast, GP_ATTN_FAST_WPS * 4 / kNWFast,
+                        GP_ATTN_SMALL_LAUNCH_NW4 ? GP_ATTN_SMALL_LAUNCH_PER_CU : 0, 64};
+  for (int i = 0; i < n && i < 4; ++i) params[i] = v[i];
+  return 0;
+}
 
 // fmt: GP_FMT_BF16, GP_FMT_F16 (fp16 q / k / v) or GP_FMT_F16_VBF16 (fp16 q / k, bf16 v; o fp16)
 static int attn_fwd_impl(const uint16_t* q, int64_t q_row_stride, int64_t q_tok_base, int64_t B, int64_t L, int H,
@@ -1590,15 +1784,26 @@ extern "C" int gp_branch_merge_ln(const uint16_t* const* o_in, const float* cons
                                    fmt, stream);
 }
 
+// the E = 768 / D = 48 merge: one token per wave, 4 waves per block
+static unsigned merge_v2_grid(int64_t tokens) { return (unsigned)((tokens + 3) / 4); }
+// its 32-bit byte offsets: every branch's o rows (B * nseg * m rows of 1,536 B) below 4 GiB
+static bool merge_v2_fits(const MergeArgs& a) {
+  for (int b = 0; b < a.nbranch; ++b)
+    if ((uint64_t)a.B * a.br[b].g.nseg * a.br[b].g.m * 1536u >= (1ull << 32)) return false;
+  return true;
+}
+
 template <bool kH>
 static void launch_merge(const MergeArgs& a, int E, int D, int nbranch, unsigned nb, hipStream_t s) {
   switch (E) {
     case 768:
-      if (D == 48 && nbranch == 5) branch_merge_kernel<12, 48, false, 5, kH><<<nb, 256, 0, s>>>(a);
-      // (5 branches, two of them in two key parts: the sequence-parallel long-branch split, seqpar.plan_key_parts)
-      else if (D == 48 && nbranch == 7) branch_merge_kernel<12, 48, false, 7, kH><<<nb, 256, 0, s>>>(a);
-      else if (D == 48) branch_merge_kernel<12, 48, false, GP_MAX_BRANCHES, kH><<<nb, 256, 0, s>>>(a);
-      else if (D == 96) branch_merge_kernel<12, 96, false, GP_MAX_BRANCHES, kH><<<nb, 256, 0, s>>>(a);
+      if (D == 48 && merge_v2_fits(a)) {
+        const unsigned g = merge_v2_grid(a.B * a.ntok);
+        if (nbranch == 5) branch_merge_v2_kernel<5, false, kH><<<g, 256, 0, s>>>(a);
+        // (5 branches, two of them in two key parts: the sequence-parallel long-branch split, seqpar.plan_key_parts)
+        else if (nbranch == 7) branch_merge_v2_kernel<7, false, kH><<<g, 256, 0, s>>>(a);
+        else branch_merge_v2_kernel<GP_MAX_BRANCHES, false, kH><<<g, 256, 0, s>>>(a);
+      } else if (D == 96) branch_merge_kernel<12, 96, false, GP_MAX_BRANCHES, kH><<<nb, 256, 0, s>>>(a);
       else branch_merge_kernel<12, 12, false, GP_MAX_BRANCHES, kH><<<nb, 256, 0, s>>>(a);
       break;
     case 1024:
@@ -1828,9 +2033,11 @@ extern "C" int gp_branch_merge_ln_varlen(const void* plan_host, const void* plan
   a.mtab = reinterpret_cast<const MergeBranch*>(static_cast<const char*>(plan_dev) + h.mtab_off);
   a.tok_off = reinterpret_cast<const int64_t*>(static_cast<const char*>(plan_dev) + h.tok_off_off);
   a.nslide = h.nslide;
-  const unsigned nb = (unsigned)((h.T + 4 * kTPW - 1) / (4 * kTPW));
-  if (fmt == GP_FMT_F16) branch_merge_kernel<12, 48, true, GP_MAX_BRANCHES, true><<<nb, 256, 0, gp_stream(stream)>>>(a);
-  else branch_merge_kernel<12, 48, true><<<nb, 256, 0, gp_stream(stream)>>>(a);
+  // (the v2 kernel's 32-bit offsets run from each slide's own o / lse region: a slide's branch rows
+  // are at most 2 L_i, below 4 GiB for any slide the 1000 x 1000 position grid admits)
+  const unsigned nb = merge_v2_grid(h.T);
+  if (fmt == GP_FMT_F16) branch_merge_v2_kernel<GP_MAX_BRANCHES, true, true><<<nb, 256, 0, gp_stream(stream)>>>(a);
+  else branch_merge_v2_kernel<GP_MAX_BRANCHES, true, false><<<nb, 256, 0, gp_stream(stream)>>>(a);
   return gp_check_launch("gp_branch_merge_ln_varlen");
 }
 

@@ -45,6 +45,7 @@ SIGNATURES = {
                             c_f32, c_i32, c_i32, c_vp],
     "gp_dilated_attn_fwd_ex": [c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i64, c_i64, c_vp, c_i32, c_f32,
                                c_i32, c_i32, c_vp],
+    "gp_attn_launch_params": [c_vp, c_i32],
     "gp_dilated_sparsify": [c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp,
                             c_vp, c_vp],
     "gp_dilated_sparsify_dests": [c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_i32,
@@ -249,6 +250,24 @@ def dilated_attn_fwd_ex(q, q_row_stride, q_tok_base, B, L, H, D, win_lo, win_hi,
     _check(lib.gp_dilated_attn_fwd_ex(_ptr(q), q_row_stride, q_tok_base, B, L, H, D, win_lo, win_hi,
                                       ctypes.cast(arr, c_vp), len(branches), float(softmax_scale),
                                       int(bool(q_log2_prescaled)), fmt, _stream()), "gp_dilated_attn_fwd_ex")
+
+
+def attn_launch_params() -> dict:
+    """The built library's attention launch constants (gp_attn_launch_params): query rows per 8-wave work
+    item, resident 8-wave workgroups per CU, the under-filled threshold (items per CU; 0 = the 4-wave switch
+    is off) and the largest key_parts.  Host only: works without a GPU."""
+    lib = load_library()
+    buf = (c_i32 * 4)()
+    _check(lib.gp_attn_launch_params(ctypes.cast(buf, c_vp), 4), "gp_attn_launch_params")
+    return {"qblk": buf[0], "wg_per_cu": buf[1], "small_per_cu": buf[2], "max_key_parts": buf[3]}
+
+
+def kv_layout_fast(k_ptr: int, v_ptr: int, kv_row_stride: int, ratio: int, D: int = 48) -> bool:
+    """gp_attn.hip's LDS-DMA layout condition for one branch (attn_fwd_impl's kv_desc_ok): v at or after k,
+    a row stride covering v's offset plus one head, 32-bit tile offsets.  Key parts need it."""
+    dv = int(v_ptr) - int(k_ptr)
+    rs2 = 2 * int(kv_row_stride)
+    return dv >= 0 and rs2 >= dv + 2 * D and dv + 64 * int(ratio) * rs2 < 0x7fffffff
 
 
 def dilated_sparsify(src, src_row_stride, k_col, v_col, tok_lo, n_tok, L, H, D, segs, ratios, dsts, dst_bases=None):

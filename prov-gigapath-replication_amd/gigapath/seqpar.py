@@ -116,7 +116,7 @@ def snapped_bounds(bounds: List[Tuple[int, int]], unit: int, L: int) -> Optional
     return [(cuts[w], cuts[w + 1]) for w in range(len(bounds))]
 
 
-def launch_items(geo: BranchGeo, H: int, win_lo: int, win_hi: int, qblk: int = 256) -> int:
+def launch_items(geo: BranchGeo, H: int, win_lo: int, win_hi: int, qblk: Optional[int] = None) -> int:
     """Work items of branch `geo` in a windowed attention launch of 8-wave (256-query) workgroups: segments
     the window meets x heads x query blocks of the fullest (segment, phase) -- gp_attn.hip's item plan."""
     n_lo, n_hi = win_lo // geo.g, (win_hi - 1) // geo.g
@@ -129,28 +129,35 @@ def launch_items(geo: BranchGeo, H: int, win_lo: int, win_hi: int, qblk: int = 2
             most = max(most, hi - lo)
     if n_hi - n_lo > 3:
         most = max(most, geo.m)                       # interior segments are full
+    if qblk is None:
+        qblk = _hip.attn_launch_params()["qblk"]
     return (n_hi - n_lo + 1) * H * max(1, -(-most // qblk))
 
 
-# resident 8-wave attention workgroups per CU (gp_attn.hip GP_ATTN_FAST_WPS: three)
-ATTN_WG_PER_CU = 3
+# A launch whose longest branch has fewer keys per item than this is not split into key parts: its items
+# take microseconds, and the split would only add merge entries (and move the outputs off the single-device
+# path's bits) for nothing (advice r05: the N = 5,000 W = 2 case split its local launch into 4 parts).
+KEY_PARTS_MIN_KEYS = 8192
 
 
 def plan_key_parts(plan: "ShardPlan", rank: int, launches: List[List[int]], n_cu: int = 256) -> List[int]:
     """Key parts per branch for one rank's attention launches (1 = all keys in one entry).
 
-    A launch whose 8-wave work items cannot fill the GPU once (fewer than ATTN_WG_PER_CU x CUs: the long
-    branches' launch of a 256k slide's rank on 8 GPUs holds ~384-480 items of 16,000-23,170 keys for 768
-    slots) splits every branch's keys into P = max(2, round(slots / items)) parts, P lowered until the merge's
-    entries fit GP_MAX_BRANCHES; items of P parts fill the slots with P x shorter items.  Measured at 256k / 8
-    ranks (profiles/r05_kp_*): long-branch attention 5.36 -> 4.90 ms per forward, the merge + 0.10 ms; splitting
-    the mid branch's launch (1,152-1,344 items, 1.5-1.75 slot rounds) instead lost 0.1-0.4 ms."""
+    A launch whose 8-wave work items cannot fill the GPU once (fewer than the library's resident workgroups
+    per CU x CUs, gp_attn_launch_params: the long branches' launch of a 256k slide's rank on 8 GPUs holds
+    ~384-480 items of 16,000-23,170 keys for 768 slots) splits every branch's keys into
+    P = max(2, round(slots / items)) parts, P lowered until the merge's entries fit GP_MAX_BRANCHES; items of
+    P parts fill the slots with P x shorter items.  Launches whose items hold fewer than KEY_PARTS_MIN_KEYS
+    keys stay whole.  Measured at 256k / 8 ranks (profiles/r05_kp_*): long-branch attention 5.36 -> 4.90 ms
+    per forward, the merge + 0.10 ms; splitting the mid branch's launch (1,152-1,344 items, 1.5-1.75 slot
+    rounds) instead lost 0.1-0.4 ms."""
     kp = [1] * len(plan.geo)
     a, e = plan.bounds[rank]
-    slots = ATTN_WG_PER_CU * n_cu
+    lp = _hip.attn_launch_params()
+    slots = lp["wg_per_cu"] * n_cu
     for br in launches:
-        items = sum(launch_items(plan.geo[b], plan.H, a, e) for b in br)
-        if items >= slots:
+        items = sum(launch_items(plan.geo[b], plan.H, a, e, lp["qblk"]) for b in br)
+        if items >= slots or max(plan.geo[b].m for b in br) < KEY_PARTS_MIN_KEYS:
             continue
         P = max(2, int(round(slots / items)))
         while P >= 2 and sum(kp) + len(br) * (P - 1) > _hip.MAX_BRANCHES:
@@ -588,9 +595,22 @@ class SeqParallelEngine:
             return [max(1, int(self.key_parts.get(b, 1))) for b in range(len(self.plan.geo))]
         if pa is not None and not (pa.D == 48 and pa.prescaled and (act == torch.bfloat16 or pa.v_bf16)):
             return [1] * len(self.plan.geo)
+        if not self._kv_layouts_fast():
+            return [1] * len(self.plan.geo)
         n_cu = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count \
             if torch.cuda.is_available() else 256
         return plan_key_parts(self.plan, self.rank, self._launches(), n_cu)
+
+    def _kv_layouts_fast(self) -> bool:
+        """The K / V layouts attention() passes (dense qkv rows: v = k + E, stride 3E; exchanged rows:
+        v = k + C, stride 2C) meet the library's LDS-DMA condition for every branch -- else key parts, which
+        need it, stay off instead of failing inside the forward (advice r05)."""
+        plan = self.plan
+        for b in range(len(plan.geo)):
+            step, stride = (plan.E, 3 * plan.E) if plan.no_xfer[b] else (plan.C[b], 2 * plan.C[b])
+            if not _hip.kv_layout_fast(0, 2 * step, stride, plan.ratios[b], plan.D):
+                return False
+        return True
 
     def _launches(self) -> List[List[int]]:
         plan = self.plan

@@ -149,13 +149,37 @@ def test_key_parts_split_only_underfilled_launches():
             a, e = plan.bounds[r]
             for br in eng._launches():
                 items = sum(seqpar.launch_items(plan.geo[b], 16, a, e) for b in br)
-                assert all(kp[b] == 1 for b in br) == (items >= 3 * 256), (W, r, br, items, kp)
+                under = items < 3 * 256 and max(plan.geo[b].m for b in br) >= seqpar.KEY_PARTS_MIN_KEYS
+                assert all(kp[b] == 1 for b in br) == (not under), (W, r, br, items, kp)
             if W == 8:
                 assert kp == [1, 1, 1, 2, 2], (r, kp)
             if W == 2:
                 assert kp == [1] * 5
     eng.key_parts = {4: 3}
     assert eng.parts() == [1, 1, 1, 1, 3]
+
+
+def test_key_parts_stay_off_for_short_launches():
+    """A small sharded forward (5,000 tiles on 2 ranks, the GPU parity case) has under-filled launches of
+    short items only: no key parts, so the merge keeps its 5-entry specialisation and the shards keep the
+    single-device path's arithmetic (advice r05)."""
+    segs, ratios = [1024, 5792, 32768, 185363, 1048576], [1, 2, 4, 8, 16]
+    plan = seqpar.ShardPlan(5001, 2, segs, ratios, 16, 48, 3072)
+    for r in range(2):
+        assert seqpar.SeqParallelEngine(plan, r, None).parts() == [1] * 5
+
+
+def test_attn_launch_params_match_the_kernel_build():
+    """The planner reads the attention launch constants from the built library (gp_attn_launch_params),
+    not from copies: 256-query 8-wave items, three resident workgroups per CU, the 4-wave switch below three
+    items per CU, at most 64 key parts -- the values the key-part rule and its measurements assume."""
+    from gigapath import _hip
+    assert _hip.attn_launch_params() == {"qblk": 256, "wg_per_cu": 3, "small_per_cu": 3, "max_key_parts": 64}
+    # the LDS-DMA layout condition key parts need (attn_fwd_impl's kv_desc_ok) on the engine's two layouts
+    assert _hip.kv_layout_fast(0, 2 * 768, 3 * 768, 16)          # dense qkv rows
+    assert _hip.kv_layout_fast(0, 2 * 48, 2 * 48, 16)            # exchanged rows, C = 48
+    assert not _hip.kv_layout_fast(2 * 768, 0, 3 * 768, 16)      # v before k
+    assert not _hip.kv_layout_fast(0, 2 * 768, 768, 16)          # stride shorter than v's offset + a head
 
 
 def test_exchange_volume_is_sparse():

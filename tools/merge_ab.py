@@ -63,8 +63,14 @@ def main():
     for p, ts in times.items():
         med = statistics.median(ts)
         ident = torch.equal(outs[p].view(torch.int16), outs[first].view(torch.int16))
-        res.append({"lib": p, "median_ms": round(med, 4), "gbps": round(nbytes / med / 1e6, 1), "identical": ident})
-        print("%-44s median %.4f ms  %7.1f GB/s  identical=%s" % (p, med, nbytes / med / 1e6, ident), flush=True)
+        d = (outs[p].float() - outs[first].float()).abs()
+        ulp = (outs[p].view(torch.int16).int() - outs[first].view(torch.int16).int()).abs()
+        res.append({"lib": p, "median_ms": round(med, 4), "gbps": round(nbytes / med / 1e6, 1), "identical": ident,
+                    "max_abs_diff": float(d.max()), "max_ulp_diff": int(ulp.max()),
+                    "frac_diff": float((ulp > 0).float().mean())})
+        print("%-44s median %.4f ms  %7.1f GB/s  identical=%s  max|d| %.3g  max ulp %d  frac %.2e" % (
+            p, med, nbytes / med / 1e6, ident, float(d.max()), int(ulp.max()), float((ulp > 0).float().mean())),
+            flush=True)
     if args.out:
         json.dump({"L": L, "results": res}, open(args.out, "w"), indent=1)
 
