@@ -218,6 +218,17 @@ class PackedAttention:
     # (DESIGN §3.3).  Every engine producer and consumer of qkv passes it; the standalone module does not.
     v_bf16: bool = False
 
+    def qkv_parts(self, qkv: torch.Tensor):
+        """(q, k, v) column views of a fused [M, 3E] qkv buffer this layer's engine wrote, each with the dtype
+        its bytes hold: with v_bf16 the V third of an fp16 qkv is bf16, so v is viewed as bfloat16 (reading
+        qkv[:, 2E:] as fp16 would silently misread it).  Readers of ws.qkv outside the engine's own entry
+        points go through here (advice r05)."""
+        E = self.E
+        q, k, v = qkv[:, :E], qkv[:, E:2 * E], qkv[:, 2 * E:3 * E]
+        if self.v_bf16 and qkv.dtype == torch.float16:
+            v = v.view(torch.bfloat16)
+        return q, k, v
+
     @staticmethod
     def from_module(m, dev, act: torch.dtype = torch.bfloat16) -> "PackedAttention":
         E, H = m.embed_dim, m.num_heads
@@ -559,6 +570,8 @@ class Workspace:
         self.key = (str(dev), B, L, E, F, H, tuple(segs), tuple(ratios), act)
         self.x = torch.empty(M, E, dtype=torch.float32, device=dev)
         self.a = torch.empty(M, E, dtype=act, device=dev)
+        # fused q | k | v; NOTE under the fp16 caller (PackedAttention.v_bf16) the V third holds bf16 bits
+        # although the tensor is fp16: read it through PackedAttention.qkv_parts
         self.qkv = torch.empty(M, 3 * E, dtype=act, device=dev)
         self.y = torch.empty(M, E, dtype=act, device=dev)
         self.f = torch.empty(M, F, dtype=act, device=dev)
@@ -579,7 +592,7 @@ class PackedWorkspace(Workspace):
         self.key = (str(dev), tuple(self.Ls), E, F, H, tuple(segs), tuple(ratios), act)
         self.x = torch.empty(M, E, dtype=torch.float32, device=dev)
         self.a = torch.empty(M, E, dtype=act, device=dev)
-        self.qkv = torch.empty(M, 3 * E, dtype=act, device=dev)
+        self.qkv = torch.empty(M, 3 * E, dtype=act, device=dev)   # (V third: see Workspace, qkv_parts)
         self.y = torch.empty(M, E, dtype=act, device=dev)
         self.f = torch.empty(M, F, dtype=act, device=dev)
         self.fstats, self.gemm_ws = ffn_buffers(dev, M, E, F)

@@ -251,3 +251,24 @@ def test_graph_outputs_cloned_with_one_copy():
     loose = [torch.randn(2, 768) for _ in range(3)]
     got2 = LongNetViT._clone_outputs(loose)
     assert all(torch.equal(a, b) and a.data_ptr() != b.data_ptr() for a, b in zip(got2, loose))
+
+
+def test_qkv_parts_views_v_in_its_stored_format():
+    """PackedAttention.qkv_parts: under the fp16 caller's V-bf16 packing (ABI 8) the V third of the fp16 qkv
+    buffer holds bf16 bits, and the helper hands it out as a bfloat16 view of the same memory; q / k stay
+    fp16; without the flag (bf16 caller, or fp16 without V-bf16) every third keeps the buffer's dtype."""
+    from gigapath import runtime
+    E = 768
+    pa = runtime.PackedAttention(E=E, H=16, D=48, segs=[1024], ratios=[1], w_qkv=None, b_qkv=None, w_o=None,
+                                 b_o=None, b_o_act=None, ln_w=None, ln_b=None, ln_eps=1e-5, v_bf16=True)
+    qkv = torch.zeros(5, 3 * E, dtype=torch.float16)
+    vals = torch.randn(5, E)
+    qkv[:, 2 * E:].view(torch.bfloat16).copy_(vals.to(torch.bfloat16))     # what the QKV GEMM writes
+    q, k, v = pa.qkv_parts(qkv)
+    assert (q.dtype, k.dtype, v.dtype) == (torch.float16, torch.float16, torch.bfloat16)
+    assert v.data_ptr() == qkv.data_ptr() + 2 * E * 2
+    assert torch.equal(v.float(), vals.to(torch.bfloat16).float())
+    pa.v_bf16 = False
+    assert pa.qkv_parts(qkv)[2].dtype == torch.float16
+    pa.v_bf16 = True
+    assert pa.qkv_parts(qkv.to(torch.bfloat16))[2].dtype == torch.bfloat16
