@@ -1278,16 +1278,22 @@ __global__ __launch_bounds__(256) void branch_merge_kernel(const MergeArgs a) {
 // per token-wave, ~70 of them 64-bit per-lane address arithmetic, and 12 dependent ds_bpermute for the
 // LN sums):
 //  * a lane owns two column chunks: 8 columns (one 16-byte access) and 4 columns (one 8-byte access)
-//    instead of three 8-byte accesses of 12 contiguous columns.  kMap 0: both in head l / 4 (lane k of
-//    a head: columns 8k.. and 32 + 4k.. of the head); kMap 1 ("x8"): [8l, 8l + 8) of head l / 6 and
-//    [512 + 4l, 516 + 4l) of head (128 + l) / 12, so each wave-instruction covers one contiguous span;
+//    instead of three 8-byte accesses of 12 contiguous columns.  kMap 1 ("x8", the default): [8l, 8l + 8)
+//    of head l / 6 and [512 + 4l, 516 + 4l) of head (128 + l) / 12, so each wave-instruction covers one
+//    contiguous span (two heads per lane: twice the softmax VALU, yet measured faster: the kernel is bound
+//    by memory requests, not issue); kMap 0: both chunks in head l / 4 (lane k of a head: columns 8k..
+//    and 32 + 4k.. of the head, one softmax per lane);
 //  * loads address a wave-uniform row base plus a 32-bit lane offset (no per-lane 64-bit math);
 //  * the LN row sums are xor-butterflies (DPP quad_perm / row_half_mirror / row_ror:8, then
 //    v_permlane16/32_swap): the same sum in every lane, no LDS round trips.
 // Per (token, head) the branch weights and the fp32 accumulation are branch_merge_kernel's bit for bit
 // (dilated_attention.py:100-131).
 #ifndef GP_MERGE_MAP
-#define GP_MERGE_MAP 0
+#define GP_MERGE_MAP 1
+#endif
+// waves (tokens) per block of the v2 merge: consecutive tokens of one block share their lse / o lines in L1
+#ifndef GP_MERGE_WPB
+#define GP_MERGE_WPB 4
 #endif
 
 // A 32-bit lane offset the compiler may not re-associate with constants: keeps a uniform-base + lane-offset
@@ -1309,12 +1315,15 @@ GP_DEV float wave_sum_xor(float v) {
 }
 
 template <int NBR, bool kTab, bool kH, int kMap = GP_MERGE_MAP>
-__global__ __launch_bounds__(256) void branch_merge_v2_kernel(const MergeArgs a) {
+__global__ __launch_bounds__(64 * GP_MERGE_WPB) void branch_merge_v2_kernel(const MergeArgs a) {
+  // no implicit contraction: the compiler fused v - s * (1/E) into one fma in some instantiations only, so the
+  // packed (varlen) and single-slide merges differed in the last bit; every fma below is explicit
+#pragma clang fp contract(off)
   constexpr int E = 768, H = 16, D = 48;
   constexpr bool k1h = kMap == 0;          // one head per lane
   const int nbr = NBR < GP_MAX_BRANCHES ? NBR : a.nbranch;
   const int lane = threadIdx.x & 63;
-  const int row = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + (int)(threadIdx.x >> 6));
+  const int row = __builtin_amdgcn_readfirstlane((int)blockIdx.x * GP_MERGE_WPB + (int)(threadIdx.x >> 6));
   const int total = (int)(a.B * a.ntok);
   if (row >= total) return;
   // the lane's chunks: columns c0 .. c0 + 7 (head h0) and c1 .. c1 + 3 (head h1)
@@ -1440,17 +1449,18 @@ __global__ __launch_bounds__(256) void branch_merge_v2_kernel(const MergeArgs a)
 #pragma unroll
     for (int e = 0; e < 12; ++e) s += v[e];
     const float mean = wave_sum_xor(s) * (1.0f / E);
+    // explicit fmas: every instantiation (the varlen one included) rounds the LN identically
     float q = 0.f;
 #pragma unroll
     for (int e = 0; e < 12; ++e) {
       const float d = v[e] - mean;
-      q += d * d;
+      q = __builtin_fmaf(d, d, q);
     }
-    const float rstd = rsqrtf(wave_sum_xor(q) * (1.0f / E) + a.eps);
+    const float rstd = rsqrtf(__builtin_fmaf(wave_sum_xor(q), 1.0f / E, a.eps));
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = (v[e] - mean) * rstd * w0[e] + b0[e];
+    for (int e = 0; e < 8; ++e) v[e] = __builtin_fmaf((v[e] - mean) * rstd, w0[e], b0[e]);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[8 + e] = (v[8 + e] - mean) * rstd * w1[e] + b1[e];
+    for (int e = 0; e < 4; ++e) v[8 + e] = __builtin_fmaf((v[8 + e] - mean) * rstd, w1[e], b1[e]);
   }
   char* orow = reinterpret_cast<char*>(a.out) + (int64_t)row * (E * 2);
   *reinterpret_cast<uint4*>(orow + 2 * c0) =
@@ -1785,7 +1795,7 @@ extern "C" int gp_branch_merge_ln(const uint16_t* const* o_in, const float* cons
 }
 
 // the E = 768 / D = 48 merge: one token per wave, 4 waves per block
-static unsigned merge_v2_grid(int64_t tokens) { return (unsigned)((tokens + 3) / 4); }
+static unsigned merge_v2_grid(int64_t tokens) { return (unsigned)((tokens + GP_MERGE_WPB - 1) / GP_MERGE_WPB); }
 // its 32-bit byte offsets: every branch's o rows (B * nseg * m rows of 1,536 B) below 4 GiB
 static bool merge_v2_fits(const MergeArgs& a) {
   for (int b = 0; b < a.nbranch; ++b)
@@ -1799,10 +1809,10 @@ static void launch_merge(const MergeArgs& a, int E, int D, int nbranch, unsigned
     case 768:
       if (D == 48 && merge_v2_fits(a)) {
         const unsigned g = merge_v2_grid(a.B * a.ntok);
-        if (nbranch == 5) branch_merge_v2_kernel<5, false, kH><<<g, 256, 0, s>>>(a);
+        if (nbranch == 5) branch_merge_v2_kernel<5, false, kH><<<g, 64 * GP_MERGE_WPB, 0, s>>>(a);
         // (5 branches, two of them in two key parts: the sequence-parallel long-branch split, seqpar.plan_key_parts)
-        else if (nbranch == 7) branch_merge_v2_kernel<7, false, kH><<<g, 256, 0, s>>>(a);
-        else branch_merge_v2_kernel<GP_MAX_BRANCHES, false, kH><<<g, 256, 0, s>>>(a);
+        else if (nbranch == 7) branch_merge_v2_kernel<7, false, kH><<<g, 64 * GP_MERGE_WPB, 0, s>>>(a);
+        else branch_merge_v2_kernel<GP_MAX_BRANCHES, false, kH><<<g, 64 * GP_MERGE_WPB, 0, s>>>(a);
       } else if (D == 96) branch_merge_kernel<12, 96, false, GP_MAX_BRANCHES, kH><<<nb, 256, 0, s>>>(a);
       else branch_merge_kernel<12, 12, false, GP_MAX_BRANCHES, kH><<<nb, 256, 0, s>>>(a);
       break;
@@ -2036,8 +2046,8 @@ extern "C" int gp_branch_merge_ln_varlen(const void* plan_host, const void* plan
   // (the v2 kernel's 32-bit offsets run from each slide's own o / lse region: a slide's branch rows
   // are at most 2 L_i, below 4 GiB for any slide the 1000 x 1000 position grid admits)
   const unsigned nb = merge_v2_grid(h.T);
-  if (fmt == GP_FMT_F16) branch_merge_v2_kernel<GP_MAX_BRANCHES, true, true><<<nb, 256, 0, gp_stream(stream)>>>(a);
-  else branch_merge_v2_kernel<GP_MAX_BRANCHES, true, false><<<nb, 256, 0, gp_stream(stream)>>>(a);
+  if (fmt == GP_FMT_F16) branch_merge_v2_kernel<GP_MAX_BRANCHES, true, true><<<nb, 64 * GP_MERGE_WPB, 0, gp_stream(stream)>>>(a);
+  else branch_merge_v2_kernel<GP_MAX_BRANCHES, true, false><<<nb, 64 * GP_MERGE_WPB, 0, gp_stream(stream)>>>(a);
   return gp_check_launch("gp_branch_merge_ln_varlen");
 }
 

@@ -12,11 +12,11 @@ Per layer the engine issues 8 kernels on torch's current HIP stream (M = B*L tok
     x   += LN_ffn(f) . W2^T + b2           gp_ffn_fc2_ln_resid (LN folded; residual + the next layer's
                                            xb = gamma1' (x - s) and statistics in the epilogue)
 
-(plus a split-K reduce after a GEMM whose last round of tiles is split).  The residual stream never
-makes a separate pass: each LayerNorm is folded into the GEMM that consumes it, from the 16-bit
-xb = act(gamma (x - s)) and per-256-column statistics its producer wrote (s = the row mean before the
-add; gp_gemm_impl.h).  Shapes outside the GEMM kernels' instantiations,
-GIGAPATH_RESID_FUSED=0, GIGAPATH_OWN_GEMMS=0 or GIGAPATH_FFN_FUSED=0 run the round-3 sequence instead:
+(plus a split-K reduce after a GEMM whose last round of tiles is split).  That fused form (each LayerNorm
+folded into the GEMM that consumes it, from the 16-bit xb = act(gamma (x - s)) and per-256-column
+statistics its producer wrote; s = the row mean before the add; gp_gemm_impl.h) runs under
+GIGAPATH_RESID_FUSED=1.  The default (round 6, faster: see RESID_FUSED below), and shapes outside the GEMM
+kernels' instantiations, GIGAPATH_OWN_GEMMS=0 or GIGAPATH_FFN_FUSED=0, run the round-3 sequence:
 gp_linear out-proj -> gp_residual_layernorm -> gp_ffn_fc1_gelu -> gp_ffn_fc2_ln -> gp_residual_layernorm
 (hipBLASLt for uncovered GEMMs; for an uncovered FFN hipBLASLt fc1 + gp_gelu_layernorm + hipBLASLt fc2).
 
@@ -319,11 +319,14 @@ class PackedLayer:
 
 
 FFN_FUSED = os.environ.get("GIGAPATH_FFN_FUSED", "1") != "0"
-# the residual adds + pre-LNs inside the out-proj / fc2 epilogues and the QKV / fc1 folds (round 4).
-# A deliberate trade: ~1 % slower in the HIP-graph forward than the round-3 sequence
-# (31.83 vs 31.55 ms, same box) for 2.3x more headroom under the north star's 1e-2 parity bound (C3
-# max-rel 6.94e-3 vs 8.65e-3: the residual stream is rounded once per layer fewer).  =0 picks speed.
-RESID_FUSED = os.environ.get("GIGAPATH_RESID_FUSED", "1") != "0"
+# the residual adds + pre-LNs inside the out-proj / fc2 epilogues and the QKV / fc1 folds (round 4), OFF by
+# default since round 6: the round-3 sequence (plain out-proj / fc2 -> gp_residual_layernorm -> plain QKV / fc1)
+# is faster in the HIP-graph forward on every measurement (r05: 30.96 / 31.08 / 30.92 vs 30.73 / 30.74 /
+# 30.69 ms; r06_base: 29.51 / 29.39 / 29.48 vs 29.38 / 29.27 / 29.06 ms, profiles/r06_base_*) and stays
+# inside the north star's 1e-2 at the headline slides (C3 max-rel 8.57e-3, C4 8.14e-3 vs 7.73e-3 / 6.45e-3
+# fused, profiles/r06_base_golden_rel_resid_fused_on_off.jsonl).  =1 picks the fused epilogues (more
+# parity headroom: the residual stream is rounded once per layer fewer).
+RESID_FUSED = os.environ.get("GIGAPATH_RESID_FUSED", "0") == "1"
 # the QKV / out-proj / patch projections on gp_linear (own MFMA GEMM, the default) instead of hipBLASLt.
 # With every GEMM of the forward on gp_gemm.hip kernels (persistent, data-parallel tiles, no workgroup ever
 # waits on another) concurrent HIP-graph replays on several streams run (tests/test_gpu_concurrent.py,

@@ -155,6 +155,33 @@ def test_c3_70k_end_to_end_vs_reference_golden(model):
         check_vectors("C3 e2e N=70000", name, got, g[name], north_star=True)
 
 
+@pytest.mark.timeout(300)
+def test_resid_fused_path_vs_reference_golden(model, monkeypatch):
+    """GIGAPATH_RESID_FUSED=1 (the residual epilogues and LN folds of DESIGN §3.4b; off by default since
+    round 6, where the round-3 sequence measured faster) still matches the reference: config C2 (16,384
+    tiles) against the reference's own fp32 output, every embedding within the model tolerance."""
+    from gigapath import runtime
+    g = load_golden("e2e_N16384_B1.npz")
+    x, coords = orc.synthetic_slide(16384)
+    xt, ct = torch.from_numpy(x).to(DEV), torch.from_numpy(coords).to(DEV)
+    eng = model.encoder.engine
+
+    def repack():
+        eng._packs.clear()
+        eng._ws.clear()
+
+    monkeypatch.setattr(runtime, "RESID_FUSED", True)
+    repack()
+    try:
+        with torch.no_grad():
+            allv = torch.stack(model(xt, ct, all_layer_embed=True)).cpu().numpy()
+        assert all(pl.resid_fused for pl in next(iter(eng._packs.values()))[1])
+    finally:
+        monkeypatch.setattr(runtime, "RESID_FUSED", False)
+        repack()
+    check_vectors("C2 e2e N=16384 resid-fused", "all_layer", allv, g["all_layer"])
+
+
 def test_fp16_autocast_caller_vs_reference_golden(model, golden_meta):
     """The reference pipeline's call (pipeline.py:186-187): fp16 tile embeddings into
     model(x, coords, all_layer_embed=True) inside torch.cuda.amp.autocast(dtype=torch.float16).

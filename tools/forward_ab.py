@@ -4,8 +4,9 @@ reports the median forward time and the median per-kernel spans (runtime.TIMER) 
 
     python tools/forward_ab.py --libs prod,tools/attn_lab/liblab_x.so [--tiles 70000] [--rounds 5]
 
-A library entry may carry host-path options after a colon: "prod:noresid" runs the product library with
-runtime.RESID_FUSED off (the round-3 out-proj -> residual_layernorm -> FFN -> residual_layernorm sequence);
+A library entry may carry host-path options after a colon: "prod:resid" / "prod:noresid" run the product
+library with runtime.RESID_FUSED on (the residual epilogues) / off (the round-3 out-proj -> residual_layernorm
+-> FFN -> residual_layernorm sequence, the default since round 6);
 "prod:nomerge" with runtime.MERGE_IN_PRODUCER off (the next LN's statistics merged by the consumer's launch),
 repacking the weights for it -- the in-process A/B of the residual epilogues.
 """
@@ -46,12 +47,13 @@ def main():
     times = {p: [] for p, _ in libs}
     spans = {p: {} for p, _ in libs}
     outs = {}
+    default_resid = runtime.RESID_FUSED      # the product default (GIGAPATH_RESID_FUSED; off since round 6)
     with torch.no_grad():
         for rnd in range(args.rounds + 1):
             for p, lib in libs:
                 _hip._lib = lib
                 runtime.MERGE_IN_PRODUCER = ":nomerge" not in p
-                want = ":noresid" not in p
+                want = True if ":resid" in p else (False if ":noresid" in p else default_resid)
                 if runtime.RESID_FUSED != want:        # (re)pack the weights for this host path
                     runtime.RESID_FUSED = want
                     model.encoder.engine._packs.clear()
