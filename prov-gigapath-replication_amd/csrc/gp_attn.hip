@@ -2046,8 +2046,15 @@ extern "C" int gp_branch_merge_ln_varlen(const void* plan_host, const void* plan
   // (the v2 kernel's 32-bit offsets run from each slide's own o / lse region: a slide's branch rows
   // are at most 2 L_i, below 4 GiB for any slide the 1000 x 1000 position grid admits)
   const unsigned nb = merge_v2_grid(h.T);
-  if (fmt == GP_FMT_F16) branch_merge_v2_kernel<GP_MAX_BRANCHES, true, true><<<nb, 64 * GP_MERGE_WPB, 0, gp_stream(stream)>>>(a);
-  else branch_merge_v2_kernel<GP_MAX_BRANCHES, true, false><<<nb, 64 * GP_MERGE_WPB, 0, gp_stream(stream)>>>(a);
+  hipStream_t s = gp_stream(stream);
+  if (h.nbranch == 5) {   // every registered arch's schedule: compile-time branch loops
+    if (fmt == GP_FMT_F16) branch_merge_v2_kernel<5, true, true><<<nb, 64 * GP_MERGE_WPB, 0, s>>>(a);
+    else branch_merge_v2_kernel<5, true, false><<<nb, 64 * GP_MERGE_WPB, 0, s>>>(a);
+  } else if (fmt == GP_FMT_F16) {
+    branch_merge_v2_kernel<GP_MAX_BRANCHES, true, true><<<nb, 64 * GP_MERGE_WPB, 0, s>>>(a);
+  } else {
+    branch_merge_v2_kernel<GP_MAX_BRANCHES, true, false><<<nb, 64 * GP_MERGE_WPB, 0, s>>>(a);
+  }
   return gp_check_launch("gp_branch_merge_ln_varlen");
 }
 
