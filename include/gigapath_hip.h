@@ -247,6 +247,16 @@ int gp_residual_layernorm(float* x, const uint16_t* y, const float* bias, const 
                           const float* ln_b, float eps, uint16_t* ln_out, int64_t rows, int cols,
                           int fmt, void* stream);
 
+/* One encoder layer's two residual adds (encoder.py:141, 159) without the mid-layer store of the fp32
+ * residual stream (round 6).  y2 == NULL: x1 = x + (y1 + b1), ln_out = LayerNorm(x1) (ln_w required),
+ * x left unchanged.  y2 != NULL: x = (x + (y1 + b1)) + (y2 + b2), ln_out = LayerNorm(new x) when ln_w
+ * != NULL.  x1 is rounded exactly as gp_residual_layernorm rounds it, so the pair equals two
+ * gp_residual_layernorm calls bit for bit while moving 22 instead of 24 bytes per element.  y1 / y2:
+ * [rows, cols] act GEMM outputs without bias; b1 / b2: [cols] fp32 or NULL. */
+int gp_residual2_layernorm(float* x, const uint16_t* y1, const float* b1, const uint16_t* y2, const float* b2,
+                           const float* ln_w, const float* ln_b, float eps, uint16_t* ln_out, int64_t rows,
+                           int cols, int fmt, void* stream);
+
 /* FFN middle (feedforward_network.py:131-137): out = LayerNorm(gelu_erf(h)) in fp32.
  * h, out: [rows, cols] act (in place allowed); cols = 64 * {48, 64, 96}.  GELU is rounded to act
  * before the LN (gelu(x.float()).type_as(x), feedforward_network.py:135). */

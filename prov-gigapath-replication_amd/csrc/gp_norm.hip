@@ -141,6 +141,63 @@ __global__ __launch_bounds__(256) void residual_ln_kernel(float* __restrict__ x,
 }
 
 // ---------------------------------------------------------------------------------------
+// The layer's two residual adds without the mid-layer write of the fp32 residual stream (encoder.py:141,159;
+// round 6): the first call computes x1 = x + (y1 + b1) and LN2(x1) but leaves x as it was, the second
+// recomputes x1 the same way (same fp32 operations, so the same bits) from the still-live out-proj output
+// y1, adds (y2 + b2) and writes x2 and LN(x2).  Per element 8 + 14 bytes instead of 12 + 12: the x1 store
+// and reload (8 B) traded for a second read of x and y1 (6 B).
+// 16-bit row loads, non-temporal (the GEMM outputs the residual pair reads are dead after it, and cached they
+// would push the LN output the next GEMM reads out of the MALL)
+typedef uint32_t gp_u2v __attribute__((ext_vector_type(2)));
+template <bool kH, int EPL>
+GP_DEV void ld_x4_e_nt(const uint16_t* row, int lane, float* v) {
+#pragma unroll
+  for (int k = 0; k < EPL / 4; ++k) {
+    const gp_u2v u = __builtin_nontemporal_load(reinterpret_cast<const gp_u2v*>(row + k * 256 + 4 * lane));
+    v[4 * k + 0] = e2f<kH>(u.x);
+    v[4 * k + 1] = e2f_hi<kH>(u.x);
+    v[4 * k + 2] = e2f<kH>(u.y);
+    v[4 * k + 3] = e2f_hi<kH>(u.y);
+  }
+}
+
+template <int EPL, bool kH, bool kY2>
+__global__ __launch_bounds__(256) void residual2_ln_kernel(float* __restrict__ x, const uint16_t* __restrict__ y1,
+                                                           const float* __restrict__ b1, const uint16_t* __restrict__ y2,
+                                                           const float* __restrict__ b2, const float* __restrict__ ln_w,
+                                                           const float* __restrict__ ln_b, float eps,
+                                                           uint16_t* __restrict__ out, int64_t rows, int cols) {
+  const int lane = threadIdx.x & 63;
+  float c1[EPL], c2[EPL], wv[EPL], bv[EPL];
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) c1[i] = c2[i] = 0.f;
+  if (b1 != nullptr) ld_x4_f32<EPL>(b1, lane, c1);
+  if (kY2 && b2 != nullptr) ld_x4_f32<EPL>(b2, lane, c2);
+  if (ln_w != nullptr) {
+    ld_x4_f32<EPL>(ln_w, lane, wv);
+    ld_x4_f32<EPL>(ln_b, lane, bv);
+  }
+  for (int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6); row < rows;
+       row += (int64_t)gridDim.x * kRowsPerBlock) {
+    float v[EPL], yv[EPL];
+    ld_x4_f32_nt<EPL>(x + row * cols, lane, v);
+    ld_x4_e_nt<kH, EPL>(y1 + row * cols, lane, yv);
+#pragma unroll
+    for (int i = 0; i < EPL; ++i) v[i] += yv[i] + c1[i];        // x1, as residual_ln_kernel rounds it
+    if constexpr (kY2) {
+      ld_x4_e_nt<kH, EPL>(y2 + row * cols, lane, yv);
+#pragma unroll
+      for (int i = 0; i < EPL; ++i) v[i] += yv[i] + c2[i];      // x2
+      st_x4_f32_nt<EPL>(x + row * cols, lane, v);
+    }
+    if (ln_w != nullptr) {
+      wave_layernorm_regs<EPL>(v, cols, wv, bv, eps);
+      st_x4_e<kH, EPL>(out + row * cols, lane, v);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // Exact-erf GELU, x * Phi(x) = 0.5 x (1 + erf(x / sqrt 2)) (feedforward_network.py:135, torch's
 // F.gelu default), with erf from Abramowitz & Stegun 7.1.26: |erf error| <= 1.5e-7, i.e. GELU
 // within 0.75e-7 |x| of the libm value -- far below the bf16 rounding of the output, at a
@@ -508,6 +565,31 @@ extern "C" int gp_residual_layernorm(float* x, const uint16_t* y, const float* b
   }
 #undef GP_RESLN
   return gp_check_launch("gp_residual_layernorm");
+}
+
+extern "C" int gp_residual2_layernorm(float* x, const uint16_t* y1, const float* b1, const uint16_t* y2,
+                                      const float* b2, const float* ln_w, const float* ln_b, float eps,
+                                      uint16_t* ln_out, int64_t rows, int cols, int fmt, void* stream) {
+  GP_REQUIRE(fmt == GP_FMT_BF16 || fmt == GP_FMT_F16, "gp_residual2_layernorm: bad fmt %d", fmt);
+  GP_REQUIRE(epl_ok(cols), "gp_residual2_layernorm: cols=%d unsupported (64*{12,16,24})", cols);
+  GP_REQUIRE(rows >= 0, "gp_residual2_layernorm: bad rows");
+  if (rows == 0) return 0;
+  GP_REQUIRE(x && y1, "gp_residual2_layernorm: null pointer");
+  GP_REQUIRE(ln_w == nullptr || (ln_b && ln_out), "gp_residual2_layernorm: LN needs ln_b and ln_out");
+  GP_REQUIRE(y2 != nullptr || ln_w != nullptr, "gp_residual2_layernorm: without y2 the call only writes ln_out");
+  hipStream_t s = gp_stream(stream);
+#define GP_RES2(EPL, KH)                                                                                        \
+  do {                                                                                                          \
+    if (y2) residual2_ln_kernel<EPL, KH, true><<<row_grid(rows), 256, 0, s>>>(x, y1, b1, y2, b2, ln_w, ln_b, eps, ln_out, rows, cols); \
+    else residual2_ln_kernel<EPL, KH, false><<<row_grid(rows), 256, 0, s>>>(x, y1, b1, y2, b2, ln_w, ln_b, eps, ln_out, rows, cols); \
+  } while (0)
+  switch (cols / 64) {
+    case 12: GP_FMT_DISPATCH(fmt, GP_RES2(12, true), GP_RES2(12, false)); break;
+    case 16: GP_FMT_DISPATCH(fmt, GP_RES2(16, true), GP_RES2(16, false)); break;
+    case 24: GP_FMT_DISPATCH(fmt, GP_RES2(24, true), GP_RES2(24, false)); break;
+  }
+#undef GP_RES2
+  return gp_check_launch("gp_residual2_layernorm");
 }
 
 extern "C" int gp_gelu_layernorm(const uint16_t* h, const float* ln_w, const float* ln_b, float eps,

@@ -57,6 +57,7 @@ SIGNATURES = {
     "gp_branch_merge_ln": [c_vp, c_vp, c_vp, c_vp, c_i32, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_f32, c_vp, c_i32,
                            c_vp],
     "gp_residual_layernorm": [c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_vp, c_i64, c_i32, c_i32, c_vp],
+    "gp_residual2_layernorm": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_vp, c_i64, c_i32, c_i32, c_vp],
     "gp_gelu_layernorm": [c_vp, c_vp, c_vp, c_f32, c_vp, c_i64, c_i32, c_i32, c_vp],
     "gp_layernorm_f32": [c_vp, c_i64, c_vp, c_vp, c_f32, c_vp, c_i64, c_i32, c_vp],
     "gp_mean_tokens": [c_vp, c_i64, c_i64, c_i32, c_i64, c_vp, c_vp],
@@ -348,6 +349,20 @@ def residual_layernorm(x, y, bias, ln_w, ln_b, eps, ln_out, rows, cols):
         _dev(ln_out, y.dtype, "ln_out")
     _check(lib.gp_residual_layernorm(_ptr(x), _ptr(y), _ptr(bias), _ptr(ln_w), _ptr(ln_b), eps, _ptr(ln_out),
                                      rows, cols, fmt, _stream()), "gp_residual_layernorm")
+
+
+def residual2_layernorm(x, y1, b1, y2, b2, ln_w, ln_b, eps, ln_out, rows, cols):
+    """gp_residual2_layernorm: y2 None -> ln_out = LN(x + (y1 + b1)), x unchanged; else x = x + (y1 + b1) +
+    (y2 + b2) (two roundings, as two residual_layernorm calls) and ln_out = LN(x)."""
+    lib = load_library()
+    fmt = fmt_of(y1.dtype)
+    _dev(x, torch.float32, "x"); _dev(y1, name="y1")
+    if y2 is not None:
+        _dev(y2, y1.dtype, "y2")
+    if ln_out is not None:
+        _dev(ln_out, y1.dtype, "ln_out")
+    _check(lib.gp_residual2_layernorm(_ptr(x), _ptr(y1), _ptr(b1), _ptr(y2), _ptr(b2), _ptr(ln_w), _ptr(ln_b), eps,
+                                      _ptr(ln_out), rows, cols, fmt, _stream()), "gp_residual2_layernorm")
 
 
 def gelu_layernorm(h, ln_w, ln_b, eps, out, rows, cols):

@@ -577,6 +577,7 @@ class Workspace:
         # although the tensor is fp16: read it through PackedAttention.qkv_parts
         self.qkv = torch.empty(M, 3 * E, dtype=act, device=dev)
         self.y = torch.empty(M, E, dtype=act, device=dev)
+        self.y2 = torch.empty(M, E, dtype=act, device=dev)     # fc2 output (y keeps the out-proj's: RESID2)
         self.f = torch.empty(M, F, dtype=act, device=dev)
         self.fstats, self.gemm_ws = ffn_buffers(dev, M, E, F)
         self.xstats, self.shift = resid_buffers(dev, M, E)
@@ -597,6 +598,7 @@ class PackedWorkspace(Workspace):
         self.a = torch.empty(M, E, dtype=act, device=dev)
         self.qkv = torch.empty(M, 3 * E, dtype=act, device=dev)   # (V third: see Workspace, qkv_parts)
         self.y = torch.empty(M, E, dtype=act, device=dev)
+        self.y2 = torch.empty(M, E, dtype=act, device=dev)
         self.f = torch.empty(M, F, dtype=act, device=dev)
         self.fstats, self.gemm_ws = ffn_buffers(dev, M, E, F)
         self.xstats, self.shift = resid_buffers(dev, M, E)
@@ -719,15 +721,35 @@ class EncoderEngine:
             dilated_attention_core(pa, ws.qkv, B, L, ws.attn, ws.a, v_bf16=pa.v_bf16)
             with TIMER.span("gemm_out"):
                 linear(ws.a, pa.w_o, None, None, ws.y, ws.gemm_ws)
-            with TIMER.span("resid_ln"):
-                _hip.residual_layernorm(ws.x, ws.y, pa.b_o, pl.ln2_w, pl.ln2_b, pl.ln2_eps, ws.a, M, E)
-            b2 = ffn_forward(pl, ws.a, ws.f, ws.y, ws.fstats, ws.gemm_ws, M, F)
             nxt = self.layers[li + 1] if li + 1 < nl else None
-            with TIMER.span("resid_ln"):
-                _hip.residual_layernorm(ws.x, ws.y, b2, nxt.ln1_w if nxt else None, nxt.ln1_b if nxt else None,
-                                        nxt.ln1_eps if nxt else 1e-5, ws.a, M, E)
+            residual_pair(pl, nxt, ws, M, E, F)
             if layer_hook is not None:
                 layer_hook(li + 1)
+
+
+# the layer's two residual adds as gp_residual2_layernorm (round 6): the first leaves x unwritten, the second
+# recomputes x1 from x and the out-proj output y and adds the fc2 output -- 22 instead of 24 bytes per element,
+# bit-identical to the two gp_residual_layernorm passes (=0 restores those)
+RESID2 = os.environ.get("GIGAPATH_RESID2", "1") != "0"
+
+
+def residual_pair(pl: "PackedLayer", nxt: Optional["PackedLayer"], ws, M: int, E: int, F: int):
+    """The unfused layer tail after the out-proj GEMM wrote ws.y: residual + LN2, FFN, residual + the next
+    layer's LN1 (encoder.py:141-162)."""
+    pa = pl.attn
+    ln1 = (nxt.ln1_w, nxt.ln1_b, nxt.ln1_eps) if nxt else (None, None, 1e-5)
+    if RESID2:
+        with TIMER.span("resid_ln"):
+            _hip.residual2_layernorm(ws.x, ws.y, pa.b_o, None, None, pl.ln2_w, pl.ln2_b, pl.ln2_eps, ws.a, M, E)
+        b2 = ffn_forward(pl, ws.a, ws.f, ws.y2, ws.fstats, ws.gemm_ws, M, F)
+        with TIMER.span("resid_ln"):
+            _hip.residual2_layernorm(ws.x, ws.y, pa.b_o, ws.y2, b2, ln1[0], ln1[1], ln1[2], ws.a, M, E)
+        return
+    with TIMER.span("resid_ln"):
+        _hip.residual_layernorm(ws.x, ws.y, pa.b_o, pl.ln2_w, pl.ln2_b, pl.ln2_eps, ws.a, M, E)
+    b2 = ffn_forward(pl, ws.a, ws.f, ws.y, ws.fstats, ws.gemm_ws, M, F)
+    with TIMER.span("resid_ln"):
+        _hip.residual_layernorm(ws.x, ws.y, b2, ln1[0], ln1[1], ln1[2], ws.a, M, E)
 
 
 def gemm_flops(B: int, N: int, E: int, F: int, C: int, depth: int) -> float:

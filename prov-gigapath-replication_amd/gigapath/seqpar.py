@@ -482,6 +482,7 @@ class ShardWorkspace:
         self.qkv_ext = torch.empty(self.hq + self.n, 3 * E, dtype=act, device=dev)
         self.qkv = self.qkv_ext[self.hq:]
         self.y = torch.empty(self.n, E, dtype=act, device=dev)
+        self.y2 = torch.empty(self.n, E, dtype=act, device=dev)     # fc2 output (runtime.residual_pair)
         self.f = torch.empty(self.n, F, dtype=act, device=dev)
         self.fstats, self.gemm_ws = runtime.ffn_buffers(dev, self.n, E, F)
         self.xstats, self.shift = runtime.resid_buffers(dev, self.n, E)
@@ -825,12 +826,7 @@ class SeqParallelEngine:
                     return
                 with runtime.TIMER.span("gemm_out"):
                     runtime.linear(ws.a, pa.w_o, None, None, ws.y, ws.gemm_ws)
-                with runtime.TIMER.span("resid_ln"):
-                    _hip.residual_layernorm(ws.x, ws.y, pa.b_o, pl.ln2_w, pl.ln2_b, pl.ln2_eps, ws.a, M, E)
-                b2 = runtime.ffn_forward(pl, ws.a, ws.f, ws.y, ws.fstats, ws.gemm_ws, M, F)
-                with runtime.TIMER.span("resid_ln"):
-                    _hip.residual_layernorm(ws.x, ws.y, b2, nxt.ln1_w if nxt else None,
-                                            nxt.ln1_b if nxt else None, nxt.ln1_eps if nxt else 1e-5, ws.a, M, E)
+                runtime.residual_pair(pl, nxt, ws, M, E, F)
 
             self._segment(("head", li, wsig), head)
             h_a = self._post(ws, plan.phase_a, True, li, "A")

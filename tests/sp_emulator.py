@@ -68,6 +68,17 @@ def residual_layernorm(x, y, bias, ln_w, ln_b, eps, ln_out, rows, cols):
         ln_out[:rows] = _ln(v, ln_w, ln_b, eps).to(ln_out.dtype)
 
 
+def residual2_layernorm(x, y1, b1, y2, b2, ln_w, ln_b, eps, ln_out, rows, cols):
+    """gp_residual2_layernorm: x1 = x + (y1 + b1) (x unchanged unless y2), x2 = x1 + (y2 + b2) -> x."""
+    assert x.shape[0] >= rows and y1.shape[0] >= rows
+    v = x[:rows] + (y1[:rows].float() + (b1.float() if b1 is not None else 0))
+    if y2 is not None:
+        v = v + (y2[:rows].float() + (b2.float() if b2 is not None else 0))
+        x[:rows] = v
+    if ln_w is not None:
+        ln_out[:rows] = _ln(v, ln_w, ln_b, eps).to(ln_out.dtype)
+
+
 def gelu_layernorm(h, ln_w, ln_b, eps, out, rows, cols):
     v = torch.nn.functional.gelu(h[:rows].float())
     out[:rows] = _ln(v, ln_w, ln_b, eps).to(out.dtype)
@@ -314,7 +325,7 @@ def branch_merge_ln_window(outs, lses, segs, ratios, B, L, tok_lo, n_tok, H, D, 
 def install():
     """Replace the _hip entry points in this process (call in a test subprocess only)."""
     from gigapath import _hip
-    for name in ("coords_to_pos", "posembed_cls_ln", "layernorm_f32", "mean_tokens", "residual_layernorm",
+    for name in ("coords_to_pos", "posembed_cls_ln", "layernorm_f32", "mean_tokens", "residual_layernorm", "residual2_layernorm",
                  "gelu_layernorm", "ffn_fc1_gelu", "ffn_fc2_ln", "linear_resid", "linear_ln", "ffn_fc1_gelu_ln",
                  "ffn_fc2_ln_resid", "dilated_sparsify", "dilated_sparsify_dests", "attn_branch", "dilated_attn_fwd_ex",
                  "branch_merge_ln_window"):

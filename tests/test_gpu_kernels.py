@@ -600,6 +600,43 @@ def test_residual_gelu_layernorm_kernels():
     assert (mt.cpu()[0] - x_ref[1:].mean(0)).abs().max().item() <= 1e-5
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("E", [768, 1024, 1536])
+def test_residual_pair_equals_two_residual_passes(dt, E):
+    """gp_residual2_layernorm (round 6, the default layer tail): the first call writes LN2(x + (y1 + b1)) and
+    leaves x alone, the second writes x2 = (x + (y1 + b1)) + (y2 + b2) and LN(x2) -- bit for bit the two
+    gp_residual_layernorm passes it replaces (x1 rounded the same way), with and without the next LN and
+    biases; rows past `rows` untouched."""
+    h = _hip()
+    rng = np.random.default_rng(E)
+    M, rows = 1001, 997
+    x = torch.from_numpy(rng.standard_normal((M, E)).astype(np.float32)).to(DEV)
+    y1 = torch.from_numpy(rng.standard_normal((M, E)).astype(np.float32)).to(dt).to(DEV)
+    y2 = torch.from_numpy(rng.standard_normal((M, E)).astype(np.float32)).to(dt).to(DEV)
+    b1 = torch.from_numpy(rng.standard_normal(E).astype(np.float32)).to(DEV)
+    b2 = torch.from_numpy(rng.standard_normal(E).astype(np.float32)).to(DEV)
+    w = torch.from_numpy((1 + 0.1 * rng.standard_normal(E)).astype(np.float32)).to(DEV)
+    b = torch.from_numpy((0.1 * rng.standard_normal(E)).astype(np.float32)).to(DEV)
+    for next_ln, bias in ((True, True), (False, True), (True, False)):
+        c1, c2 = (b1, b2) if bias else (None, None)
+        xa, xb = x.clone(), x.clone()
+        la1, la2 = (torch.full((M, E), 7.0, dtype=dt, device=DEV) for _ in range(2))
+        lb1, lb2 = (torch.full((M, E), 7.0, dtype=dt, device=DEV) for _ in range(2))
+        # reference: the two passes (x1 written, then x2)
+        h.residual_layernorm(xa, y1, c1, w, b, 1e-5, la1, rows, E)
+        h.residual_layernorm(xa, y2, c2, w if next_ln else None, b if next_ln else None, 1e-5, la2, rows, E)
+        # the pair
+        h.residual2_layernorm(xb, y1, c1, None, None, w, b, 1e-5, lb1, rows, E)
+        assert torch.equal(xb, x)                                    # the first call leaves x alone
+        h.residual2_layernorm(xb, y1, c1, y2, c2, w if next_ln else None, b if next_ln else None, 1e-5, lb2, rows,
+                              E)
+        torch.cuda.synchronize()
+        assert torch.equal(xa, xb)
+        assert torch.equal(la1.view(torch.int16), lb1.view(torch.int16))
+        assert torch.equal(la2.view(torch.int16), lb2.view(torch.int16))
+        assert torch.equal(xb[rows:], x[rows:]) and (lb1[rows:] == 7.0).all()
+
+
 # ------------------------------------------------------------------ windows + sparsified K/V (sequence parallel)
 WINDOW_CASES = [
     ("default_1025", 1025, [1024, 5792, 32768, 185363, 1048576], [1, 2, 4, 8, 16], [(0, 1), (1, 700), (700, 1025)]),
