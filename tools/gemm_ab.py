@@ -74,6 +74,7 @@ def main():
         ("out_bias", lambda: _hip.linear(a, w_out, bE, y, ws), lambda: y),
         ("out_resid", lambda: _hip.linear_resid(a, w_out, bE, x, s0, gam, xb, xst, ws), lambda: xb),
         ("fc1_bias", lambda: _hip.linear(a, w_fc1, bF, h, ws), lambda: h),
+        ("fc1_gelu", lambda: _hip.ffn_fc1_gelu(a, w_fc1, bF, h, hst), lambda: h),
         ("fc1_gelu_ln", lambda: _hip.ffn_fc1_gelu_ln(a, w_fc1, xst, E // 256, cF, dF, 1e-5, s0, s1, h, hst), lambda: h),
         ("fc2_bias", lambda: _hip.linear(h_in, w_fc2, bE, y, ws), lambda: y),
         ("fc2_ln_resid", lambda: _hip.ffn_fc2_ln_resid(h_in, w_fc2, hst, cE, dE, 1e-5, x, s0, gam, xb, xst, ws),
