@@ -67,16 +67,6 @@ namespace {
 #ifndef GP_GEMM_GELU_EARLY_STORE
 #define GP_GEMM_GELU_EARLY_STORE 1
 #endif
-// GP_GEMM_EPI_INTERLEAVE: the bias (linear) / LN fold (fc2) applied to each m-frag right before its stores
-// instead of to all 8 first
-#ifndef GP_GEMM_EPI_INTERLEAVE
-#define GP_GEMM_EPI_INTERLEAVE 0
-#endif
-// GP_GEMM_GELU_PIPE: the bf16 GELU epilogue issues m-frag mi + 1's table reads before it finishes m-frag mi
-// (their LDS latency under mi's sums, statistics and stores instead of exposed once per m-frag)
-#ifndef GP_GEMM_GELU_PIPE
-#define GP_GEMM_GELU_PIPE 0
-#endif
 constexpr int kBM = 256, kBN = 256, kBK = 64;
 constexpr int kThreads = 512;
 constexpr int kRowB = kBK * 2;                // 128-byte LDS rows
@@ -209,18 +199,6 @@ typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 constexpr int kLutNegB = 8192;
 static_assert(2 * kGeluLutN <= kLutNegB, "");
 __shared__ __attribute__((aligned(16384))) uint16_t g_lut[(kLutNegB + 2 * kGeluLutN) / 2];
-
-// (the two table reads of gelu_lut_pair, left uncombined: GP_GEMM_GELU_PIPE issues an m-frag's reads one
-// m-frag ahead of their use)
-GP_DEV void gelu_lut_reads(uint32_t xp, bool& bad, uint32_t& lo, uint32_t& hi) {
-  const uint32_t m = xp & 0x7fff7fffu;
-  const u16x2 t = __builtin_bit_cast(u16x2, m) - (u16x2)kGeluLutLo;
-  const u16x2 tc = __builtin_elementwise_min(t, (u16x2)(kGeluLutN - 1));
-  bad |= __builtin_bit_cast(uint32_t, tc) != __builtin_bit_cast(uint32_t, t);
-  const uint32_t off = (__builtin_bit_cast(uint32_t, tc) << 1) | ((xp ^ m) >> 2);
-  lo = *reinterpret_cast<const uint16_t*>(reinterpret_cast<const char*>(g_lut) + (off & 0xffff));
-  hi = *reinterpret_cast<const uint16_t*>(reinterpret_cast<const char*>(g_lut) + (off >> 16));
-}
 
 GP_DEV uint32_t gelu_lut_pair(uint32_t xp, bool& bad) {
   const uint32_t m = xp & 0x7fff7fffu;
@@ -495,10 +473,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
         __builtin_amdgcn_sched_barrier(0);
       }
     };
-    // GP_GEMM_EPI_INTERLEAVE: the plain fold / bias epilogues (fc2, the linear GEMMs) apply them per m-frag in
-    // the store loop below instead
-    constexpr bool kIlv = GP_GEMM_EPI_INTERLEAVE != 0 && (EPI == kEpiLnFold || EPI == kEpiLinear);
-    if constexpr (kFold && !kIlv) {   // s * (acc - mu c) + d.  (mean, rstd) and c | d landed during the K loop
+    if constexpr (kFold) {   // s * (acc - mu c) + d.  (mean, rstd) and c | d landed during the K loop
                              // (init_tile's DMA, retired by the issuing waves' first counted waits,
                              // published by the barriers after them)
       float2 rs[8];
@@ -515,7 +490,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
           for (int j = 0; j < 4; ++j) acc[mi][ni][j] = fmaf(rs[mi].y, fmaf(-rs[mi].x, cc[j], acc[mi][ni][j]), dd[j]);
       }
     }
-    if constexpr ((EPI == kEpiLinear && !kIlv) || EPI == kEpiGelu) {   // + bias (landed with the tile's column parameters)
+    if constexpr (EPI == kEpiLinear || EPI == kEpiGelu) {   // + bias (landed with the tile's column parameters)
       if (g.colp0 != nullptr) {
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) {
@@ -611,49 +586,20 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
       // packed 16-bit pairs (64 registers: an m-frag's accumulators die as it is converted).  Per tile
       // and row, M2 = sum h^2 - (sum h)^2 / 256 over 256 bounded activation values: the fp32
       // cancellation is ~1e-7 * (1 + mean^2 / var), far below the act rounding of h itself.
-      // GP_GEMM_GELU_PIPE: packed pre-activations and raw table reads of the current and the next m-frag
-      uint32_t pq[2][4][2], plo[2][4][2], phi[2][4][2];
-      bool pbad[2] = {false, false};
-      auto pipe_issue = [&](int mj, int sl) {
-        pbad[sl] = false;
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni)
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            pq[sl][ni][e] = pack2e<false>(acc[mj][ni][2 * e], acc[mj][ni][2 * e + 1]);
-            gelu_lut_reads(pq[sl][ni][e], pbad[sl], plo[sl][ni][e], phi[sl][ni][e]);
-          }
-      };
-      // (the plain GELU epilogue only: the LN-folded one has no registers to spare)
-      constexpr bool kPipe = !kH && GP_GEMM_GELU_PIPE != 0 && EPI == kEpiGelu;
-      if constexpr (kPipe) pipe_issue(0, 0);
 #pragma unroll
       for (int mi = 0; mi < 8; ++mi) {
         float s = 0.f, s2 = 0.f;
         if constexpr (!kH) {   // bf16: table lookup, sums by v_dot2 (exact bf16 products, fp32 adds)
           uint32_t xp[4][2];
           bool bad = false;
-          if constexpr (kPipe) {
-            const int cur = mi & 1;
-            if (mi + 1 < 8) pipe_issue(mi + 1, cur ^ 1);
 #pragma unroll
-            for (int ni = 0; ni < 4; ++ni)
+          for (int ni = 0; ni < 4; ++ni)
 #pragma unroll
-              for (int e = 0; e < 2; ++e) {
-                xp[ni][e] = pq[cur][ni][e];
-                hp[mi][ni][e] = plo[cur][ni][e] | (phi[cur][ni][e] << 16);
-              }
-            bad = pbad[cur];
-          } else {
-#pragma unroll
-            for (int ni = 0; ni < 4; ++ni)
-#pragma unroll
-              for (int e = 0; e < 2; ++e) {
-                xp[ni][e] = pack2e<false>(acc[mi][ni][2 * e], acc[mi][ni][2 * e + 1]);
-                if constexpr ((GP_LAB_EPI & 8) != 0) hp[mi][ni][e] = xp[ni][e];
-                else hp[mi][ni][e] = gelu_lut_pair(xp[ni][e], bad);
-              }
-          }
+            for (int e = 0; e < 2; ++e) {
+              xp[ni][e] = pack2e<false>(acc[mi][ni][2 * e], acc[mi][ni][2 * e + 1]);
+              if constexpr ((GP_LAB_EPI & 8) != 0) hp[mi][ni][e] = xp[ni][e];
+              else hp[mi][ni][e] = gelu_lut_pair(xp[ni][e], bad);
+            }
           if (__builtin_amdgcn_ballot_w64(bad) != 0) {   // a |x| < 2^-16 or > 5.53 in this m-frag (rare)
 #pragma unroll
             for (int ni = 0; ni < 4; ++ni)
@@ -712,23 +658,6 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const GemmArgs g) {
       if constexpr (kGelu) {
         if constexpr (GP_GEMM_GELU_EARLY_STORE == 0) store_mfrag(mi, hp[mi]);
       } else {
-        if constexpr (kIlv && EPI == kEpiLnFold) {
-          const float2 rs = g_rowst[slot][wm * 128 + mi * 16 + r16];
-#pragma unroll
-          for (int ni = 0; ni < 4; ++ni) {
-            const float4 c = *reinterpret_cast<const float4*>(colt + ni * 16);
-            const float4 d = *reinterpret_cast<const float4*>(colt + kBN + ni * 16);
-            const float cc[4] = {c.x, c.y, c.z, c.w}, dd[4] = {d.x, d.y, d.z, d.w};
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc[mi][ni][j] = fmaf(rs.y, fmaf(-rs.x, cc[j], acc[mi][ni][j]), dd[j]);
-          }
-        }
-        if constexpr (kIlv && EPI == kEpiLinear) {
-          if (g.colp0 != nullptr) {
-#pragma unroll
-            for (int ni = 0; ni < 4; ++ni) acc[mi][ni] += *reinterpret_cast<const f32x4v*>(colt + ni * 16);
-          }
-        }
         uint32_t pk[4][2];
         if (kH && tn * kBN >= g.vcol0) {   // (wave-uniform) the bf16 V columns of an fp16 QKV
 #pragma unroll
