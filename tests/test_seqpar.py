@@ -100,8 +100,9 @@ def test_balanced_bounds_equalise_modelled_cost():
 
 def test_shard_cuts_snap_to_segments_when_the_exchange_pays():
     """C4 on 8 ranks: the cuts land on multiples of 32,768, so the 32,768- and 1,024-token branches
-    exchange nothing and the busiest rank pair carries ~27.5 MB per layer instead of ~49 MB; the
-    chosen plan's modelled compute + busiest-link time is never worse than the cost-balanced cuts'."""
+    exchange nothing and the busiest rank pair carries ~27.5 MB per layer instead of ~49 MB.  The round-6
+    planner (simulated launches, seqpar.LaunchModel) keeps round 5's plan unless its model scores another
+    SP_PLAN_MARGIN better."""
     L = 256001
     plan = seqpar.ShardPlan(L, 8, *DEFAULT, H, D, F)
     assert all(a % 32768 == 0 for a, _ in plan.bounds)
@@ -110,8 +111,28 @@ def test_shard_cuts_snap_to_segments_when_the_exchange_pays():
     bal = seqpar.ShardPlan(L, 8, *DEFAULT, H, D, F,
                            bounds=seqpar.balanced_bounds(seqpar.token_cost(L, *DEFAULT, H, D, F), 8))
     assert plan.max_pair_bytes() < 0.6 * bal.max_pair_bytes()
+    for n, w in [(70001, 8), (100001, 3), (16385, 4), (256001, 2), (256001, 4)]:
+        p = seqpar.ShardPlan(n, w, *DEFAULT, H, D, F)
+        assert not p.cheap_in_a
+        os.environ["GIGAPATH_SP_PLANNER"] = "cost"
+        try:
+            r5 = seqpar.ShardPlan(n, w, *DEFAULT, H, D, F)
+        finally:
+            del os.environ["GIGAPATH_SP_PLANNER"]
+
+        def sim(pl):
+            return max(pl.model_rank(r)["total"] for r in range(w))
+        # round 5's plan, or one the model scores at least SP_PLAN_MARGIN better
+        assert p.bounds == r5.bounds or sim(p) < sim(r5) * (1 - seqpar.SP_PLAN_MARGIN), (n, w)
+
+
+def test_round5_cost_planner_still_available(monkeypatch):
+    """GIGAPATH_SP_PLANNER=cost: round 5's choice -- modelled token cost of the busiest rank + the busiest
+    link's bytes, never worse than the cost-balanced cuts by that measure."""
+    monkeypatch.setenv("GIGAPATH_SP_PLANNER", "cost")
     for n, w in [(70001, 2), (70001, 8), (100001, 3), (16385, 4), (256001, 2)]:
         p = seqpar.ShardPlan(n, w, *DEFAULT, H, D, F)
+        assert not p.cheap_in_a
         cost = seqpar.token_cost(n, *DEFAULT, H, D, F)
         q = seqpar.ShardPlan(n, w, *DEFAULT, H, D, F, bounds=seqpar.balanced_bounds(cost, w))
 
@@ -135,10 +156,11 @@ def test_branches_without_transfers():
     assert not any(bal.no_xfer)
 
 
-def test_key_parts_split_only_underfilled_launches():
-    """seqpar.plan_key_parts: at 256k / 8 ranks the long branches' launch (~384-480 8-wave items for 768 slots)
-    splits both branches' keys in two; the filled launches (and every launch at W = 2) keep whole branches;
-    the merge's entries never exceed GP_MAX_BRANCHES."""
+def test_key_parts_split_only_underfilled_launches(monkeypatch):
+    """GIGAPATH_SP_KEY_PARTS=rule (round 5's item-count rule): at 256k / 8 ranks the long branches' launch
+    (~384-480 8-wave items for 768 slots) splits both branches' keys in two; the filled launches (and every
+    launch at W = 2) keep whole branches; the merge's entries never exceed GP_MAX_BRANCHES."""
+    monkeypatch.setenv("GIGAPATH_SP_KEY_PARTS", "rule")
     segs, ratios = [1024, 5792, 32768, 185363, 1048576], [1, 2, 4, 8, 16]
     for W in (2, 4, 8):
         plan = seqpar.ShardPlan(256001, W, segs, ratios, 16, 48, 3072)
@@ -151,12 +173,43 @@ def test_key_parts_split_only_underfilled_launches():
                 items = sum(seqpar.launch_items(plan.geo[b], 16, a, e) for b in br)
                 under = items < 3 * 256 and max(plan.geo[b].m for b in br) >= seqpar.KEY_PARTS_MIN_KEYS
                 assert all(kp[b] == 1 for b in br) == (not under), (W, r, br, items, kp)
-            if W == 8:
+            if W == 8 and not plan.cheap_in_a:
                 assert kp == [1, 1, 1, 2, 2], (r, kp)
             if W == 2:
                 assert kp == [1] * 5
     eng.key_parts = {4: 3}
     assert eng.parts() == [1, 1, 1, 1, 3]
+
+
+def test_key_parts_chosen_by_simulated_launches():
+    """Round 6: a launch's long branches (>= KEY_PARTS_MIN_KEYS keys per item) split into P parts only when
+    the simulated launch (seqpar.LaunchModel) plus the merge's extra entries beats the whole launch by 2 %,
+    and no other P in 2..4 within the merge's 8 entries would have been chosen instead; short branches stay
+    whole.  At 256k / 8 ranks the 32,768-token ranks split the 185,363-token branch in two (round 5's
+    measured best; (3, 2) was slower, profiles/r05_kp3_*)."""
+    segs, ratios = [1024, 5792, 32768, 185363, 1048576], [1, 2, 4, 8, 16]
+    m = seqpar.LAUNCH_MODEL
+    for L, W in ((256001, 2), (256001, 4), (256001, 8), (70001, 8)):
+        plan = seqpar.ShardPlan(L, W, segs, ratios, 16, 48, 3072)
+        for r in range(W):
+            eng = seqpar.SeqParallelEngine(plan, r, None)
+            kp = eng.parts()
+            assert sum(kp) <= 8
+            a, e = plan.bounds[r]
+            done = [1] * 5
+            for br in eng._launches():
+                long_ = [b for b in br if plan.geo[b].m >= seqpar.KEY_PARTS_MIN_KEYS]
+                assert all(kp[b] == 1 for b in br if b not in long_)
+                assert len({kp[b] for b in long_}) <= 1
+                whole = plan.launch_time(r, br, done)
+                P = kp[long_[0]] if long_ else 1
+                if P > 1:
+                    t = plan.launch_time(r, br, kp) + len(long_) * (P - 1) * (e - a) * m.merge_entry_s
+                    assert t < 0.98 * whole, (L, W, r, br, kp)
+                for b in long_:
+                    done[b] = P
+            if L == 256001 and W == 8 and e - a == 32768 and not plan.cheap_in_a:
+                assert kp[3] == 2, (r, kp)
 
 
 def test_key_parts_stay_off_for_short_launches():

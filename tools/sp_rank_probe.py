@@ -49,6 +49,9 @@ def main():
                     help="comma list of key-part settings: default (the engine's rule), none, or b=P[/b=P...]")
     ap.add_argument("--bounds", default="plan", help="comma list: plan (ShardPlan's choice), balanced (the "
                     "cost-balanced cuts, never snapped to a segment multiple), cuts:c1/c2/... (explicit)")
+    ap.add_argument("--planner", default="sim", help="comma list: sim (round 6: simulated launches, the default), "
+                    "sim1 (the same with the cheap-exchange phase variant), "
+                    "r5 (round 5's token-cost planner and item-count key-part rule)")
     ap.add_argument("--per-branch", action="store_true",
                     help="also time each branch's attention as a launch of its own (valid TFLOP/s per branch)")
     args = ap.parse_args()
@@ -70,9 +73,13 @@ def main():
         if spec == "none":
             return {}
         return {int(x.split("=")[0]): int(x.split("=")[1]) for x in spec.split("/")}
-    for W, nph, lf, kps, bnd in [(int(w), int(p), int(f), k, bd) for w in args.worlds.split(",")
-                                 for p in args.phases.split(",") for f in args.local_first.split(",")
-                                 for k in args.key_parts.split(",") for bd in args.bounds.split(",")]:
+    for W, nph, lf, kps, bnd, pln in [(int(w), int(p), int(f), k, bd, pl) for w in args.worlds.split(",")
+                                      for p in args.phases.split(",") for f in args.local_first.split(",")
+                                      for k in args.key_parts.split(",") for bd in args.bounds.split(",")
+                                      for pl in args.planner.split(",")]:
+        os.environ["GIGAPATH_SP_PLANNER"] = "cost" if pln == "r5" else "sim"
+        os.environ["GIGAPATH_SP_KEY_PARTS"] = "rule" if pln == "r5" else "sim"
+        os.environ["GIGAPATH_SP_CHEAP_IN_A"] = "1" if pln == "sim1" else "0"
         cuts = None
         if bnd == "balanced":
             cuts = seqpar.balanced_bounds(seqpar.token_cost(L, pa.segs, pa.ratios, pa.H, pa.D, F), W)
@@ -154,7 +161,10 @@ def main():
             aA = spans.get("attn_A", 0.0) / nl
             expA = max(0.0, tA - aL)
             expB = max(0.0, tA + tB - max(tA, aL) - aA)
-            ranks.append({"rank": r, "tokens": b - a, "ms": round(best, 3), "key_parts": eng.parts(),
+            mod = plan.model_rank(r, eng.parts(), bool(lf))
+            ranks.append({"rank": r, "tokens": b - a, "bounds": [a, b], "ms": round(best, 3), "key_parts": eng.parts(),
+                          "model_ms": {k: round(v * nl * 1e3, 3) for k, v in mod.items()},
+                          "phases": [plan.phase_a, plan.phase_b1, plan.phase_b2],
                           "recv_MB_per_layer": round(plan.exchange_bytes(r) / 1e6, 1), "spans_ms": spans,
                           "per_branch_attention": per_branch,
                           "link_ms_per_layer": {"A": round(tA, 3), "B": round(tB, 3)},
@@ -163,7 +173,8 @@ def main():
             del eng, ws
             torch.cuda.empty_cache()
         key = str(W) + ("" if nph == 2 else "/phases%d" % nph) + ("/local-first" if lf else "") + \
-            ("" if kps == "default" else "/kp:" + kps) + ("" if bnd == "plan" else "/bounds:" + bnd)
+            ("" if kps == "default" else "/kp:" + kps) + ("" if bnd == "plan" else "/bounds:" + bnd) + \
+            ("" if pln == "sim" else "/planner:" + pln)
         out["worlds"][key] = {"max_ms": max(x["ms"] for x in ranks), "ranks": ranks,
                               "max_ms_plus_exposed": max(x["ms_plus_exposed"] for x in ranks),
                               "link_bytes_per_s": seqpar.LINK_BYTES_PER_S}
