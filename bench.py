@@ -404,7 +404,7 @@ def main():
         "attn_mfma_util_pct": round(100 * achieved / PEAK_BF16_TFLOPS, 2),
         "merge_roofline": {"bound": "hbm", "kernel": "gp_branch_merge_ln", "achieved": round(merge_gbs, 1),
                            "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(merge_gbs / PEAK_HBM_GBS, 4),
-                           "traffic": pmc_traffic(args.tiles, "branch_merge_v2_kernel<5") if plain else None,
+                           "traffic": pmc_traffic(args.tiles, "branch_merge_v3_kernel<5") if plain else None,
                            "bytes_per_launch": merge_bytes},
         "model_tflops": round(total_tf * args.steps * (1 if (sp or mixed) else world) / elapsed, 2),
         "kernel_ms_per_step": {k: round(v[1] / args.timing_steps, 3) for k, v in sorted(kt.items())},

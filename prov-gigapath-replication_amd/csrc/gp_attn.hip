@@ -1468,6 +1468,170 @@ __global__ __launch_bounds__(64 * GP_MERGE_WPB) void branch_merge_v2_kernel(cons
   *reinterpret_cast<uint2*>(orow + 2 * c1) = make_uint2(pack2e<kH>(v[8], v[9]), pack2e<kH>(v[10], v[11]));
 }
 
+// GP_MERGE_V3 (round 6, product 1): the v2 merge with the LSEs staged per block of up to kV3Tok consecutive tokens.  The
+// [B * nseg, H, m] lse layout puts one token's covered heads in 16 / r different cache lines, and the v2 kernel's
+// one-token waves fetch them token by token (~16 of its ~42 L2 read requests per token, at the per-CU cap of
+// outstanding requests, §3.5).  Here the block's four waves first load every lse its 64 tokens need -- lane t =
+// token t, so one wave-instruction reads up to 64 consecutive rows of a head -- into LDS, then each wave merges
+// a quarter of the tokens (t = wave + 4k) exactly as branch_merge_v2_kernel does, reading the weights' LSEs from
+// LDS.  Same arithmetic per token, so the same bits (the varlen merge keeps the v2 kernel).  Same-process A/B
+// (profiles/r06_mv3e_merge_ab_*): 70k 73.5 vs 84.2 us, 256k 238 vs 284 us per launch, bit-identical; up to 64
+// tokens per block 82.5 / 246 us, 16: 82.0 / 272 us.
+#ifndef GP_MERGE_V3
+#define GP_MERGE_V3 1
+#endif
+#ifndef GP_MERGE_V3_TOK
+#define GP_MERGE_V3_TOK 32
+#endif
+constexpr int kV3Tok = GP_MERGE_V3_TOK;    // most tokens per block (4 waves, up to kV3Tok / 4 tokens each); <= 64
+
+template <int NBR, bool kH>
+__global__ __launch_bounds__(256) void branch_merge_v3_kernel(const MergeArgs a, const int tpb) {
+#pragma clang fp contract(off)
+  constexpr int E = 768, H = 16, D = 48;
+  constexpr int LS = NBR * 16 + 1;           // LDS floats per token (16 per branch entry; +1: bank spread)
+  __shared__ float lse_s[kV3Tok * LS];
+  const int nbr = NBR < GP_MAX_BRANCHES ? NBR : a.nbranch;
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const int total = (int)(a.B * a.ntok);
+  const int row0 = (int)blockIdx.x * tpb;    // tpb <= kV3Tok tokens of this block (the launch balances them)
+  // ---- stage: lane t loads, for token row0 + t, the covered heads' lse of every branch (wave w: heads h' = w mod 4)
+  if (lane < tpb) {
+    const int tl = lane;
+    const int row = row0 + tl;
+    const bool live = row < total;
+    const int rr = live ? row : total - 1;
+    const int bidx = (int)div_magic((uint32_t)rr, a.dnt);
+    const int p = (int)a.tok_lo + (rr - bidx * (int)a.ntok);
+#pragma unroll
+    for (int b = 0; b < NBR; ++b) {
+      if (b < nbr) {
+        const MergeBranch& mb = a.br[b];
+        const int pn = (int)div_magic((uint32_t)p, mb.dg);
+        const int pt = p - pn * mb.g.g;
+        const int pi = (int)div_magic((uint32_t)pt, mb.dr);
+        const int pj = pt - pi * mb.g.r;
+        const int hpg = mb.g.hpg;
+        const uint32_t rb = (uint32_t)(bidx * mb.g.nseg + pn);
+        const float* lrow = mb.lse + (size_t)rb * (uint32_t)(H * mb.g.m) + (uint32_t)pi;
+        for (int hq = wv; hq < hpg; hq += 4) {
+          const float v = lrow[(size_t)(uint32_t)(pj * hpg + hq) * (uint32_t)mb.g.m];
+          lse_s[tl * LS + b * 16 + hq] = v;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // ---- merge: wave wv takes tokens wv, wv + 4, ..., as branch_merge_v2_kernel (kMap 1, "x8") does one token
+  const int kq = lane & 3;
+  (void)kq;
+  const int h0 = lane / 6, h1 = (128 + lane) / 12;
+  const int c0 = 8 * lane, c1 = 512 + 4 * lane;
+  const bool ln = a.ln_w != nullptr;
+  const float* lw = ln ? a.ln_w : reinterpret_cast<const float*>(a.out);
+  const float* lb = ln ? a.ln_b : reinterpret_cast<const float*>(a.out);
+  float w0[8], w1[4], b0[8], b1[4];
+  load_f32<8>(lw + c0, w0);
+  load_f32<4>(lw + c1, w1);
+  load_f32<8>(lb + c0, b0);
+  load_f32<4>(lb + c1, b1);
+  for (int k = 0; k < kV3Tok / 4; ++k) {
+    const int t = wv + 4 * k;
+    const int row = row0 + t;
+    if (t >= tpb || row >= total) break;
+    const int bidx = (int)div_magic((uint32_t)row, a.dnt);
+    const int p = (int)a.tok_lo + (row - bidx * (int)a.ntok);
+    uint4 o0[NBR];
+    uint2 o1[NBR];
+    float l0[NBR], l1[NBR];
+    bool cv0[NBR], cv1[NBR];
+#pragma unroll
+    for (int b = 0; b < NBR; ++b) {
+      cv0[b] = cv1[b] = false;
+      l0[b] = l1[b] = -1e8f;
+      o0[b] = make_uint4(0, 0, 0, 0);
+      o1[b] = make_uint2(0, 0);
+      if (b < nbr) {
+        const MergeBranch& mb = a.br[b];
+        const int pn = (int)div_magic((uint32_t)p, mb.dg);
+        const int pt = p - pn * mb.g.g;
+        const int pi = (int)div_magic((uint32_t)pt, mb.dr);
+        const int pj = pt - pi * mb.g.r;
+        const int hpg = mb.g.hpg;
+        const int hf = pj * hpg;
+        const uint32_t rb = (uint32_t)(bidx * mb.g.nseg + pn);
+        const char* orow = reinterpret_cast<const char*>(mb.o) + (rb * (uint32_t)mb.g.m + (uint32_t)pi) * (uint32_t)(E * 2);
+        cv0[b] = (unsigned)(h0 - hf) < (unsigned)hpg;
+        cv1[b] = (unsigned)(h1 - hf) < (unsigned)hpg;
+        l0[b] = lse_s[t * LS + b * 16 + (cv0[b] ? h0 - hf : 0)];
+        l1[b] = lse_s[t * LS + b * 16 + (cv1[b] ? h1 - hf : 0)];
+        o0[b] = *reinterpret_cast<const uint4*>(orow + opaque_u32(cv0[b] ? 2 * c0 : 2 * D * hf));
+        o1[b] = *reinterpret_cast<const uint2*>(orow + opaque_u32(cv1[b] ? 2 * c1 : 2 * D * hf));
+      }
+    }
+    float mx0 = -INFINITY, mx1 = -INFINITY;
+#pragma unroll
+    for (int b = 0; b < NBR; ++b)
+      if (b < nbr) {
+        if (!cv0[b] || l0[b] == 0.f) l0[b] = -1e8f;   // dilated_attention.py:46
+        mx0 = fmaxf(mx0, l0[b]);
+        if (!cv1[b] || l1[b] == 0.f) l1[b] = -1e8f;
+        mx1 = fmaxf(mx1, l1[b]);
+      }
+    float ws0 = 0.f, ws1 = 0.f;
+#pragma unroll
+    for (int b = 0; b < NBR; ++b)
+      if (b < nbr) {
+        l0[b] = fast_exp2((l0[b] - mx0) * 1.44269504088896340736f);
+        ws0 += l0[b];
+        l1[b] = fast_exp2((l1[b] - mx1) * 1.44269504088896340736f);
+        ws1 += l1[b];
+      }
+    const float inv0 = __builtin_amdgcn_rcpf(ws0), inv1 = __builtin_amdgcn_rcpf(ws1);
+    float v[12];
+#pragma unroll
+    for (int e = 0; e < 12; ++e) v[e] = 0.f;
+#pragma unroll
+    for (int b = 0; b < NBR; ++b)
+      if (b < nbr) {
+        const float wb0 = cv0[b] ? l0[b] * inv0 : 0.f;
+        const float wb1 = cv1[b] ? l1[b] * inv1 : 0.f;
+        const uint32_t u0[4] = {o0[b].x, o0[b].y, o0[b].z, o0[b].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          v[2 * q] = __builtin_fmaf(e2f<kH>(u0[q]), wb0, v[2 * q]);
+          v[2 * q + 1] = __builtin_fmaf(e2f_hi<kH>(u0[q]), wb0, v[2 * q + 1]);
+        }
+        v[8] = __builtin_fmaf(e2f<kH>(o1[b].x), wb1, v[8]);
+        v[9] = __builtin_fmaf(e2f_hi<kH>(o1[b].x), wb1, v[9]);
+        v[10] = __builtin_fmaf(e2f<kH>(o1[b].y), wb1, v[10]);
+        v[11] = __builtin_fmaf(e2f_hi<kH>(o1[b].y), wb1, v[11]);
+      }
+    if (ln) {
+      float s = 0.f;
+#pragma unroll
+      for (int e = 0; e < 12; ++e) s += v[e];
+      const float mean = wave_sum_xor(s) * (1.0f / E);
+      float q = 0.f;
+#pragma unroll
+      for (int e = 0; e < 12; ++e) {
+        const float d = v[e] - mean;
+        q = __builtin_fmaf(d, d, q);
+      }
+      const float rstd = rsqrtf(__builtin_fmaf(wave_sum_xor(q), 1.0f / E, a.eps));
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = __builtin_fmaf((v[e] - mean) * rstd, w0[e], b0[e]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[8 + e] = __builtin_fmaf((v[8 + e] - mean) * rstd, w1[e], b1[e]);
+    }
+    char* orow = reinterpret_cast<char*>(a.out) + (int64_t)row * (E * 2);
+    *reinterpret_cast<uint4*>(orow + 2 * c0) =
+        make_uint4(pack2e<kH>(v[0], v[1]), pack2e<kH>(v[2], v[3]), pack2e<kH>(v[4], v[5]), pack2e<kH>(v[6], v[7]));
+    *reinterpret_cast<uint2*>(orow + 2 * c1) = make_uint2(pack2e<kH>(v[8], v[9]), pack2e<kH>(v[10], v[11]));
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void dilated_gather_kernel(const uint16_t* __restrict__ src, int64_t row_stride,
                                                              int64_t col_off, int64_t L, int H, int D, GpBranch g,
@@ -1807,7 +1971,18 @@ template <bool kH>
 static void launch_merge(const MergeArgs& a, int E, int D, int nbranch, unsigned nb, hipStream_t s) {
   switch (E) {
     case 768:
-      if (D == 48 && merge_v2_fits(a)) {
+      // (5 entries only: the 7 / 8-entry instantiations need 134-145 VGPRs and spill SGPRs; they keep the v2 kernel)
+      if (GP_MERGE_V3 != 0 && D == 48 && nbranch == 5 && merge_v2_fits(a)) {
+        // tokens per block: the blocks spread evenly over the CUs -- the kernel is bound per CU (outstanding L2
+        // requests), so a CU holding one block more than another finishes a block's time later (70k: 9 blocks of
+        // 31 tokens per CU; 256k: 32 blocks of 32)
+        const int64_t T = a.B * a.ntok;
+        const int64_t ncu = attn_num_cus(s);
+        const int64_t per_cu = (T + ncu * kV3Tok - 1) / (ncu * kV3Tok);
+        const int tpb = (int)std::max<int64_t>(1, (T + ncu * per_cu - 1) / (ncu * per_cu));
+        const unsigned g = (unsigned)((T + tpb - 1) / tpb);
+        branch_merge_v3_kernel<5, kH><<<g, 256, 0, s>>>(a, tpb);
+      } else if (D == 48 && merge_v2_fits(a)) {
         const unsigned g = merge_v2_grid(a.B * a.ntok);
         if (nbranch == 5) branch_merge_v2_kernel<5, false, kH><<<g, 64 * GP_MERGE_WPB, 0, s>>>(a);
         // (5 branches, two of them in two key parts: the sequence-parallel long-branch split, seqpar.plan_key_parts)
