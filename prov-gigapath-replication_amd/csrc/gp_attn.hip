@@ -773,30 +773,30 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
       // the fast kernel (GP_ATTN_FAST_WPS): one 32-key sub-tile at a time -- S, exps and P.V of sub-tile u before
       // sub-tile u + 1's S -- so the body fits 80 VGPRs and three workgroups share each CU
       if (wact) {
-  #pragma unroll
+#pragma unroll
         for (int u = 0; u < 2; ++u) {
           f32x16 acc;
-  #pragma unroll
+#pragma unroll
           for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  #pragma unroll
+#pragma unroll
           for (int ks = 0; ks < KS; ++ks) {
             const bf16x8 kk = *reinterpret_cast<const bf16x8*>(Kb + (32 * u + l32) * KROWB + 32 * ks + 16 * h);
             acc = mfma_32x32x16<kH>(kk, qf[ks], acc);
           }
           if (kv0 + 64 > c) {
-  #pragma unroll
+#pragma unroll
             for (int r = 0; r < 16; ++r)
               if (kv0 + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * h >= c) acc[r] = -INFINITY;
           }
           bf16x8 pu[2];
-  #pragma unroll
+#pragma unroll
           for (int s = 0; s < 2; ++s)
-  #pragma unroll
+#pragma unroll
             for (int e = 0; e < 8; ++e) pu[s][e] = f2e_slot<kVH>(fast_exp2(acc[8 * s + e]));
-  #pragma unroll
+#pragma unroll
           for (int s = 0; s < 2; ++s) {
             const int row = 32 * u + 16 * s + 4 * (lane >> 5) + ((lane >> 2) & 3);
-  #pragma unroll
+#pragma unroll
             for (int mt = 0; mt < 2; ++mt) {
               const int blk = 2 * mt + ((lane >> 4) & 1);
               const char* p0 = Vb + row * VROWB + 32 * (blk ^ (row & 3)) + 8 * (lane & 3);
@@ -816,21 +816,21 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
       f32x16 ini;
       if constexpr (kMI) {
         f32x16 zero;
-  #pragma unroll
+#pragma unroll
         for (int r = 0; r < 16; ++r) zero[r] = 0.f;
         ini = __builtin_amdgcn_mfma_f32_32x32x16_bf16(onesA, mqB, zero, 0, 0, 0);
       }
       const float init = (kPre && !kZM && !kMI && t > t_lo) ? -m_run : 0.f;
-  #pragma unroll
+#pragma unroll
       for (int u = 0; u < 2; ++u) {
         f32x16 acc;
         if constexpr (kMI) {
           acc = ini;
         } else {
-  #pragma unroll
+#pragma unroll
           for (int r = 0; r < 16; ++r) acc[r] = init;
         }
-  #pragma unroll
+#pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
           const bf16x8 kk = *reinterpret_cast<const bf16x8*>(Kb + (32 * u + l32) * KROWB + 32 * ks + 16 * h);
           acc = mfma_32x32x16<kH>(kk, qf[ks], acc);
@@ -838,9 +838,9 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
         sacc[u] = acc;
       }
       if (kv0 + 64 > c) {      // keys >= c are zero pads (added analytically at the end)
-  #pragma unroll
+#pragma unroll
         for (int u = 0; u < 2; ++u)
-  #pragma unroll
+#pragma unroll
           for (int r = 0; r < 16; ++r)
             if (kv0 + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * h >= c) sacc[u][r] = -INFINITY;
       }
@@ -849,7 +849,7 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
       float mx = 0.f;
       if (!kZM) {
         float mxa = sacc[0][0], mxb = sacc[1][0];
-  #pragma unroll
+#pragma unroll
         for (int r = 1; r < 16; ++r) {
           mxa = fmaxf(mxa, sacc[0][r]);
           mxb = fmaxf(mxb, sacc[1][r]);
@@ -879,16 +879,16 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
               const float d = m_new - m_old;
               if (t > t_lo) {
                 const float alpha = fast_exp2(-d);
-  #pragma unroll
+#pragma unroll
                 for (int mt = 0; mt < 2; ++mt)
-  #pragma unroll
+#pragma unroll
                   for (int r = 0; r < 16; ++r) oacc[mt][r] *= alpha;
                 lsum *= alpha;
               }
               m_run = m_new;
-  #pragma unroll
+#pragma unroll
               for (int u = 0; u < 2; ++u)
-  #pragma unroll
+#pragma unroll
                 for (int r = 0; r < 16; ++r) sacc[u][r] -= d;
               if (h == 0) {
                 const __bf16 hi = (__bf16)(-m_run);
@@ -899,25 +899,25 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
               const float delta = need ? mx : 0.f;
               const float alpha = fast_exp2(-delta);
               if (t > t_lo) {
-  #pragma unroll
+#pragma unroll
                 for (int mt = 0; mt < 2; ++mt)
-  #pragma unroll
+#pragma unroll
                   for (int r = 0; r < 16; ++r) oacc[mt][r] *= alpha;
                 lsum *= alpha;
               }
               m_run = (t == t_lo) ? delta : m_run + delta;
-  #pragma unroll
+#pragma unroll
               for (int u = 0; u < 2; ++u)
-  #pragma unroll
+#pragma unroll
                 for (int r = 0; r < 16; ++r) sacc[u][r] -= delta;
             }
           }
         }
-  #pragma unroll
+#pragma unroll
         for (int u = 0; u < 2; ++u)
-  #pragma unroll
+#pragma unroll
           for (int s = 0; s < 2; ++s)
-  #pragma unroll
+#pragma unroll
             for (int e = 0; e < 8; ++e) {
               const float p = fast_exp2(sacc[u][8 * s + e]);
               if constexpr (!kOnes) lsum += p;
@@ -929,18 +929,18 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
         if (__builtin_amdgcn_ballot_w64(need)) {
           const float m_new = need ? tm : m_run;
           const float alpha = fast_exp2(m_run - m_new);
-  #pragma unroll
+#pragma unroll
           for (int mt = 0; mt < 2; ++mt)
-  #pragma unroll
+#pragma unroll
             for (int r = 0; r < 16; ++r) oacc[mt][r] *= alpha;
           lsum *= alpha;
           m_run = m_new;
         }
-  #pragma unroll
+#pragma unroll
         for (int u = 0; u < 2; ++u)
-  #pragma unroll
+#pragma unroll
           for (int s = 0; s < 2; ++s)
-  #pragma unroll
+#pragma unroll
             for (int e = 0; e < 8; ++e) {
               const float p = fast_exp2(fmaf(sacc[u][8 * s + e], a.c_log2, -m_run));
               if constexpr (!kOnes) lsum += p;
@@ -949,12 +949,12 @@ __device__ __forceinline__ void attn32_item(const AttnArgs& a, const int item_id
       }
 
       // ---- O^T += V^T . P^T  (2 sub-tiles x 2 k-steps x 2 d-tiles)
-  #pragma unroll
+#pragma unroll
       for (int u = 0; u < 2; ++u)
-  #pragma unroll
+#pragma unroll
         for (int s = 0; s < 2; ++s) {
           const int row = 32 * u + 16 * s + 4 * (lane >> 5) + ((lane >> 2) & 3);
-  #pragma unroll
+#pragma unroll
           for (int mt = 0; mt < 2; ++mt) {
             const int blk = 2 * mt + ((lane >> 4) & 1);
             const char* p0 = Vb + row * VROWB + 32 * (blk ^ (row & 3)) + 8 * (lane & 3);
@@ -1474,18 +1474,42 @@ __global__ __launch_bounds__(64 * GP_MERGE_WPB) void branch_merge_v2_kernel(cons
 // outstanding requests, §3.5).  Here the block's four waves first load every lse its 64 tokens need -- lane t =
 // token t, so one wave-instruction reads up to 64 consecutive rows of a head -- into LDS, then each wave merges
 // a quarter of the tokens (t = wave + 4k) exactly as branch_merge_v2_kernel does, reading the weights' LSEs from
-// LDS.  Same arithmetic per token, so the same bits (the varlen merge keeps the v2 kernel).  Same-process A/B
+// LDS.  Same arithmetic per token, so the same bits (the varlen merge too, GP_MERGE_V3_TAB).  Same-process A/B
 // (profiles/r06_mv3e_merge_ab_*): 70k 73.5 vs 84.2 us, 256k 238 vs 284 us per launch, bit-identical; up to 64
 // tokens per block 82.5 / 246 us, 16: 82.0 / 272 us.
 #ifndef GP_MERGE_V3
 #define GP_MERGE_V3 1
+#endif
+// GP_MERGE_V3_TAB (product 1): the packed-slide (varlen) merge on the v3 kernel too, when every slide holds at least a
+// block's tokens: C5 batch (675,619 tokens) 0.625 vs 0.868 ms per launch, bit-identical (profiles/r06_mv3tab2_*)
+#ifndef GP_MERGE_V3_TAB
+#define GP_MERGE_V3_TAB 1
 #endif
 #ifndef GP_MERGE_V3_TOK
 #define GP_MERGE_V3_TOK 32
 #endif
 constexpr int kV3Tok = GP_MERGE_V3_TOK;    // most tokens per block (4 waves, up to kV3Tok / 4 tokens each); <= 64
 
-template <int NBR, bool kH>
+// A MergeBranch table entry by scalar loads (uniform index, constant address space): the entries then live in
+// SGPRs even when the load follows the kernel's global stores (the compiler's uniform-load analysis would
+// otherwise fall back to per-lane loads into VGPRs)
+GP_DEV MergeBranch merge_entry_scalar(const MergeBranch* tab, int idx) {
+  MergeBranch e;
+#if defined(__HIP_DEVICE_COMPILE__)
+  static_assert(sizeof(MergeBranch) % 4 == 0, "");
+  uint32_t words[sizeof(MergeBranch) / 4];
+  const __attribute__((address_space(4))) uint32_t* src =
+      (const __attribute__((address_space(4))) uint32_t*)(uintptr_t)(tab + __builtin_amdgcn_readfirstlane(idx));
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(MergeBranch) / 4); ++i) words[i] = src[i];
+  __builtin_memcpy(&e, words, sizeof(MergeBranch));
+#else
+  e = tab[idx];
+#endif
+  return e;
+}
+
+template <int NBR, bool kH, bool kTab = false>
 __global__ __launch_bounds__(256) void branch_merge_v3_kernel(const MergeArgs a, const int tpb) {
 #pragma clang fp contract(off)
   constexpr int E = 768, H = 16, D = 48;
@@ -1496,28 +1520,84 @@ __global__ __launch_bounds__(256) void branch_merge_v3_kernel(const MergeArgs a,
   const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const int total = (int)(a.B * a.ntok);
   const int row0 = (int)blockIdx.x * tpb;    // tpb <= kV3Tok tokens of this block (the launch balances them)
+  // kTab (packed slides): the slide of the block's first token (wave-uniform binary search); a block of at most
+  // kV3Tok tokens meets at most two slides (every slide holds more tokens than that, checked by the launch)
+  int slide0 = 0;
+  if constexpr (kTab) {
+    int lo = 0, hi = a.nslide - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if ((int64_t)row0 >= a.tok_off[mid]) lo = mid; else hi = mid - 1;
+    }
+    slide0 = __builtin_amdgcn_readfirstlane(lo);
+  }
   // ---- stage: lane t loads, for token row0 + t, the covered heads' lse of every branch (wave w: heads h' = w mod 4)
-  if (lane < tpb) {
-    const int tl = lane;
-    const int row = row0 + tl;
-    const bool live = row < total;
-    const int rr = live ? row : total - 1;
-    const int bidx = (int)div_magic((uint32_t)rr, a.dnt);
-    const int p = (int)a.tok_lo + (rr - bidx * (int)a.ntok);
+  if constexpr (!kTab) {
+    if (lane < tpb) {
+      const int tl = lane;
+      const int row = row0 + tl;
+      const bool live = row < total;
+      const int rr = live ? row : total - 1;
+      const int bidx = (int)div_magic((uint32_t)rr, a.dnt);
+      const int p = (int)a.tok_lo + (rr - bidx * (int)a.ntok);
 #pragma unroll
-    for (int b = 0; b < NBR; ++b) {
-      if (b < nbr) {
-        const MergeBranch& mb = a.br[b];
-        const int pn = (int)div_magic((uint32_t)p, mb.dg);
-        const int pt = p - pn * mb.g.g;
-        const int pi = (int)div_magic((uint32_t)pt, mb.dr);
-        const int pj = pt - pi * mb.g.r;
-        const int hpg = mb.g.hpg;
-        const uint32_t rb = (uint32_t)(bidx * mb.g.nseg + pn);
-        const float* lrow = mb.lse + (size_t)rb * (uint32_t)(H * mb.g.m) + (uint32_t)pi;
-        for (int hq = wv; hq < hpg; hq += 4) {
-          const float v = lrow[(size_t)(uint32_t)(pj * hpg + hq) * (uint32_t)mb.g.m];
-          lse_s[tl * LS + b * 16 + hq] = v;
+      for (int b = 0; b < NBR; ++b) {
+        if (b < nbr) {
+          const MergeBranch& mb = a.br[b];
+          const int pn = (int)div_magic((uint32_t)p, mb.dg);
+          const int pt = p - pn * mb.g.g;
+          const int pi = (int)div_magic((uint32_t)pt, mb.dr);
+          const int pj = pt - pi * mb.g.r;
+          const int hpg = mb.g.hpg;
+          const uint32_t rb = (uint32_t)(bidx * mb.g.nseg + pn);
+          const float* lrow = mb.lse + (size_t)rb * (uint32_t)(H * mb.g.m) + (uint32_t)pi;
+          for (int hq = wv; hq < hpg; hq += 4) {
+            const float v = lrow[(size_t)(uint32_t)(pj * hpg + hq) * (uint32_t)mb.g.m];
+            lse_s[tl * LS + b * 16 + hq] = v;
+          }
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int pass = 0; pass < (kTab ? 2 : 1); ++pass) {
+      int s_lo = 0, s_hi = total;
+      MergeBranch tb[kTab ? NBR : 1];
+      if constexpr (kTab) {
+        const int sl = slide0 + pass;
+        if (sl >= a.nslide) break;
+        s_lo = (int)a.tok_off[sl];
+        s_hi = (int)a.tok_off[sl + 1];
+#pragma unroll
+        for (int b = 0; b < NBR; ++b)
+          if (b < nbr) tb[b] = a.mtab[sl * a.nbranch + b];
+      }
+      const int tl = lane;
+      const int row = row0 + tl;
+      if (tl < tpb && row < total && row >= s_lo && row < s_hi) {
+        int bidx = 0, p;
+        if constexpr (kTab) {
+          p = row - s_lo;
+        } else {
+          bidx = (int)div_magic((uint32_t)row, a.dnt);
+          p = (int)a.tok_lo + (row - bidx * (int)a.ntok);
+        }
+#pragma unroll
+        for (int b = 0; b < NBR; ++b) {
+          if (b < nbr) {
+            const MergeBranch& mb = kTab ? tb[b] : a.br[b];
+            const int pn = (int)div_magic((uint32_t)p, mb.dg);
+            const int pt = p - pn * mb.g.g;
+            const int pi = (int)div_magic((uint32_t)pt, mb.dr);
+            const int pj = pt - pi * mb.g.r;
+            const int hpg = mb.g.hpg;
+            const uint32_t rb = (uint32_t)(bidx * mb.g.nseg + pn);
+            const float* lrow = mb.lse + (size_t)rb * (uint32_t)(H * mb.g.m) + (uint32_t)pi;
+            for (int hq = wv; hq < hpg; hq += 4) {
+              const float v = lrow[(size_t)(uint32_t)(pj * hpg + hq) * (uint32_t)mb.g.m];
+              lse_s[tl * LS + b * 16 + hq] = v;
+            }
+          }
         }
       }
     }
@@ -1536,12 +1616,37 @@ __global__ __launch_bounds__(256) void branch_merge_v3_kernel(const MergeArgs a,
   load_f32<4>(lw + c1, w1);
   load_f32<8>(lb + c0, b0);
   load_f32<4>(lb + c1, b1);
+  // kTab: the first slide's entries, loaded once for the wave's tokens (its tokens ascend, so a crossing into
+  // the next slide happens at most once)
+  MergeBranch tb[kTab ? NBR : 1];
+  int t_sl = 0, t_base = 0, t_bnd = INT_MAX;
+  if constexpr (kTab) {
+    t_sl = slide0;
+    t_base = (int)a.tok_off[slide0];
+    t_bnd = slide0 + 1 < a.nslide ? (int)a.tok_off[slide0 + 1] : INT_MAX;
+#pragma unroll
+    for (int b = 0; b < NBR; ++b)
+      if (b < nbr) tb[b] = merge_entry_scalar(a.mtab, slide0 * a.nbranch + b);
+  }
   for (int k = 0; k < kV3Tok / 4; ++k) {
     const int t = wv + 4 * k;
     const int row = row0 + t;
     if (t >= tpb || row >= total) break;
-    const int bidx = (int)div_magic((uint32_t)row, a.dnt);
-    const int p = (int)a.tok_lo + (row - bidx * (int)a.ntok);
+    int bidx = 0, p;
+    if constexpr (kTab) {
+      if (row >= t_bnd) {                    // this wave's tokens crossed into the next slide (rare): switch tables
+        t_sl += 1;
+        t_base = t_bnd;
+        t_bnd = t_sl + 1 < a.nslide ? (int)a.tok_off[t_sl + 1] : INT_MAX;
+#pragma unroll
+        for (int b = 0; b < NBR; ++b)
+          if (b < nbr) tb[b] = merge_entry_scalar(a.mtab, t_sl * a.nbranch + b);
+      }
+      p = row - t_base;
+    } else {
+      bidx = (int)div_magic((uint32_t)row, a.dnt);
+      p = (int)a.tok_lo + (row - bidx * (int)a.ntok);
+    }
     uint4 o0[NBR];
     uint2 o1[NBR];
     float l0[NBR], l1[NBR];
@@ -1553,7 +1658,7 @@ __global__ __launch_bounds__(256) void branch_merge_v3_kernel(const MergeArgs a,
       o0[b] = make_uint4(0, 0, 0, 0);
       o1[b] = make_uint2(0, 0);
       if (b < nbr) {
-        const MergeBranch& mb = a.br[b];
+        const MergeBranch& mb = kTab ? tb[b] : a.br[b];
         const int pn = (int)div_magic((uint32_t)p, mb.dg);
         const int pt = p - pn * mb.g.g;
         const int pi = (int)div_magic((uint32_t)pt, mb.dr);
@@ -2222,6 +2327,22 @@ extern "C" int gp_branch_merge_ln_varlen(const void* plan_host, const void* plan
   // are at most 2 L_i, below 4 GiB for any slide the 1000 x 1000 position grid admits)
   const unsigned nb = merge_v2_grid(h.T);
   hipStream_t s = gp_stream(stream);
+  if constexpr (GP_MERGE_V3_TAB != 0 && GP_MERGE_V3 != 0) if (h.nbranch == 5) {
+    // the v3 merge over the packed tokens when every slide holds at least a block's tokens (a block then meets at
+    // most two slides); tokens per block as the single-slide launch
+    const int64_t* toh = reinterpret_cast<const int64_t*>(static_cast<const char*>(plan_host) + h.tok_off_off);
+    int64_t shortest = INT64_MAX;
+    for (int i = 0; i < h.nslide; ++i) shortest = std::min<int64_t>(shortest, toh[i + 1] - toh[i]);
+    const int64_t ncu = attn_num_cus(s);
+    const int64_t per_cu = (h.T + ncu * kV3Tok - 1) / (ncu * kV3Tok);
+    const int tpb = (int)std::max<int64_t>(1, (h.T + ncu * per_cu - 1) / (ncu * per_cu));
+    if (shortest >= tpb) {
+      const unsigned g = (unsigned)((h.T + tpb - 1) / tpb);
+      if (fmt == GP_FMT_F16) branch_merge_v3_kernel<5, true, true><<<g, 256, 0, s>>>(a, tpb);
+      else branch_merge_v3_kernel<5, false, true><<<g, 256, 0, s>>>(a, tpb);
+      return gp_check_launch("gp_branch_merge_ln_varlen");
+    }
+  }
   if (h.nbranch == 5) {   // every registered arch's schedule: compile-time branch loops
     if (fmt == GP_FMT_F16) branch_merge_v2_kernel<5, true, true><<<nb, 64 * GP_MERGE_WPB, 0, s>>>(a);
     else branch_merge_v2_kernel<5, true, false><<<nb, 64 * GP_MERGE_WPB, 0, s>>>(a);
